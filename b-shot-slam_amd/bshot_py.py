@@ -1,0 +1,354 @@
+"""ctypes binding of libbshot_amd.so (the C ABI in include/bshot_abi.h) for tests and bench.py.
+
+This is a thin host-side mirror of the reference's LidarOdometry frame loop
+(test/odometry_test.cpp:159-194) over the C ABI; every compute call runs the gfx950 kernels.
+The product never falls back to CPU: a missing library or GPU raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libbshot_amd.so")
+SYNTH_PATH = os.path.join(HERE, "lib", "libbshot_synth.so")
+P = ctypes.c_void_p
+
+NSTAGES = 10
+STAGE_NAMES = ["grid", "seg_ratio", "iss", "normals", "shot_gather", "shot_sort", "lrf", "shot_hist", "match", "icp"]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("seg_radius", ctypes.c_float), ("seg_max_nn", ctypes.c_int), ("sr_type", ctypes.c_int),
+        ("num_keypoints", ctypes.c_int), ("iss_salient", ctypes.c_float), ("iss_nonmax", ctypes.c_float),
+        ("iss_gamma21", ctypes.c_double), ("iss_gamma32", ctypes.c_double), ("iss_min_nn", ctypes.c_int),
+        ("normal_radius", ctypes.c_float), ("normal_max_nn", ctypes.c_int), ("shot_radius", ctypes.c_float),
+        ("map_range", ctypes.c_float), ("ransac_max_iter", ctypes.c_int), ("ransac_thresh", ctypes.c_double),
+        ("icp_max_iter", ctypes.c_int), ("run_icp", ctypes.c_int), ("run_iss", ctypes.c_int),
+    ]
+
+
+class FrameStats(ctypes.Structure):
+    _fields_ = [
+        ("n_points", ctypes.c_int), ("n_valid_ratios", ctypes.c_int), ("n_keypoints", ctypes.c_int),
+        ("n_iss", ctypes.c_int), ("n_target", ctypes.c_int), ("n_mutual", ctypes.c_int),
+        ("n_inliers", ctypes.c_int), ("icp_iters", ctypes.c_int), ("gated", ctypes.c_int),
+        ("h_diff", ctypes.c_float), ("t_diff", ctypes.c_float), ("T_ransac", ctypes.c_float * 16),
+        ("pose", ctypes.c_float * 16), ("map_size", ctypes.c_int), ("repeat_sr", ctypes.c_float),
+        ("repeat_iss", ctypes.c_float),
+    ]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("T_ransac", "pose")}
+        d["T_ransac"] = np.array(self.T_ransac, np.float32).reshape(4, 4)
+        d["pose"] = np.array(self.pose, np.float32).reshape(4, 4)
+        return d
+
+
+ABI_SYMBOLS = [
+    "bshot_default_params", "bshot_create", "bshot_destroy", "bshot_last_error", "bshot_sync", "bshot_stream",
+    "bshot_set_cloud", "bshot_set_cloud_device", "bshot_seg_ratio", "bshot_select_topk", "bshot_iss",
+    "bshot_describe", "bshot_get_normals", "bshot_match", "bshot_ransac", "bshot_icp", "bshot_odom_create",
+    "bshot_odom_destroy", "bshot_odom_last_error", "bshot_odom_process", "bshot_odom_process_device",
+    "bshot_odom_get_keypoints", "bshot_odom_get_ratios", "bshot_odom_get_bits", "bshot_odom_get_target",
+    "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
+    "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
+    "bshot_set_timing", "bshot_work_counters",
+]
+
+_lib = None
+_synth = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libbshot_amd.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.bshot_last_error.restype = ctypes.c_char_p
+        _lib.bshot_odom_last_error.restype = ctypes.c_char_p
+        _lib.bshot_stream.restype = P
+        _lib.bshot_odom_ctx.restype = P
+    return _lib
+
+
+def default_params(**kw):
+    p = Params()
+    lib().bshot_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _f32(a, cols=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P)
+
+
+class BshotError(RuntimeError):
+    pass
+
+
+class Context:
+    """One GPU, one HIP stream (bshot_ctx)."""
+
+    def __init__(self, device=0, params=None):
+        self.L = lib()
+        self.h = P()
+        self.params = params if params is not None else default_params()
+        rc = self.L.bshot_create(ctypes.byref(self.h), device, ctypes.byref(self.params))
+        if rc != 0:
+            raise BshotError(f"bshot_create failed ({rc}): no usable GPU?")
+
+    def _chk(self, rc, what):
+        if rc < 0:
+            raise BshotError(f"{what}: {self.L.bshot_last_error(self.h).decode()} ({rc})")
+        return rc
+
+    def close(self):
+        if self.h:
+            self.L.bshot_destroy(self.h)
+            self.h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_cloud(self, xyz):
+        xyz = _f32(xyz).reshape(-1, 3)
+        self._xyz = xyz
+        self.n = len(xyz)
+        self._chk(self.L.bshot_set_cloud(self.h, _ptr(xyz), self.n), "set_cloud")
+
+    def set_cloud_device(self, dptr, n):
+        self.n = n
+        self._chk(self.L.bshot_set_cloud_device(self.h, P(dptr), n), "set_cloud_device")
+
+    def seg_ratio(self):
+        idx = np.zeros(max(self.n, 1), np.int32)
+        rat = np.zeros(max(self.n, 1), np.float32)
+        m = ctypes.c_int()
+        self._chk(self.L.bshot_seg_ratio(self.h, _ptr(idx), _ptr(rat), ctypes.byref(m)), "seg_ratio")
+        return idx[: m.value].copy(), rat[: m.value].copy()
+
+    def iss(self):
+        out = np.zeros(max(self.n, 1), np.int32)
+        m = ctypes.c_int()
+        self._chk(self.L.bshot_iss(self.h, _ptr(out), len(out), ctypes.byref(m)), "iss")
+        return out[: m.value].copy()
+
+    def describe(self, kps, want_shot=True):
+        kps = _f32(kps).reshape(-1, 3)
+        k = len(kps)
+        bits = np.zeros((max(k, 1), 11), np.uint32)
+        shot = np.zeros((max(k, 1), 352), np.float32) if want_shot else None
+        rf = np.zeros((max(k, 1), 9), np.float32) if want_shot else None
+        self._chk(self.L.bshot_describe(self.h, _ptr(kps), k, _ptr(shot) if want_shot else None,
+                                        _ptr(rf) if want_shot else None, _ptr(bits)), "describe")
+        if want_shot:
+            return bits[:k], shot[:k], rf[:k]
+        return bits[:k]
+
+    def normals(self, n):
+        out = np.zeros((max(n, 1), 4), np.float32)
+        self._chk(self.L.bshot_get_normals(self.h, _ptr(out), n), "get_normals")
+        return out[:n]
+
+    def match(self, a, b):
+        a = np.ascontiguousarray(a, np.uint32).reshape(-1, 11)
+        b = np.ascontiguousarray(b, np.uint32).reshape(-1, 11)
+        na, nb = len(a), len(b)
+        left = np.zeros(max(na, 1), np.int32)
+        right = np.zeros(max(nb, 1), np.int32)
+        cq = np.zeros(max(na, 1), np.int32)
+        cm = np.zeros(max(na, 1), np.int32)
+        nc = ctypes.c_int()
+        self._chk(self.L.bshot_match(self.h, _ptr(a), na, _ptr(b), nb, _ptr(left), _ptr(right), _ptr(cq), _ptr(cm),
+                                     ctypes.byref(nc)), "match")
+        return left[:na], right[:nb], cq[: nc.value], cm[: nc.value]
+
+    def icp(self, src, tgt, max_iter=10):
+        src = _f32(src).reshape(-1, 3)
+        tgt = _f32(tgt).reshape(-1, 3)
+        T = np.zeros(16, np.float32)
+        it = ctypes.c_int()
+        self._chk(self.L.bshot_icp(self.h, _ptr(src), len(src), _ptr(tgt), len(tgt), max_iter, _ptr(T),
+                                   ctypes.byref(it)), "icp")
+        return T.reshape(4, 4), it.value
+
+    def set_timing(self, on):
+        self.L.bshot_set_timing(self.h, 1 if on else 0)
+
+    def stage_times(self):
+        ms = (ctypes.c_double * NSTAGES)()
+        nl = (ctypes.c_int64 * NSTAGES)()
+        self.L.bshot_stage_times(self.h, ms, nl, NSTAGES)
+        return {STAGE_NAMES[i]: (ms[i], nl[i]) for i in range(NSTAGES)}
+
+    def stage_reset(self):
+        self.L.bshot_stage_reset(self.h)
+
+    def work(self):
+        w = (ctypes.c_int64 * 8)()
+        self.L.bshot_work_counters(self.h, w, 8)
+        return list(w)
+
+    def sync(self):
+        self._chk(self.L.bshot_sync(self.h), "sync")
+
+
+def select_topk(idx, ratio, k):
+    idx = np.ascontiguousarray(idx, np.int32)
+    ratio = np.ascontiguousarray(ratio, np.float32)
+    o = np.zeros(max(k, 1), np.int32)
+    r = np.zeros(max(k, 1), np.float32)
+    m = ctypes.c_int()
+    rc = lib().bshot_select_topk(_ptr(idx), _ptr(ratio), len(idx), k, _ptr(o), _ptr(r), ctypes.byref(m))
+    if rc < 0:
+        raise BshotError("select_topk failed")
+    return o[: m.value].copy(), r[: m.value].copy()
+
+
+def ransac(src, tgt, cq, cm, max_iter=2000, thresh=1500.0):
+    src = _f32(src).reshape(-1, 3)
+    tgt = _f32(tgt).reshape(-1, 3)
+    cq = np.ascontiguousarray(cq, np.int32)
+    cm = np.ascontiguousarray(cm, np.int32)
+    T = np.zeros(16, np.float32)
+    iq = np.zeros(max(len(cq), 1), np.int32)
+    im = np.zeros(max(len(cq), 1), np.int32)
+    ni = ctypes.c_int()
+    rc = lib().bshot_ransac(_ptr(src), len(src), _ptr(tgt), len(tgt), _ptr(cq), _ptr(cm), len(cq), max_iter,
+                            ctypes.c_double(thresh), _ptr(T), _ptr(iq), _ptr(im), ctypes.byref(ni))
+    if rc < 0:
+        raise BshotError("ransac failed")
+    return rc, T.reshape(4, 4), iq[: ni.value].copy(), im[: ni.value].copy()
+
+
+class Odometry:
+    """Headless odometry_test loop (bshot_odom)."""
+
+    def __init__(self, device=0, params=None):
+        self.L = lib()
+        self.h = P()
+        self.params = params if params is not None else default_params()
+        rc = self.L.bshot_odom_create(ctypes.byref(self.h), device, ctypes.byref(self.params))
+        if rc != 0:
+            raise BshotError(f"bshot_odom_create failed ({rc})")
+
+    def close(self):
+        if self.h:
+            self.L.bshot_odom_destroy(self.h)
+            self.h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc < 0:
+            raise BshotError(f"{what}: {self.L.bshot_odom_last_error(self.h).decode()} ({rc})")
+        return rc
+
+    def process(self, xyz):
+        xyz = _f32(xyz).reshape(-1, 3)
+        st = FrameStats()
+        self._chk(self.L.bshot_odom_process(self.h, _ptr(xyz), len(xyz), ctypes.byref(st)), "odom_process")
+        return st
+
+    def process_device(self, dptr, n):
+        st = FrameStats()
+        self._chk(self.L.bshot_odom_process_device(self.h, P(dptr), n, ctypes.byref(st)), "odom_process_device")
+        return st
+
+    def _get(self, fn, shape_cols, dtype, cap=1 << 20):
+        buf = np.zeros((cap, shape_cols), dtype)
+        n = fn(self.h, _ptr(buf), cap)
+        if n < 0:
+            return self._get(fn, shape_cols, dtype, -n)
+        return buf[:n].copy()
+
+    def keypoints(self):
+        return self._get(self.L.bshot_odom_get_keypoints, 3, np.float32)
+
+    def ratios(self):
+        return self._get(self.L.bshot_odom_get_ratios, 1, np.float32)[:, 0]
+
+    def bits(self):
+        return self._get(self.L.bshot_odom_get_bits, 11, np.uint32)
+
+    def iss(self):
+        return self._get(self.L.bshot_odom_get_iss, 3, np.float32)
+
+    def target(self, cap=1 << 20):
+        xyz = np.zeros((cap, 3), np.float32)
+        bits = np.zeros((cap, 11), np.uint32)
+        n = self.L.bshot_odom_get_target(self.h, _ptr(xyz), _ptr(bits), cap)
+        if n < 0:
+            return self.target(-n)
+        return xyz[:n].copy(), bits[:n].copy()
+
+    def inliers(self, cap=1 << 16):
+        q = np.zeros(cap, np.int32)
+        m = np.zeros(cap, np.int32)
+        n = self.L.bshot_odom_get_inliers(self.h, _ptr(q), _ptr(m), cap)
+        if n < 0:
+            return self.inliers(-n)
+        return q[:n].copy(), m[:n].copy()
+
+    def map_delta(self, cap=1 << 16):
+        rec = np.zeros((cap, 15), np.float32)
+        n = self.L.bshot_odom_map_delta(self.h, _ptr(rec), cap)
+        if n < 0:
+            return self.map_delta(-n)
+        return rec[:n].copy()
+
+    def replica_insert(self, replica, rec):
+        rec = np.ascontiguousarray(rec, np.float32).reshape(-1, 15)
+        self._chk(self.L.bshot_odom_replica_insert(self.h, replica, _ptr(rec), len(rec)), "replica_insert")
+
+    def replica_size(self, replica):
+        return self.L.bshot_odom_replica_size(self.h, replica)
+
+    def context(self):
+        return self.L.bshot_odom_ctx(self.h)
+
+    def stage_times(self):
+        ms = (ctypes.c_double * NSTAGES)()
+        nl = (ctypes.c_int64 * NSTAGES)()
+        self.L.bshot_stage_times(P(self.context()), ms, nl, NSTAGES)
+        return {STAGE_NAMES[i]: (ms[i], nl[i]) for i in range(NSTAGES)}
+
+    def set_timing(self, on):
+        self.L.bshot_set_timing(P(self.context()), 1 if on else 0)
+
+    def stage_reset(self):
+        self.L.bshot_stage_reset(P(self.context()))
+
+
+# ---------------------------------------------------------------- synthetic input (not the product)
+def synth_sweep(frame, sensor=0, seed=42, no_ground=False, max_range=120000.0):
+    """Deterministic synthetic Velodyne sweep (b-shot-slam_amd/tools/synth.cpp), sensor frame, mm."""
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise RuntimeError(f"{SYNTH_PATH} not built")
+        _synth = ctypes.CDLL(SYNTH_PATH)
+    cap = 300000
+    buf = np.zeros((cap, 3), np.float32)
+    pose = np.zeros(16, np.float32)
+    n = _synth.synth_sweep(sensor, seed, frame, 1 if no_ground else 0, ctypes.c_float(max_range), _ptr(buf), cap,
+                           _ptr(pose))
+    if n < 0:
+        raise RuntimeError("synth capacity")
+    return buf[:n].copy(), pose.reshape(4, 4)

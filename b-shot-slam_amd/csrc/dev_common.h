@@ -1,0 +1,106 @@
+// dev_common.h -- device-side building blocks for the gfx950 kernels of libbshot_amd.
+//
+// HBM layout of one hashed voxel grid (DESIGN.md "Data layout"):
+//   pts4[N]     float4 (x, y, z, bits(idx)) in original index order
+//   spts[N]     float4 (x, y, z, bits(idx)) sorted by (cell key, idx): every cell is one
+//               contiguous, 16-B aligned run, so a wave streams a cell with coalesced dwordx4 loads
+//   table[H]    open-addressed hash (H = pow2 >= 2 * #points): {u64 key, u32 start, u32 count}
+// Cell key = 21-bit biased (ix, iy, iz) packed into a u64; empty slot = ~0.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BS_WAVE 64
+#define BS_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
+
+struct CellEntry {
+    unsigned long long key;
+    unsigned int start;
+    unsigned int count;
+};
+
+struct GridView {
+    const float4* spts;       // cell-sorted points
+    const CellEntry* table;   // hash table
+    unsigned int mask;        // H - 1
+    float cell;               // cell edge (mm)
+    float inv_cell;           // 1 / cell (only used for speed-insensitive cell ranges, see cell_of)
+};
+
+__device__ __forceinline__ unsigned long long cell_key(int ix, int iy, int iz) {
+    return ((unsigned long long)(unsigned)(ix + (1 << 20)) << 42) | ((unsigned long long)(unsigned)(iy + (1 << 20)) << 21) |
+           (unsigned long long)(unsigned)(iz + (1 << 20));
+}
+
+__device__ __forceinline__ unsigned int hash_key(unsigned long long k) {
+    k ^= k >> 29;
+    k *= 0xBF58476D1CE4E5B9ull;
+    k ^= k >> 32;
+    return (unsigned int)k;
+}
+
+// cell coordinate of a coordinate value: floor(x / cell) computed in double (matches the grid build)
+__device__ __forceinline__ int cell_of(float x, float cell) { return (int)floor((double)x / (double)cell); }
+
+__device__ __forceinline__ bool grid_lookup(const GridView& g, unsigned long long key, unsigned int& start,
+                                            unsigned int& count) {
+    unsigned int h = hash_key(key) & g.mask;
+    for (unsigned int probe = 0; probe <= g.mask; ++probe) {
+        const unsigned long long k = g.table[h].key;
+        if (k == key) {
+            start = g.table[h].start;
+            count = g.table[h].count;
+            return true;
+        }
+        if (k == BS_EMPTY_KEY) return false;
+        h = (h + 1) & g.mask;
+    }
+    return false;
+}
+
+// FLANN L2_Simple squared distance in float: ((dx*dx + dy*dy) + dz*dz), dx = q - p (no FMA:
+// the library is built with -ffp-contract=off).
+__device__ __forceinline__ float d2_flann(float qx, float qy, float qz, float px, float py, float pz) {
+    const float dx = qx - px, dy = qy - py, dz = qz - pz;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// wave-wide exclusive prefix sum of an int (64 lanes)
+__device__ __forceinline__ int wave_excl_scan(int v, int& total) {
+    const int lane = lane_id();
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// pairwise butterfly sum with a FIXED tree (lane 0's association: partner = lane ^ off,
+// off = 32, 16, ..., 1). Documented convention for the LRF covariance.
+__device__ __forceinline__ double wave_tree_sum_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ unsigned int f2u(float f) { return __float_as_uint(f); }

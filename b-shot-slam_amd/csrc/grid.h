@@ -1,0 +1,37 @@
+// grid.h -- host-side handle of one hashed voxel grid (device buffers, grow-only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev_common.h"
+
+namespace bsh {
+
+struct DevGrid {
+    int cap = 0, n = 0;
+    unsigned int H = 0;
+    float cell = 0.f;
+    unsigned long long *keys = nullptr, *keys2 = nullptr;
+    unsigned int *vals = nullptr, *vals2 = nullptr;
+    float4* spts = nullptr;
+    CellEntry* table = nullptr;
+    int* ncells = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+
+    GridView view() const {
+        GridView v;
+        v.spts = spts;
+        v.table = table;
+        v.mask = H - 1;
+        v.cell = cell;
+        v.inv_cell = 1.0f / cell;
+        return v;
+    }
+};
+
+// Builds the grid of d_xyz (N x 3 floats, device) with edge `cell`; writes float4 copies of the
+// points in index order to d_pts4 (N entries).
+hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s);
+void grid_free(DevGrid& g);
+
+}  // namespace bsh

@@ -1,0 +1,121 @@
+// grid.hip -- hashed voxel grid build on gfx950 (the "hashed-voxel radius-neighbour search" of
+// BASELINE.json north_star). Replaces pcl::KdTreeFLANN::setInputCloud
+// (src/lidar_odometry.cpp:53-54, include/bshot_bits.h:52-53) with a counting structure that every
+// radius query kernel streams with coalesced float4 loads.
+//
+// Build: keys -> rocprim radix sort of (cell key, idx) -> cell-start detection (binary search for
+// the run end) + hash insert -> scatter float4 points into cell order. All O(N), no host sync.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "dev_common.h"
+#include "grid.h"
+
+namespace bsk {
+
+__global__ void k_grid_keys(const float* __restrict__ xyz, int n, float cell, unsigned long long* __restrict__ keys,
+                            unsigned int* __restrict__ vals, float4* __restrict__ pts4) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    pts4[i] = make_float4(x, y, z, __uint_as_float((unsigned)i));
+    unsigned long long k = BS_EMPTY_KEY;
+    if (__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z)) {
+        const int ix = cell_of(x, cell), iy = cell_of(y, cell), iz = cell_of(z, cell);
+        if (ix > -(1 << 20) && ix < (1 << 20) && iy > -(1 << 20) && iy < (1 << 20) && iz > -(1 << 20) && iz < (1 << 20))
+            k = cell_key(ix, iy, iz);
+    }
+    keys[i] = k;
+    vals[i] = (unsigned)i;
+}
+
+__global__ void k_grid_clear(CellEntry* __restrict__ table, unsigned int H) {
+    const unsigned int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < H) {
+        table[i].key = BS_EMPTY_KEY;
+        table[i].start = 0;
+        table[i].count = 0;
+    }
+}
+
+__global__ void k_grid_cells(const unsigned long long* __restrict__ keys, const unsigned int* __restrict__ vals,
+                             const float4* __restrict__ pts4, int n, CellEntry* __restrict__ table, unsigned int mask,
+                             float4* __restrict__ spts, int* __restrict__ ncells) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    spts[j] = pts4[vals[j]];
+    const unsigned long long k = keys[j];
+    if (k == BS_EMPTY_KEY) return;
+    if (j > 0 && keys[j - 1] == k) return;
+    // run end: first position > j whose key differs (keys sorted ascending)
+    int lo = j + 1, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] == k) lo = mid + 1;
+        else hi = mid;
+    }
+    unsigned int h = hash_key(k) & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&table[h].key, BS_EMPTY_KEY, k);
+        if (prev == BS_EMPTY_KEY) break;
+        h = (h + 1) & mask;
+    }
+    table[h].start = (unsigned)j;
+    table[h].count = (unsigned)(lo - j);
+    atomicAdd(ncells, 1);
+}
+
+}  // namespace bsk
+
+// host side --------------------------------------------------------------------------------
+namespace bsh {
+
+static unsigned int pow2_at_least(unsigned int x) {
+    unsigned int p = 1024;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s) {
+    hipError_t e;
+    if (n > g.cap) {
+        grid_free(g);
+        g.cap = n + n / 4 + 1024;
+        if ((e = hipMalloc(&g.keys, sizeof(unsigned long long) * g.cap))) return e;
+        if ((e = hipMalloc(&g.keys2, sizeof(unsigned long long) * g.cap))) return e;
+        if ((e = hipMalloc(&g.vals, sizeof(unsigned int) * g.cap))) return e;
+        if ((e = hipMalloc(&g.vals2, sizeof(unsigned int) * g.cap))) return e;
+        if ((e = hipMalloc(&g.spts, sizeof(float4) * g.cap))) return e;
+        g.H = pow2_at_least(2u * (unsigned)g.cap);
+        if ((e = hipMalloc(&g.table, sizeof(CellEntry) * g.H))) return e;
+        if ((e = hipMalloc(&g.ncells, sizeof(int)))) return e;
+        size_t tb = 0;
+        if ((e = rocprim::radix_sort_pairs(nullptr, tb, g.keys, g.keys2, g.vals, g.vals2, (unsigned)g.cap, 0, 64, s))) return e;
+        g.tmp_bytes = tb;
+        if ((e = hipMalloc(&g.tmp, tb))) return e;
+    }
+    g.n = n;
+    g.cell = cell;
+    const int B = 256;
+    bsk::k_grid_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, cell, g.keys, g.vals, d_pts4);
+    size_t tb = g.tmp_bytes;
+    if ((e = rocprim::radix_sort_pairs(g.tmp, tb, g.keys, g.keys2, g.vals, g.vals2, (unsigned)n, 0, 64, s))) return e;
+    bsk::k_grid_clear<<<(g.H + B - 1) / B, B, 0, s>>>(g.table, g.H);
+    if ((e = hipMemsetAsync(g.ncells, 0, sizeof(int), s))) return e;
+    bsk::k_grid_cells<<<(n + B - 1) / B, B, 0, s>>>(g.keys2, g.vals2, d_pts4, n, g.table, g.H - 1, g.spts, g.ncells);
+    return hipGetLastError();
+}
+
+void grid_free(DevGrid& g) {
+    if (g.keys) (void)hipFree(g.keys);
+    if (g.keys2) (void)hipFree(g.keys2);
+    if (g.vals) (void)hipFree(g.vals);
+    if (g.vals2) (void)hipFree(g.vals2);
+    if (g.spts) (void)hipFree(g.spts);
+    if (g.table) (void)hipFree(g.table);
+    if (g.ncells) (void)hipFree(g.ncells);
+    if (g.tmp) (void)hipFree(g.tmp);
+    g = DevGrid();
+}
+
+}  // namespace bsh

@@ -1,0 +1,384 @@
+// knn.hip -- exact radius-capped k-NN on the hashed grid + the two kernels built on it:
+//   * k_seg_ratio : A1, segmentation ratio of every point (src/lidar_odometry.cpp:53-126)
+//   * k_normals   : A4, keypoint normals (include/bshot_bits.h:43-94, pcl::computePointNormal)
+//
+// Selection semantics (FLANN KNNRadiusResultSet, sorted): the max_nn smallest (d2, idx) with
+// d2 < r2, in ascending (d2, idx) order. One wavefront per query:
+//   1. radius ladder rs in {r/4, r/2, r}: LDS histogram of d2 over [0, rs^2); stop at the first rs
+//      with >= max_nn hits (then every one of the max_nn nearest lies inside rs) -- exact;
+//   2. histogram refinement (<= 3 levels of 512 buckets) until the boundary bucket fits;
+//   3. collect the prefix into LDS (<= 1024 u64 keys (d2bits<<32 | idx)), bitonic sort;
+//   4. ordered float reductions in rank order exactly as PCL (computeCentroid, covariance).
+// Candidates are streamed cell by cell: 64 cells per round are looked up (one per lane), a wave
+// prefix sum flattens their runs, lanes read consecutive float4s of each run (coalesced).
+#include <hip/hip_runtime.h>
+
+#include "bshot_math.h"
+#include "dev_cand.h"
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace bsk {
+
+#define KNN_NB 512
+#define KNN_CAP 1024
+#define KNN_WAVES 2
+
+struct KnnLds {
+    unsigned int hist[KNN_NB];
+    unsigned long long list[KNN_CAP];
+    unsigned int cstart[64];
+    int coff[64];
+};
+
+__device__ __forceinline__ int bucket_of(float d2, float lo, float sc) {
+    float v = (d2 - lo) * sc;
+    int b = (int)v;
+    if (!(v >= 0.f)) b = 0;
+    if (b > KNN_NB - 1) b = KNN_NB - 1;
+    return b;
+}
+
+// wave: find bucket B where the cumulative count crosses `need` (1-based); returns B and the
+// count strictly below B in *below.
+__device__ __forceinline__ int hist_cross(KnnLds* L, int need, int* below) {
+    const int lane = lane_id();
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < KNN_NB / 64; ++j) s += (int)L->hist[lane * (KNN_NB / 64) + j];
+    int tot;
+    const int ex = wave_excl_scan(s, tot);
+    // lane whose range contains the crossing
+    const bool mine = ex < need && ex + s >= need;
+    const unsigned long long m = __ballot(mine);
+    const int owner = m ? (int)__ffsll((long long)m) - 1 : 63;
+    int B = 0, bl = 0;
+    if (lane == owner) {
+        int acc = ex;
+        B = lane * (KNN_NB / 64);
+        for (int j = 0; j < KNN_NB / 64; ++j) {
+            const int h = (int)L->hist[lane * (KNN_NB / 64) + j];
+            if (acc + h >= need) { B = lane * (KNN_NB / 64) + j; break; }
+            acc += h;
+        }
+        bl = acc;
+    }
+    B = __shfl(B, owner, 64);
+    *below = __shfl(bl, owner, 64);
+    return B;
+}
+
+__device__ __forceinline__ void hist_clear(KnnLds* L) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < KNN_NB / 64; ++j) L->hist[lane + 64 * j] = 0;
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Exact selection: leaves the `*need` nearest (d2, idx) sorted in L->list[0, *need).
+// Returns false when the neighbourhood is pathological (> KNN_CAP exactly tied keys at the
+// boundary after 3 refinement levels) -- reported through the error word.
+__device__ bool knn_select(const GridView& g, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
+                           int* need_out) {
+    const int lane = lane_id();
+    const float r2 = (float)((double)r * (double)r);
+    float rs = r * 0.25f, rs2 = r2;
+    int total = 0;
+    for (int step = 0; step < 3; ++step) {
+        rs = step == 0 ? r * 0.25f : (step == 1 ? r * 0.5f : r);
+        rs2 = step == 2 ? r2 : (float)((double)rs * (double)rs);
+        hist_clear(L);
+        const float sc = (float)KNN_NB / rs2;
+        for_candidates(g, L->cstart, L->coff, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+            if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
+        });
+        __builtin_amdgcn_wave_barrier();
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < KNN_NB / 64; ++j) s += (int)L->hist[lane + 64 * j];
+        total = wave_sum_i(s);
+        if (total >= max_nn) break;
+    }
+    const int need = total < max_nn ? total : max_nn;
+    *need_out = need;
+    if (need == 0) return true;
+    // bucket path bound: collect candidates with path <= (B[0..lev-1]) lexicographically
+    int B[3] = {KNN_NB, KNN_NB, KNN_NB};
+    float lo[3] = {0.f, 0.f, 0.f}, sc[3] = {(float)KNN_NB / rs2, 0.f, 0.f};
+    int levels = 0;
+    int count_le = total;  // number of candidates the collect pass will take
+    if (total > KNN_CAP) {
+        int below_acc = 0;
+        float w = rs2;
+        for (int lev = 0; lev < 3; ++lev) {
+            if (lev > 0) {
+                hist_clear(L);
+                const int lv = lev;
+                for_candidates(g, L->cstart, L->coff, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+                    if (!v) return;
+                    int b = bucket_of(d2, lo[0], sc[0]);
+                    if (b != B[0]) return;
+                    b = bucket_of(d2, lo[1], sc[1]);
+                    if (lv == 1) { atomicAdd(&L->hist[b], 1u); return; }
+                    if (b != B[1]) return;
+                    atomicAdd(&L->hist[bucket_of(d2, lo[2], sc[2])], 1u);
+                });
+                __builtin_amdgcn_wave_barrier();
+            }
+            int below;
+            const int Bl = hist_cross(L, need - below_acc, &below);
+            B[lev] = Bl;
+            levels = lev + 1;
+            const int inb = (int)L->hist[Bl];
+            below_acc += below;
+            count_le = below_acc + inb;
+            if (count_le <= KNN_CAP) break;
+            if (lev == 2) return false;
+            // next level range inside bucket Bl
+            const float wb = w / (float)KNN_NB;
+            lo[lev + 1] = lo[lev] + (float)Bl * wb;
+            sc[lev + 1] = (float)KNN_NB / wb;
+            w = wb;
+        }
+    }
+    // collect pass
+    int cnt = 0;
+    const int lv = levels;
+    for_candidates(g, L->cstart, L->coff, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        bool take = v;
+        if (take && lv > 0) {
+            const int b0 = bucket_of(d2, lo[0], sc[0]);
+            if (b0 > B[0]) take = false;
+            else if (b0 == B[0] && lv > 1) {
+                const int b1 = bucket_of(d2, lo[1], sc[1]);
+                if (b1 > B[1]) take = false;
+                else if (b1 == B[1] && lv > 2) {
+                    if (bucket_of(d2, lo[2], sc[2]) > B[2]) take = false;
+                }
+            }
+        }
+        const unsigned long long m = __ballot(take);
+        if (take) {
+            const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            if (slot < KNN_CAP) L->list[slot] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+        }
+        cnt += __popcll(m);
+    });
+    if (cnt > KNN_CAP) return false;
+    int P = 64;
+    while (P < cnt) P <<= 1;
+    for (int i = cnt + lane; i < P; i += 64) L->list[i] = ~0ull;
+    __builtin_amdgcn_wave_barrier();
+    wave_bitonic(L->list, P);
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// A1: segmentation ratio of every point
+__global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView g, const float4* __restrict__ pts4, int n,
+                                                              float radius, int max_nn, int sr_type,
+                                                              float* __restrict__ ratio, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
+    // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD group a contiguous query range
+    const int G = gridDim.x, b = blockIdx.x;
+    const int xg = b & 7, gi = b >> 3, ng = (G + 7 - xg) >> 3;
+    const int per = (n + 7) >> 3;
+    const int q_begin = xg * per, q_end = min(n, q_begin + per);
+    float* fl = reinterpret_cast<float*>(L->list);  // reused after selection: x[0..511], y, z...
+    for (int q = q_begin + gi * KNN_WAVES + wave; q < q_end; q += ng * KNN_WAVES) {
+        const float4 sp = pts4[q];
+        float out = __builtin_nanf("");
+        const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
+        const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
+        if (!origin && fin) {
+            int need = 0;
+            if (!knn_select(g, L, sp.x, sp.y, sp.z, radius, max_nn, &need)) {
+                if (lane == 0) atomicOr(err, 1);
+            } else if (need > 0) {
+                // gather neighbour coordinates (rank order) into LDS (overlaying the key list)
+                unsigned int myidx[KNN_CAP / 64];
+#pragma unroll
+                for (int j = 0; j < KNN_CAP / 64; ++j) {
+                    const int r = lane + 64 * j;
+                    myidx[j] = r < need ? (unsigned int)(L->list[r] & 0xFFFFFFFFu) : 0u;
+                }
+                __builtin_amdgcn_wave_barrier();
+                float px[KNN_CAP / 64], py[KNN_CAP / 64], pz[KNN_CAP / 64];
+#pragma unroll
+                for (int j = 0; j < KNN_CAP / 64; ++j) {
+                    const int r = lane + 64 * j;
+                    if (r < need) {
+                        const float4 p = pts4[myidx[j]];
+                        px[j] = p.x; py[j] = p.y; pz[j] = p.z;
+                        fl[r] = p.x; fl[512 + r] = p.y; fl[1024 + r] = p.z;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                // pcl::computeCentroid: sequential float sums in rank order (lanes 0,1,2)
+                float acc = 0.f;
+                if (lane < 3) {
+                    const float* src = fl + 512 * lane;
+                    for (int r = 0; r < need; ++r) acc = acc + src[r];
+                }
+                const float fn = (float)need;
+                const float cx = __shfl(acc, 0, 64) / fn, cy = __shfl(acc, 1, 64) / fn, cz = __shfl(acc, 2, 64) / fn;
+                const float tx = sp.x - cx, ty = sp.y - cy, tz = sp.z - cz;
+                if (sr_type == 0) {
+                    int pos = 0, neg = 0;
+#pragma unroll
+                    for (int j = 0; j < KNN_CAP / 64; ++j) {
+                        const int r = lane + 64 * j;
+                        bool p = false, m = false;
+                        if (r < need) {
+                            const float vx = px[j] - sp.x, vy = py[j] - sp.y, vz = pz[j] - sp.z;
+                            const float dot = (tx * vx + ty * vy) + tz * vz;
+                            p = dot > 0.f;
+                            m = dot < 0.f;
+                        }
+                        pos += __popcll(__ballot(p));
+                        neg += __popcll(__ballot(m));
+                    }
+                    const float fp = (float)pos, fm = (float)neg;
+                    out = 1.0f - fminf(fp, fm) / fmaxf(fp, fm);
+                    if (fp != fp || fm != fm) out = __builtin_nanf("");
+                } else {
+                    // CVS / CVSN: per-neighbour terms in parallel, sequential float sum in rank order
+                    const float ctn = sqrtf((tx * tx + ty * ty) + tz * tz);
+                    float* term = fl + 1536;  // 512 entries
+                    unsigned int* use = reinterpret_cast<unsigned int*>(L->hist);
+#pragma unroll
+                    for (int j = 0; j < KNN_CAP / 64; ++j) {
+                        const int r = lane + 64 * j;
+                        if (r < need && r < 512) {
+                            const float vx = px[j] - sp.x, vy = py[j] - sp.y, vz = pz[j] - sp.z;
+                            const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
+                            const float dot = (tx * vx + ty * vy) + tz * vz;
+                            use[r] = (ctn == 0.f || vn == 0.f) ? 0u : 1u;
+                            term[r] = sr_type == 1 ? dot : dot / (ctn * vn);
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    float sum = 0.f;
+                    if (lane == 0)
+                        for (int r = 0; r < need; ++r)
+                            if (use[r]) sum = sum + term[r];
+                    sum = __shfl(sum, 0, 64);
+                    out = fabsf(sum) / (float)need;
+                }
+            }
+        }
+        if (lane == 0) ratio[q] = out;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// A4: normals of K keypoints written to slots [0, K) of the persistent N-sized array
+__global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView g, const float4* __restrict__ pts4,
+                                                            const float* __restrict__ kps, int k, float radius,
+                                                            int max_nn, float4* __restrict__ normals,
+                                                            int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
+    float* fl = reinterpret_cast<float*>(L->list);
+    const float qn = __builtin_nanf("");
+    for (int q = blockIdx.x * KNN_WAVES + wave; q < k; q += gridDim.x * KNN_WAVES) {
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        float nx = qn, ny = qn, nz = qn, curv = qn;
+        bool write_nan_all = true;
+        if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
+            int need = 0;
+            if (!knn_select(g, L, kx, ky, kz, radius, max_nn, &need)) {
+                if (lane == 0) atomicOr(err, 2);
+            } else if (need > 0) {
+                write_nan_all = false;
+                if (need >= 3) {
+                    unsigned int myidx[KNN_CAP / 64];
+#pragma unroll
+                    for (int j = 0; j < KNN_CAP / 64; ++j) {
+                        const int r = lane + 64 * j;
+                        myidx[j] = r < need ? (unsigned int)(L->list[r] & 0xFFFFFFFFu) : 0u;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int j = 0; j < KNN_CAP / 64; ++j) {
+                        const int r = lane + 64 * j;
+                        if (r < need) {
+                            const float4 p = pts4[myidx[j]];
+                            fl[r] = p.x; fl[512 + r] = p.y; fl[1024 + r] = p.z;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    // pcl::computeMeanAndCovarianceMatrix: 9 float accumulators, rank order
+                    float acc = 0.f;
+                    if (lane < 9) {
+                        const int a = lane < 6 ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
+                        const int bsel = lane < 6 ? (lane < 3 ? lane : (lane < 5 ? lane - 2 : 2)) : -1;
+                        const float* A = fl + 512 * a;
+                        if (bsel >= 0) {
+                            const float* Bv = fl + 512 * bsel;
+                            for (int r = 0; r < need; ++r) acc = acc + A[r] * Bv[r];
+                        } else {
+                            for (int r = 0; r < need; ++r) acc = acc + A[r];
+                        }
+                    }
+                    float ac[9];
+#pragma unroll
+                    for (int a = 0; a < 9; ++a) ac[a] = __shfl(acc, a, 64);
+                    const float fn = (float)need;
+#pragma unroll
+                    for (int a = 0; a < 9; ++a) ac[a] = ac[a] / fn;
+                    float cov[9];
+                    cov[0] = ac[0] - ac[6] * ac[6];
+                    cov[1] = ac[1] - ac[6] * ac[7];
+                    cov[2] = ac[2] - ac[6] * ac[8];
+                    cov[4] = ac[3] - ac[7] * ac[7];
+                    cov[5] = ac[4] - ac[7] * ac[8];
+                    cov[8] = ac[5] - ac[8] * ac[8];
+                    cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+                    float ev, vec[3];
+                    bm::eigen33_min(cov, &ev, vec);
+                    nx = vec[0]; ny = vec[1]; nz = vec[2];
+                    const float eig_sum = (cov[0] + cov[4]) + cov[8];
+                    curv = (eig_sum != 0.f) ? fabsf(ev / eig_sum) : 0.f;
+                }
+                const float vx = 0.f - kx, vy = 0.f - ky, vz = 0.f - kz;
+                const float cth = (vx * nx + vy * ny) + vz * nz;
+                if (cth < 0.f) { nx *= -1.f; ny *= -1.f; nz *= -1.f; }
+            }
+        }
+        (void)write_nan_all;
+        if (lane == 0) normals[q] = make_float4(nx, ny, nz, curv);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES; }
+
+}  // namespace bsk
+
+namespace bsh {
+
+hipError_t launch_seg_ratio(const bsh::DevGrid& g, const float4* pts4, int n, float radius, int max_nn, int sr_type,
+                            float* ratio, int* err, hipStream_t s) {
+    const size_t lds = bsk::knn_lds_bytes();
+    int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
+    if (blocks > 8 * 256 * 4) blocks = 8 * 256 * 4;
+    blocks = (blocks + 7) & ~7;
+    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(g.view(), pts4, n, radius, max_nn, sr_type, ratio, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_normals(const bsh::DevGrid& g, const float4* pts4, const float* kps, int k, float radius, int max_nn,
+                          float4* normals, int* err, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    const size_t lds = bsk::knn_lds_bytes();
+    int blocks = (k + KNN_WAVES - 1) / KNN_WAVES;
+    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(g.view(), pts4, kps, k, radius, max_nn, normals, err);
+    return hipGetLastError();
+}
+
+}  // namespace bsh

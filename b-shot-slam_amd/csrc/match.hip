@@ -1,0 +1,103 @@
+// match.hip -- A9 on gfx950: brute-force B-SHOT Hamming matching (src/lidar_odometry.cpp:210-242).
+// Integer-exact. minVect's FIRST-index argmin (include/bshot_bits.h:6-20) is a min over the packed
+// key (dist << 32 | index): the smallest index wins every distance tie, whatever the reduction
+// order, so tiles may be reduced with 64-bit atomicMin across workgroups.
+//   k_ham_min: each thread owns one query descriptor (11 words in VGPRs); the workgroup streams a
+//   tile of reference descriptors through LDS (48-B padded rows, broadcast reads:
+//   3 x ds_read_b128 per reference), XOR + popcount, running packed min; one atomicMin per
+//   (query, tile). Run once per direction (left: A vs B, right: B vs A).
+//   k_mutual: corr flag i <=> right[left[i]] == i.
+#include <hip/hip_runtime.h>
+
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace bsk {
+
+#define HM_THREADS 256
+#define HM_TILE 1024
+
+__global__ void __launch_bounds__(HM_THREADS) k_ham_min(const unsigned int* __restrict__ q, int nq,
+                                                        const unsigned int* __restrict__ r, int nr, int tile,
+                                                        unsigned long long* __restrict__ best) {
+    __shared__ uint4 rt[HM_TILE * 3];
+    const int t = threadIdx.x;
+    const int qi = blockIdx.x * HM_THREADS + t;
+    const int r0 = blockIdx.y * tile;
+    const int r1 = min(nr, r0 + tile);
+    unsigned int a[11];
+#pragma unroll
+    for (int w = 0; w < 11; ++w) a[w] = qi < nq ? q[11 * (size_t)qi + w] : 0u;
+    unsigned long long m = ~0ull;
+    for (int s0 = r0; s0 < r1; s0 += HM_TILE) {
+        const int cnt = min(HM_TILE, r1 - s0);
+        __syncthreads();
+        for (int i = t; i < cnt * 12; i += HM_THREADS) {
+            const int row = i / 12, w = i % 12;
+            reinterpret_cast<unsigned int*>(rt)[i] = w < 11 ? r[11 * (size_t)(s0 + row) + w] : 0u;
+        }
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            const uint4 b0 = rt[3 * j], b1 = rt[3 * j + 1], b2 = rt[3 * j + 2];
+            unsigned int d = __builtin_popcount(a[0] ^ b0.x);
+            d += __builtin_popcount(a[1] ^ b0.y);
+            d += __builtin_popcount(a[2] ^ b0.z);
+            d += __builtin_popcount(a[3] ^ b0.w);
+            d += __builtin_popcount(a[4] ^ b1.x);
+            d += __builtin_popcount(a[5] ^ b1.y);
+            d += __builtin_popcount(a[6] ^ b1.z);
+            d += __builtin_popcount(a[7] ^ b1.w);
+            d += __builtin_popcount(a[8] ^ b2.x);
+            d += __builtin_popcount(a[9] ^ b2.y);
+            d += __builtin_popcount(a[10] ^ b2.z);
+            const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)(s0 + j);
+            m = key < m ? key : m;
+        }
+    }
+    if (qi < nq) atomicMin(&best[qi], m);
+}
+
+__global__ void k_fill_u64(unsigned long long* p, int n, unsigned long long v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__global__ void k_mutual(const unsigned long long* __restrict__ lbest, int na, const unsigned long long* __restrict__ rbest,
+                         int* __restrict__ left, int* __restrict__ right, int nb, int* __restrict__ flag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb) right[i] = (int)(rbest[i] & 0xFFFFFFFFu);
+    if (i < na) {
+        const int l = (int)(lbest[i] & 0xFFFFFFFFu);
+        left[i] = l;
+        flag[i] = ((int)(rbest[l] & 0xFFFFFFFFu) == i) ? 1 : 0;
+    }
+}
+
+}  // namespace bsk
+
+namespace bsh {
+
+static void ham_dir(const unsigned int* q, int nq, const unsigned int* r, int nr, unsigned long long* best,
+                    hipStream_t s) {
+    bsk::k_fill_u64<<<(nq + 255) / 256, 256, 0, s>>>(best, nq, ~0ull);
+    // split the reference set so the launch has >= ~1024 workgroups when nq is small
+    const int qb = (nq + HM_THREADS - 1) / HM_THREADS;
+    int splits = (1024 + qb - 1) / qb;
+    int tile = (nr + splits - 1) / splits;
+    if (tile < 256) tile = 256;
+    splits = (nr + tile - 1) / tile;
+    dim3 grid(qb, splits);
+    bsk::k_ham_min<<<grid, HM_THREADS, 0, s>>>(q, nq, r, nr, tile, best);
+}
+
+hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* lbest,
+                        unsigned long long* rbest, int* left, int* right, int* flag, hipStream_t s) {
+    if (na <= 0 || nb <= 0) return hipSuccess;
+    ham_dir(a, na, b, nb, lbest, s);
+    ham_dir(b, nb, a, na, rbest, s);
+    const int m = na > nb ? na : nb;
+    bsk::k_mutual<<<(m + 255) / 256, 256, 0, s>>>(lbest, na, rbest, left, right, nb, flag);
+    return hipGetLastError();
+}
+
+}  // namespace bsh

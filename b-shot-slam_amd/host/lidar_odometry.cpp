@@ -1,0 +1,316 @@
+// lidar_odometry.cpp -- myslam::LidarOdometry on MI355X (reference: src/lidar_odometry.cpp:1-525).
+// Host C++ keeps the order-defining, data-dependent steps that are cheap and serial (libstdc++
+// sort semantics for the top-K, the unordered_map keypoint map, RANSAC, gating); everything
+// proportional to N or K x neighbourhood runs in the gfx950 kernels through the context.
+#include "../../include/bshot/lidar_odometry.h"
+
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "../csrc/ctx.h"
+#include "geom.h"
+
+namespace myslam {
+
+static void zero_stats(bshot_frame_stats& s) { std::memset(&s, 0, sizeof(s)); }
+
+LidarOdometry::LidarOdometry()
+    : status_(INITIAL), shouldUpdateMap(true), sr_type_("CV"), evaluate_icp_(true), evaluate_corr_(false),
+      run_icp_(true) {
+    bshot_default_params(&prm_);
+    check(bshot_create(&ctx_, 0, &prm_), "bshot_create");
+    zero_stats(stats_);
+}
+
+LidarOdometry::LidarOdometry(const bshot_params& p, int device)
+    : prm_(p), status_(INITIAL), shouldUpdateMap(true), sr_type_("CV"), evaluate_icp_(true), evaluate_corr_(false),
+      run_icp_(p.run_icp != 0) {
+    if (prm_.sr_type == 1) sr_type_ = "CVS";
+    if (prm_.sr_type == 2) sr_type_ = "CVSN";
+    check(bshot_create(&ctx_, device, &prm_), "bshot_create");
+    zero_stats(stats_);
+}
+
+LidarOdometry::~LidarOdometry() { bshot_destroy(ctx_); }
+
+void LidarOdometry::check(int rc, const char* where) {
+    if (rc >= 0) return;
+    err_ = std::string(where) + ": " + (ctx_ ? bshot_last_error(ctx_) : "no context");
+    throw std::runtime_error(err_);
+}
+
+void LidarOdometry::setSRType(std::string sr_type) {
+    sr_type_ = sr_type;
+    prm_.sr_type = sr_type == "CVS" ? 1 : (sr_type == "CVSN" ? 2 : 0);
+    ctx_->prm.sr_type = prm_.sr_type;
+}
+
+void LidarOdometry::setRefFrame(Frame::Ptr ref) {
+    ref_ = ref;
+    ref_pc_ = *ref_->getPointCloud();
+}
+
+void LidarOdometry::setSrcFrame(Frame::Ptr src) {
+    src_ = src;
+    src_pc_ = *src_->getPointCloud();
+    src_dev_ = nullptr;
+    src_n_ = (int)src_pc_.size();
+    check(bshot_set_cloud(ctx_, src_n_ ? &src_pc_[0][0] : nullptr, src_n_), "setSrcFrame");
+}
+
+void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n) {
+    src_ = src;
+    src_pc_.clear();
+    src_dev_ = d_xyz;
+    src_n_ = n;
+    check(bshot_set_cloud_device(ctx_, d_xyz, n), "setSrcFrameDevice");
+}
+
+void LidarOdometry::passSrc2Ref() {
+    ref_ = src_;
+    ref_pc_ = src_pc_;
+    isskps_ref = isskps_src;
+}
+
+// gather xyz of the given cloud indices (device gather; works for host and device clouds)
+static PointCloudXYZ gather_points(bshot_ctx* c, const std::vector<int32_t>& idx, DBuf<float>& dst) {
+    PointCloudXYZ out(idx.size());
+    if (idx.empty()) return out;
+    if (bsh::ctx_gather(c, idx.data(), (int)idx.size(), dst) != BSHOT_OK ||
+        hipMemcpyAsync(&out[0][0], dst.p, sizeof(float) * 3 * idx.size(), hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        throw std::runtime_error(std::string("gather: ") + c->err);
+    return out;
+}
+
+void LidarOdometry::extractKeypoints() {
+    zero_stats(stats_);
+    const int n = src_n_;
+    stats_.n_points = n;
+    // A1 + A2 (src/lidar_odometry.cpp:51-153)
+    std::vector<int32_t> idx(n > 0 ? n : 1), kidx(prm_.num_keypoints > 0 ? prm_.num_keypoints : 1);
+    std::vector<float> ratio(n > 0 ? n : 1), kr(kidx.size());
+    int nv = 0, k = 0;
+    check(bshot_seg_ratio(ctx_, idx.data(), ratio.data(), &nv), "seg_ratio");
+    check(bshot_select_topk(idx.data(), ratio.data(), nv, prm_.num_keypoints, kidx.data(), kr.data(), &k), "topk");
+    kidx.resize(k);
+    stats_.n_valid_ratios = nv;
+    stats_.n_keypoints = k;
+    seg_ratios_.assign(kr.begin(), kr.begin() + k);
+    src_->setKeypoints(std::make_shared<std::vector<Vector3f>>(gather_points(ctx_, kidx, ctx_->kps)));
+    if (isInitial()) {
+        passSrc2Ref();
+        ref_->setKeypoints(src_->getKeypoints());
+    }
+    cloud1_kps_ = *src_->getKeypoints();
+    cloud2_kps_ = *ref_->getKeypoints();
+    // A3 ISS (src/lidar_odometry.cpp:164-170): computed every frame, used by kpEvaluation only
+    isskps_src.clear();
+    if (prm_.run_iss) {
+        std::vector<int32_t> iss(n > 0 ? n : 1);
+        int ni = 0;
+        check(bshot_iss(ctx_, iss.data(), (int)iss.size(), &ni), "iss");
+        iss.resize(ni);
+        isskps_src = gather_points(ctx_, iss, ctx_->gout);
+    }
+    stats_.n_iss = (int)isskps_src.size();
+    if (isInitial()) isskps_ref = isskps_src;
+}
+
+void LidarOdometry::computeDescriptors() {
+    // A4-A7 (src/lidar_odometry.cpp:173-184); keypoints are already on the device (ctx->kps)
+    const int k = (int)cloud1_kps_.size();
+    check(bsh::ctx_describe_dev(ctx_, k), "describe");
+    std::vector<uint32_t> words(11 * (size_t)(k > 0 ? k : 1));
+    if (k > 0) {
+        if (hipMemcpyAsync(words.data(), ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
+                           ctx_->stream) != hipSuccess)
+            check(BSHOT_EHIP, "D2H bits");
+    }
+    check(bshot_sync(ctx_), "describe sync");
+    int herr = 0;
+    if (ctx_->errw.p && hipMemcpy(&herr, ctx_->errw.p, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && (herr & 2))
+        check(BSHOT_ECAP, "normals neighbourhood overflow");
+    cloud1_bshot_.resize(k);
+    auto desc = std::make_shared<std::vector<std::bitset<352>>>();
+    desc->reserve(k);
+    for (int i = 0; i < k; ++i) {
+        cloud1_bshot_[i].bits = words_to_bits(&words[11 * (size_t)i]);
+        desc->push_back(cloud1_bshot_[i].bits);
+    }
+    src_->setDescriptors(desc);
+}
+
+void LidarOdometry::featureMatching() {
+    // src/lidar_odometry.cpp:186-265
+    if (isInitial()) {
+        passSrc2Ref();
+        ref_->setKeypoints(src_->getKeypoints());
+        cloud2_bshot_ = cloud1_bshot_;
+        cloud2_kps_ = *ref_->getKeypoints();
+    } else {
+        const Matrix4f rp = ref_->getPose();
+        globalMap_.getKeypoints(rp.topRightCorner(), prm_.map_range, cloud2_kps_, cloud2_bshot_);
+        for (const Vector3f& q : *ref_->getKeypoints()) cloud2_kps_.push_back(rp.transformPoint(q));
+        std::vector<bshot_descriptor> rb = eigen2dc(ref_->getDescriptors());
+        cloud2_bshot_.insert(cloud2_bshot_.end(), rb.begin(), rb.end());
+    }
+    const int na = (int)cloud1_bshot_.size(), nb = (int)cloud2_bshot_.size();
+    stats_.n_target = nb;
+    std::vector<uint32_t> a(11 * (size_t)(na > 0 ? na : 1)), b(11 * (size_t)(nb > 0 ? nb : 1));
+    for (int i = 0; i < na; ++i) bits_to_words(cloud1_bshot_[i].bits, &a[11 * (size_t)i]);
+    for (int i = 0; i < nb; ++i) bits_to_words(cloud2_bshot_[i].bits, &b[11 * (size_t)i]);
+    std::vector<int32_t> left(na > 0 ? na : 1), right(nb > 0 ? nb : 1), cq(na > 0 ? na : 1), cm(na > 0 ? na : 1);
+    int nc = 0;
+    check(bshot_match(ctx_, a.data(), na, b.data(), nb, left.data(), right.data(), cq.data(), cm.data(), &nc), "match");
+    stats_.n_mutual = nc;
+    // RANSAC rejection (maxIter 2000, threshold 1500 mm)
+    std::vector<int32_t> iq(nc > 0 ? nc : 1), im(nc > 0 ? nc : 1);
+    int ni = 0;
+    float T[16];
+    check(bshot_ransac(na ? &cloud1_kps_[0][0] : nullptr, na, nb ? &cloud2_kps_[0][0] : nullptr, nb, cq.data(),
+                       cm.data(), nc, prm_.ransac_max_iter, prm_.ransac_thresh, T, iq.data(), im.data(), &ni),
+          "ransac");
+    std::memcpy(T_ransac_.m, T, sizeof(T));
+    corr_.resize(ni);
+    for (int i = 0; i < ni; ++i) corr_[i] = std::make_pair(iq[i], im[i]);
+    stats_.n_inliers = ni;
+}
+
+void LidarOdometry::evaluateEstimation() {
+    // src/lidar_odometry.cpp:267-331
+    const Matrix4f T_j = T_ransac_;
+    const Matrix4f T_i = ref_->getPose();
+    const Matrix4f T_ij = T_i.inverse() * T_j;
+    const float h_diff = std::acos(T_ij(1, 1));  // e_y^T R e_y
+    const Vector3f t = T_ij.topRightCorner();
+    const float t_diff = t.norm();
+    stats_.h_diff = h_diff;
+    stats_.t_diff = t_diff;
+    Matrix4f T_est;
+    if (h_diff * 180 / M_PI > 10 || t_diff > 1200 || corr_.size() < 15) {
+        T_est = ref_->getPose();
+        shouldUpdateMap = false;
+        stats_.gated = 1;
+    } else {
+        T_est = T_j;
+        shouldUpdateMap = true;
+    }
+    // ICP always runs (:291-297), source = cloud1 keypoints transformed by T_est
+    const int k = (int)cloud1_kps_.size(), m = (int)cloud2_kps_.size();
+    std::vector<float> src(3 * (size_t)(k > 0 ? k : 1));
+    for (int i = 0; i < k; ++i) {
+        const Vector3f p = T_est.transformPoint(cloud1_kps_[i]);
+        src[3 * i] = p[0]; src[3 * i + 1] = p[1]; src[3 * i + 2] = p[2];
+    }
+    float Ticp[16];
+    int iters = 0;
+    check(bshot_icp(ctx_, src.data(), k, m ? &cloud2_kps_[0][0] : nullptr, m, prm_.icp_max_iter, Ticp, &iters), "icp");
+    stats_.icp_iters = iters;
+    Matrix4f F;
+    std::memcpy(F.m, Ticp, sizeof(Ticp));
+    T_best_ = run_icp_ ? F * T_est : T_j;
+    if (evaluate_corr_ && !corr_.empty()) {
+        // correspondence distance statistics (:303-330): computed for the logs, not returned
+        const Matrix4f& Tc = evaluate_icp_ ? T_best_ : T_j;
+        double acc = 0;
+        for (auto& c : corr_) acc += (Tc.transformPoint(cloud1_kps_[c.first]) - cloud2_kps_[c.second]).norm();
+        (void)acc;
+    }
+}
+
+void LidarOdometry::poseEstimation() { src_->setPose(T_best_); }
+
+void LidarOdometry::updateMap() {
+    // src/lidar_odometry.cpp:344-376 (shouldUpdateMap is never read by the reference)
+    const Matrix3f R = T_best_.block33();
+    const Vector3f T = T_best_.topRightCorner();
+    Frame::PCPtr kps = src_->getKeypoints();
+    for (size_t i = 0; i < cloud1_bshot_.size(); i++) {
+        Vector3f kp_pos = R * kps->at(i) + T;
+        Keypoint::Ptr kp = Keypoint::createKeypoint(kp_pos, seg_ratios_[i], cloud1_bshot_[i]);
+        globalMap_.addKeypoint(kp);
+    }
+    status_ = RUN;
+    std::memcpy(stats_.T_ransac, T_ransac_.m, sizeof(stats_.T_ransac));
+    std::memcpy(stats_.pose, T_best_.m, sizeof(stats_.pose));
+    stats_.map_size = globalMap_.size();
+}
+
+void LidarOdometry::updateCorrespondence() {
+    corrs.clear();
+    corrs.reserve(corr_.size());
+    for (auto& co : corr_) corrs.push_back(std::make_pair(cloud1_kps_[co.first], cloud2_kps_[co.second]));
+}
+
+static float repeat_rate(const PointCloudXYZ& src, const PointCloudXYZ& ref) {
+    if (src.empty()) return 0.f;
+    float hit = 0.f;
+    for (const Vector3f& s : src) {
+        if (s[0] == 0 && s[1] == 0 && s[2] == 0) continue;
+        float best = INFINITY;
+        for (const Vector3f& r : ref) {
+            const float dx = s[0] - r[0], dy = s[1] - r[1], dz = s[2] - r[2];
+            const float d2 = (dx * dx + dy * dy) + dz * dz;
+            if (d2 < best) best = d2;
+        }
+        if (!ref.empty() && best <= 900.f) hit += 1.f;
+    }
+    return hit / (float)src.size();
+}
+
+void LidarOdometry::kpEvaluation() {
+    // src/lidar_odometry.cpp:392-445: 1-NN repeatability (<= 30 mm) of SR and ISS keypoints
+    stats_.repeat_sr = repeat_rate(*src_->getKeypoints(), *ref_->getKeypoints());
+    stats_.repeat_iss = repeat_rate(isskps_src, isskps_ref);
+}
+
+PointCloudXYZ LidarOdometry::issKpDetection(const PointCloudXYZ& kps) {
+    // standalone ISS over an arbitrary cloud (src/lidar_odometry.cpp:447-461)
+    const int n = (int)kps.size();
+    check(bshot_set_cloud(ctx_, n ? kps.data()->v : nullptr, n), "iss set cloud");
+    std::vector<int32_t> iss(n > 0 ? n : 1);
+    int ni = 0;
+    check(bshot_iss(ctx_, iss.data(), (int)iss.size(), &ni), "iss");
+    PointCloudXYZ out;
+    for (int i = 0; i < ni; ++i) out.push_back(kps[iss[i]]);
+    // restore the source cloud
+    if (src_n_ > 0) {
+        if (src_dev_) check(bshot_set_cloud_device(ctx_, src_dev_, src_n_), "restore cloud");
+        else check(bshot_set_cloud(ctx_, &src_pc_[0][0], src_n_), "restore cloud");
+    }
+    return out;
+}
+
+Frame::PCPtr LidarOdometry::getKeypoints() {
+    Frame::PCPtr kps = std::make_shared<std::vector<Vector3f>>();
+    globalMap_.getAllKeypoints(*kps);
+    return kps;
+}
+Frame::PCPtr LidarOdometry::getSrcKeypoints() { return std::make_shared<std::vector<Vector3f>>(cloud1_kps_); }
+Frame::PCPtr LidarOdometry::getRefKeypoints() { return std::make_shared<std::vector<Vector3f>>(cloud2_kps_); }
+Frame::PCPtr LidarOdometry::getISSKeypoints() { return std::make_shared<std::vector<Vector3f>>(isskps_src); }
+
+PointCloudXYZ LidarOdometry::eigen2pcl(Frame::PCPtr pcptr) { return pcptr ? *pcptr : PointCloudXYZ(); }
+
+std::vector<bshot_descriptor> LidarOdometry::eigen2dc(Frame::DCPPtr pcptr) {
+    std::vector<bshot_descriptor> d;
+    if (!pcptr) return d;
+    d.reserve(pcptr->size());
+    for (auto& b : *pcptr) {
+        bshot_descriptor x;
+        x.bits = b;
+        d.push_back(x);
+    }
+    return d;
+}
+
+std::vector<LidarOdometry::PC> LidarOdometry::getBlockKeypoints() {
+    std::vector<PC> kpblock;
+    globalMap_.getBlockKeypoints(kpblock);
+    return kpblock;
+}
+
+}  // namespace myslam

@@ -1,0 +1,200 @@
+// odom_abi.cpp -- C ABI over myslam::LidarOdometry: the headless odometry_test frame loop
+// (test/odometry_test.cpp:159-194, test/kp_test.cpp:159-181) plus the map-delta records used by
+// the multi-GPU throughput mode (BASELINE config 4). No exception crosses the ABI.
+#include <cstring>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/bshot/lidar_odometry.h"
+#include "../../include/bshot_abi.h"
+
+struct bshot_odom {
+    std::unique_ptr<myslam::LidarOdometry> lo;
+    std::string err;
+    std::vector<float> delta;  // last frame's map delta, 15 floats per keypoint
+    std::vector<myslam::Map> replicas;
+};
+
+static int guard(bshot_odom* o, const std::function<void()>& f);
+
+namespace {
+
+constexpr int kRec = 15;  // x, y, z, ratio, 11 descriptor words (bit patterns)
+
+int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_frame_stats* st) {
+    myslam::LidarOdometry& lo = *o->lo;
+    myslam::Frame::Ptr f = myslam::Frame::createFrame();
+    if (xyz) {
+        auto pc = std::make_shared<std::vector<myslam::Vector3f>>(n);
+        if (n > 0) std::memcpy(&(*pc)[0][0], xyz, sizeof(float) * 3 * n);
+        f->setPointCloud(pc);
+    }
+    if (!lo.isInitial()) lo.passSrc2Ref();
+    if (xyz) lo.setSrcFrame(f);
+    else lo.setSrcFrameDevice(f, d_xyz, n);
+    lo.extractKeypoints();
+    lo.computeDescriptors();
+    lo.featureMatching();
+    lo.evaluateEstimation();
+    lo.poseEstimation();
+    lo.kpEvaluation();
+    lo.updateMap();
+    lo.updateCorrespondence();
+    if (st) *st = lo.lastStats();
+    // map delta: the K keypoint records this frame offered to Map::addKeypoint
+    const myslam::Matrix4f P = f->getPose();
+    const myslam::Matrix3f R = P.block33();
+    const myslam::Vector3f T = P.topRightCorner();
+    auto kps = f->getKeypoints();
+    auto ds = f->getDescriptors();
+    const auto& ratios = lo.segRatios();
+    const size_t k = kps ? kps->size() : 0;
+    o->delta.assign(k * kRec, 0.f);
+    for (size_t i = 0; i < k; ++i) {
+        myslam::Vector3f w = R * kps->at(i) + T;
+        bshot_descriptor d;
+        d.bits = ds->at(i);
+        auto kp = myslam::Keypoint::createKeypoint(w, ratios[i], d);
+        float* r = &o->delta[i * kRec];
+        r[0] = kp->getPosition()[0];
+        r[1] = kp->getPosition()[1];
+        r[2] = kp->getPosition()[2];
+        r[3] = ratios[i];
+        uint32_t words[11];
+        myslam::bits_to_words(d.bits, words);
+        std::memcpy(r + 4, words, sizeof(words));
+    }
+    return BSHOT_OK;
+}
+
+}  // namespace
+
+static int guard(bshot_odom* o, const std::function<void()>& f) {
+    try {
+        f();
+        return BSHOT_OK;
+    } catch (const std::exception& e) {
+        o->err = e.what();
+        return BSHOT_EHIP;
+    }
+}
+
+extern "C" {
+
+int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p) {
+    if (!out) return BSHOT_EINVAL;
+    *out = nullptr;
+    bshot_params prm;
+    if (p) prm = *p;
+    else bshot_default_params(&prm);
+    auto* o = new bshot_odom();
+    try {
+        o->lo.reset(new myslam::LidarOdometry(prm, device));
+    } catch (const std::exception& e) {
+        delete o;
+        return BSHOT_EHIP;
+    }
+    *out = o;
+    return BSHOT_OK;
+}
+
+void bshot_odom_destroy(bshot_odom* o) { delete o; }
+
+const char* bshot_odom_last_error(const bshot_odom* o) { return o ? o->err.c_str() : "null"; }
+
+int bshot_odom_process(bshot_odom* o, const float* xyz, int n, bshot_frame_stats* st) {
+    if (!o || n < 0 || (n > 0 && !xyz)) return BSHOT_EINVAL;
+    return guard(o, [&]() { run_frame(o, xyz, nullptr, n, st); });
+}
+
+int bshot_odom_process_device(bshot_odom* o, const float* d_xyz, int n, bshot_frame_stats* st) {
+    if (!o || n < 0 || (n > 0 && !d_xyz)) return BSHOT_EINVAL;
+    return guard(o, [&]() { run_frame(o, nullptr, d_xyz, n, st); });
+}
+
+int bshot_odom_get_keypoints(bshot_odom* o, float* xyz, int cap) {
+    auto k = o->lo->getSrcFrame() ? o->lo->getSrcFrame()->getKeypoints() : nullptr;
+    const int n = k ? (int)k->size() : 0;
+    if (n > cap) return -n;
+    if (n) std::memcpy(xyz, &(*k)[0][0], sizeof(float) * 3 * n);
+    return n;
+}
+
+int bshot_odom_get_ratios(bshot_odom* o, float* r, int cap) {
+    const auto& v = o->lo->segRatios();
+    const int n = (int)v.size();
+    if (n > cap) return -n;
+    if (n) std::memcpy(r, v.data(), sizeof(float) * n);
+    return n;
+}
+
+int bshot_odom_get_bits(bshot_odom* o, uint32_t* bits, int cap) {
+    auto d = o->lo->getSrcFrame() ? o->lo->getSrcFrame()->getDescriptors() : nullptr;
+    const int n = d ? (int)d->size() : 0;
+    if (n > cap) return -n;
+    for (int i = 0; i < n; ++i) myslam::bits_to_words((*d)[i], bits + 11 * (size_t)i);
+    return n;
+}
+
+int bshot_odom_get_target(bshot_odom* o, float* xyz, uint32_t* bits, int cap) {
+    const auto& k = o->lo->targetKeypoints();
+    const auto& d = o->lo->targetDescriptors();
+    const int n = (int)k.size();
+    if (n > cap) return -n;
+    if (xyz && n) std::memcpy(xyz, k.data()->v, sizeof(float) * 3 * n);
+    if (bits)
+        for (int i = 0; i < n; ++i) myslam::bits_to_words(d[i].bits, bits + 11 * (size_t)i);
+    return n;
+}
+
+int bshot_odom_get_inliers(bshot_odom* o, int32_t* q, int32_t* m, int cap) {
+    const auto& c = o->lo->inlierCorrespondences();
+    const int n = (int)c.size();
+    if (n > cap) return -n;
+    for (int i = 0; i < n; ++i) { q[i] = c[i].first; m[i] = c[i].second; }
+    return n;
+}
+
+int bshot_odom_get_iss(bshot_odom* o, float* xyz, int cap) {
+    auto k = o->lo->getISSKeypoints();
+    const int n = (int)k->size();
+    if (n > cap) return -n;
+    if (n) std::memcpy(xyz, &(*k)[0][0], sizeof(float) * 3 * n);
+    return n;
+}
+
+bshot_ctx* bshot_odom_ctx(bshot_odom* o) { return o ? o->lo->context() : nullptr; }
+
+int bshot_odom_map_delta(bshot_odom* o, float* rec, int cap) {
+    const int n = (int)(o->delta.size() / kRec);
+    if (n > cap) return -n;
+    if (n) std::memcpy(rec, o->delta.data(), sizeof(float) * kRec * n);
+    return n;
+}
+
+int bshot_odom_replica_insert(bshot_odom* o, int replica, const float* rec, int n) {
+    if (!o || replica < 0 || n < 0) return BSHOT_EINVAL;
+    if ((int)o->replicas.size() <= replica) o->replicas.resize(replica + 1);
+    return guard(o, [&]() {
+        for (int i = 0; i < n; ++i) {
+            const float* r = rec + (size_t)i * kRec;
+            myslam::Vector3f p(r[0], r[1], r[2]);
+            uint32_t words[11];
+            std::memcpy(words, r + 4, sizeof(words));
+            bshot_descriptor d;
+            d.bits = myslam::words_to_bits(words);
+            // positions are already on the 10 mm grid: createKeypoint is idempotent on them
+            o->replicas[replica].addKeypoint(myslam::Keypoint::createKeypoint(p, r[3], d));
+        }
+    });
+}
+
+int bshot_odom_replica_size(bshot_odom* o, int replica) {
+    if (!o || replica < 0 || replica >= (int)o->replicas.size()) return 0;
+    return o->replicas[replica].size();
+}
+
+}  // extern "C"

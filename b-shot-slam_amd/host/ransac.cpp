@@ -1,0 +1,162 @@
+// ransac.cpp -- A10 RANSAC correspondence rejection with PCL semantics
+// (src/lidar_odometry.cpp:251-261: CorrespondenceRejectorSampleConsensus, maxIter 2000, inlier
+// threshold 1500 mm; RandomSampleConsensus + SampleConsensusModelRegistration).
+//
+// Structure: the hypothesis stream does not depend on model scores (draws happen only in
+// getSamples: mt19937(12345) >> 1, partial Fisher-Yates on the persistent shuffled index vector,
+// isSampleGood redraws), so phase 1 generates every sample triplet up front and phase 2 scans the
+// hypotheses in order applying PCL's best-model / adaptive-k / max-iteration rules. Phase 2's
+// scoring is independent per hypothesis (the batched-GPU evaluation of SURVEY.md §8f rank 2 slots in
+// here).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <random>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/bshot_abi.h"
+#include "geom.h"
+
+namespace {
+
+struct Pt { float x, y, z; };
+
+// computeMeanAndCovarianceMatrix (float, single pass) over src[indices] -> eigen33 values
+double sample_threshold(const Pt* src, const std::vector<int>& ind) {
+    float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int id : ind) {
+        const Pt& p = src[id];
+        acc[0] += p.x * p.x; acc[1] += p.x * p.y; acc[2] += p.x * p.z;
+        acc[3] += p.y * p.y; acc[4] += p.y * p.z; acc[5] += p.z * p.z;
+        acc[6] += p.x; acc[7] += p.y; acc[8] += p.z;
+    }
+    const float fn = (float)ind.size();
+    for (int a = 0; a < 9; ++a) acc[a] = acc[a] / fn;
+    float cov[9];
+    cov[0] = acc[0] - acc[6] * acc[6]; cov[1] = acc[1] - acc[6] * acc[7]; cov[2] = acc[2] - acc[6] * acc[8];
+    cov[4] = acc[3] - acc[7] * acc[7]; cov[5] = acc[4] - acc[7] * acc[8]; cov[8] = acc[5] - acc[8] * acc[8];
+    cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+    float ev[3];
+    bm::eigen33_vals(cov, ev);
+    const float s = (std::sqrt(ev[0]) + std::sqrt(ev[1])) + std::sqrt(ev[2]);
+    double t = (double)s / 3.0;
+    return t * t;
+}
+
+}  // namespace
+
+extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, int nt, const int32_t* corr_q,
+                            const int32_t* corr_m, int n_corr, int max_iter, double thresh, float* T_out,
+                            int32_t* inl_q, int32_t* inl_m, int* n_inl) {
+    if (!T_out || !n_inl || n_corr < 0 || ns < 0 || nt < 0) return BSHOT_EINVAL;
+    const Pt* src = reinterpret_cast<const Pt*>(src_xyz);
+    const Pt* tgt = reinterpret_cast<const Pt*>(tgt_xyz);
+    auto fallback = [&]() {
+        const bg::Mat4f I = bg::Mat4f::identity();
+        std::memcpy(T_out, I.m, sizeof(I.m));
+        for (int i = 0; i < n_corr; ++i) { inl_q[i] = corr_q[i]; inl_m[i] = corr_m[i]; }
+        *n_inl = n_corr;
+        return 0;
+    };
+    std::vector<int> indices(corr_q, corr_q + n_corr);
+    if ((int)indices.size() > ns) indices.clear();  // SampleConsensusModel ctor index check
+    std::unordered_map<int, int> tgt_of;
+    tgt_of.reserve(n_corr * 2 + 1);
+    for (int i = 0; i < n_corr; ++i) tgt_of[corr_q[i]] = corr_m[i];
+    const int nidx = (int)indices.size();
+    if (nidx < 3) return fallback();
+    const double sample_thresh = sample_threshold(src, indices);
+
+    // ---- phase 1: the hypothesis stream (getSamples for iterations 0..max_iter)
+    std::mt19937 rng(12345u);
+    std::vector<int> shuffled = indices;
+    std::vector<int> samples;
+    samples.reserve(3 * (size_t)(max_iter + 1));
+    for (int it = 0; it <= max_iter; ++it) {
+        bool got = false;
+        for (unsigned chk = 0; chk < 1000 && !got; ++chk) {
+            for (int i = 0; i < 3; ++i) {
+                const unsigned r = rng() >> 1;
+                std::swap(shuffled[i], shuffled[i + (int)(r % (unsigned)(nidx - i))]);
+            }
+            const Pt &a = src[shuffled[0]], &b = src[shuffled[1]], &c = src[shuffled[2]];
+            const float p10x = b.x - a.x, p10y = b.y - a.y, p10z = b.z - a.z;
+            const float p20x = c.x - a.x, p20y = c.y - a.y, p20z = c.z - a.z;
+            const float p21x = c.x - b.x, p21y = c.y - b.y, p21z = c.z - b.z;
+            got = (double)((p10x * p10x + p10y * p10y) + p10z * p10z) > sample_thresh &&
+                  (double)((p20x * p20x + p20y * p20y) + p20z * p20z) > sample_thresh &&
+                  (double)((p21x * p21x + p21y * p21y) + p21z * p21z) > sample_thresh;
+        }
+        if (!got) break;
+        samples.push_back(shuffled[0]);
+        samples.push_back(shuffled[1]);
+        samples.push_back(shuffled[2]);
+    }
+    const int nhyp = (int)samples.size() / 3;
+
+    // per-correspondence source / target points in index order (countWithinDistance loop order)
+    std::vector<Pt> cs(nidx), ct(nidx);
+    for (int i = 0; i < nidx; ++i) { cs[i] = src[indices[i]]; ct[i] = tgt[tgt_of[indices[i]]]; }
+    const double thr2 = thresh * thresh;
+    auto count_within = [&](const bg::Mat4f& T, std::vector<int>* inl) {
+        int cnt = 0;
+        for (int i = 0; i < nidx; ++i) {
+            float p[3];
+            bg::xform(T, &cs[i].x, p);
+            const float dx = p[0] - ct[i].x, dy = p[1] - ct[i].y, dz = p[2] - ct[i].z;
+            const float d2 = (dx * dx + dz * dz) + (dy * dy + 0.0f);  // Vector4f squaredNorm (SSE)
+            if ((double)d2 < thr2) { ++cnt; if (inl) inl->push_back(indices[i]); }
+        }
+        return cnt;
+    };
+    auto model_of = [&](int h) {
+        double sd[9], td[9];
+        for (int i = 0; i < 3; ++i) {
+            const Pt& a = src[samples[3 * h + i]];
+            const Pt& b = tgt[tgt_of[samples[3 * h + i]]];
+            sd[i * 3] = a.x; sd[i * 3 + 1] = a.y; sd[i * 3 + 2] = a.z;
+            td[i * 3] = b.x; td[i * 3 + 1] = b.y; td[i * 3 + 2] = b.z;
+        }
+        return bg::umeyama<double>(sd, td, 3);
+    };
+
+    // ---- phase 2: RandomSampleConsensus::computeModel acceptance scan
+    const double log_prob = std::log(1.0 - 0.99);
+    const double one_over_indices = 1.0 / (double)nidx;
+    double k = 1.0;
+    int best_cnt = -std::numeric_limits<int>::max();
+    bg::Mat4f best_T = bg::Mat4f::identity();
+    bool have = false;
+    for (int it = 0; it < nhyp && (double)it < k; ++it) {
+        const bg::Mat4f T = model_of(it);
+        const int cnt = count_within(T, nullptr);
+        if (cnt > best_cnt) {
+            best_cnt = cnt;
+            best_T = T;
+            have = true;
+            const double w = (double)best_cnt * one_over_indices;
+            double p_no = 1.0 - std::pow(w, 3.0);
+            p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
+            p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
+            k = log_prob / std::log(p_no);
+        }
+        if (it + 1 > max_iter) break;
+    }
+    if (!have) return fallback();
+    std::vector<int> inl;
+    count_within(best_T, &inl);
+    if (inl.size() < 3) return fallback();
+    std::unordered_map<int, int> pos_of;
+    for (int i = 0; i < n_corr; ++i) pos_of[corr_q[i]] = i;
+    for (size_t i = 0; i < inl.size(); ++i) {
+        const int p = pos_of[inl[i]];
+        inl_q[i] = corr_q[p];
+        inl_m[i] = corr_m[p];
+    }
+    *n_inl = (int)inl.size();
+    std::memcpy(T_out, best_T.m, sizeof(best_T.m));
+    return 1;
+}

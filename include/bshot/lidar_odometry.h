@@ -1,0 +1,98 @@
+// lidar_odometry.h -- myslam::LidarOdometry, the drop-in surface of the reference
+// (include/lidar_odometry.h:13-73) used by odometry_test / kp_test. Same method names, call order
+// and per-frame state; the hot stages run on the GPU through the C ABI context (bshot_abi.h).
+// Differences: PCL types leave the API (PointCloudXYZ instead of
+// pcl::PointCloud<pcl::PointXYZ>); the bshot member becomes private; two constructors take the
+// parameter block / device; lastStats() reports per-frame counters.
+#pragma once
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../bshot_abi.h"
+#include "bshot_bits.h"
+#include "frame.h"
+#include "mymap.h"
+#include "types.h"
+
+namespace myslam {
+
+class LidarOdometry {
+  public:
+    LidarOdometry();
+    explicit LidarOdometry(const bshot_params& p, int device = 0);
+    ~LidarOdometry();
+    LidarOdometry(const LidarOdometry&) = delete;
+    LidarOdometry& operator=(const LidarOdometry&) = delete;
+
+    enum STATUS { INITIAL, RUN };
+
+    void setRefFrame(Frame::Ptr ref);
+    void setSrcFrame(Frame::Ptr src);
+    // device-resident cloud (n x 3 floats already in HBM); the Frame keeps a host copy lazily
+    void setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n);
+    void extractKeypoints();
+    void computeDescriptors();
+    void featureMatching();
+    void poseEstimation();
+    void evaluateEstimation();
+    void updateMap();
+    void updateCorrespondence();
+    void kpEvaluation();
+    PointCloudXYZ issKpDetection(const PointCloudXYZ& kps);
+    void passSrc2Ref();
+    bool isInitial() { return status_ == INITIAL; }
+    Frame::Ptr getRefFrame() { return ref_; }
+    Frame::Ptr getSrcFrame() { return src_; }
+    Frame::PCPtr getKeypoints();
+    Frame::PCPtr getSrcKeypoints();
+    Frame::PCPtr getRefKeypoints();
+    Frame::PCPtr getISSKeypoints();
+    typedef std::vector<Vector3f> PC;
+    std::vector<PC> getBlockKeypoints();
+    Matrix4f getTransformationDiff() { return src_->getPose() * ref_->getPose().inverse(); }
+    std::vector<std::pair<Vector3f, Vector3f>> getCorrespondences() { return corrs; }
+    PointCloudXYZ eigen2pcl(Frame::PCPtr pcptr);
+    std::vector<bshot_descriptor> eigen2dc(Frame::DCPPtr pcptr);
+    void setSRType(std::string sr_type);
+    void setEvaluateCorr(bool eval_corr) { evaluate_corr_ = eval_corr; }
+    void setEvaluateICP(bool eval_icp) { evaluate_icp_ = eval_icp; }
+    void setRunICP(bool run_icp) { run_icp_ = run_icp; }
+
+    // extensions (not in the reference)
+    const bshot_frame_stats& lastStats() const { return stats_; }
+    bshot_ctx* context() { return ctx_; }
+    const std::vector<float>& segRatios() const { return seg_ratios_; }
+    const PointCloudXYZ& targetKeypoints() const { return cloud2_kps_; }
+    const std::vector<bshot_descriptor>& targetDescriptors() const { return cloud2_bshot_; }
+    const std::vector<std::pair<int, int>>& inlierCorrespondences() const { return corr_; }
+    Map& globalMap() { return globalMap_; }
+    const std::string& lastError() const { return err_; }
+
+  private:
+    void check(int rc, const char* where);
+
+    bshot_params prm_;
+    bshot_ctx* ctx_ = nullptr;
+    Frame::Ptr ref_, src_;
+    PointCloudXYZ src_pc_, ref_pc_;  // src_pcl_ / ref_pcl_ (src/lidar_odometry.cpp:29-41)
+    const float* src_dev_ = nullptr;
+    int src_n_ = 0;
+    STATUS status_;
+    std::vector<float> seg_ratios_;
+    Map globalMap_;
+    PointCloudXYZ cloud1_kps_, cloud2_kps_;
+    std::vector<bshot_descriptor> cloud1_bshot_, cloud2_bshot_;
+    std::vector<std::pair<int, int>> corr_;  // RANSAC inliers (index_query, index_match)
+    std::vector<std::pair<Vector3f, Vector3f>> corrs;
+    Matrix4f T_best_, T_ransac_;
+    bool shouldUpdateMap;
+    std::string sr_type_;
+    bool evaluate_icp_, evaluate_corr_, run_icp_;
+    PointCloudXYZ isskps_src, isskps_ref;
+    bshot_frame_stats stats_;
+    std::string err_;
+};
+
+}  // namespace myslam

@@ -1,0 +1,156 @@
+/* bshot_abi.h -- C ABI of the MI355X-native B-SHOT hot path (libbshot_amd.so).
+ *
+ * The reference (TingKaiChen/B-SHOT-SLAM) has no plugin/FFI layer: its boundary is the C++ class
+ * API (include/lidar_odometry.h:13-73, include/frame.h:10-51, include/keypoint.h:8-32,
+ * include/mymap.h:9-51, include/bshot_bits.h:6-281). This C ABI sits UNDER the C++ API in
+ * include/bshot/ (which keeps those class names) and is what ctypes/cgo/JNI would bind
+ * (INTEGRATION.md). Conventions: 0 = OK, negative = error (message via bshot_last_error); no C++
+ * exception crosses the ABI; host buffers are caller-owned and only read/written during the call;
+ * device memory is context-owned; one context per host thread and GPU; no global mutable state.
+ * Points are float32 millimetres, AoS xyz. 4x4 matrices are row-major float[16].
+ * Descriptors (B-SHOT) are 11 x uint32 per keypoint: bit j of the reference's std::bitset<352> is
+ * bit (j % 32) of word j / 32 (include/bshot_bits.h:25, :264-275).
+ */
+#ifndef BSHOT_ABI_H
+#define BSHOT_ABI_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSHOT_WORDS 11
+#define BSHOT_OK 0
+#define BSHOT_EINVAL (-1)
+#define BSHOT_EHIP (-2)
+#define BSHOT_ECAP (-3)
+#define BSHOT_ESTATE (-4)
+
+typedef struct bshot_ctx bshot_ctx;
+
+/* Defaults = the reference's hard-coded constants (cited per field). */
+typedef struct {
+    float seg_radius;     /* 3000  src/lidar_odometry.cpp:68 (SR radius, mm) */
+    int seg_max_nn;       /* 300   src/lidar_odometry.cpp:70 */
+    int sr_type;          /* 0 CV, 1 CVS, 2 CVSN: include/lidar_odometry.h:47 setSRType */
+    int num_keypoints;    /* 600   src/lidar_odometry.cpp:138 (BASELINE config 2: 2048) */
+    float iss_salient;    /* 60    src/lidar_odometry.cpp:452 */
+    float iss_nonmax;     /* 40    src/lidar_odometry.cpp:453 */
+    double iss_gamma21;   /* 0.975 src/lidar_odometry.cpp:454 */
+    double iss_gamma32;   /* 0.975 src/lidar_odometry.cpp:455 */
+    int iss_min_nn;       /* 5     src/lidar_odometry.cpp:456 */
+    float normal_radius;  /* 3000  src/lidar_odometry.cpp:174 */
+    int normal_max_nn;    /* 300   include/bshot_bits.h:66 */
+    float shot_radius;    /* 3000  src/lidar_odometry.cpp:175 */
+    float map_range;      /* 100000 src/lidar_odometry.cpp:198 */
+    int ransac_max_iter;  /* 2000  src/lidar_odometry.cpp:254 */
+    double ransac_thresh; /* 1500  src/lidar_odometry.cpp:256 */
+    int icp_max_iter;     /* 10    (PCL IterativeClosestPoint default, :293-297) */
+    int run_icp;          /* 1     test/odometry_test.cpp:41, include/lidar_odometry.h:50 */
+    int run_iss;          /* 1     ISS runs every frame (src/lidar_odometry.cpp:164-170) */
+} bshot_params;
+
+void bshot_default_params(bshot_params* p);
+
+/* ---- context ------------------------------------------------------------------------------ */
+int bshot_create(bshot_ctx** out, int device, const bshot_params* p);
+void bshot_destroy(bshot_ctx* c);
+const char* bshot_last_error(const bshot_ctx* c);
+int bshot_sync(bshot_ctx* c);
+/* hipStream_t the context launches on (as void*), for callers that time or chain work. */
+void* bshot_stream(bshot_ctx* c);
+
+/* ---- A0: cloud (replaces LidarOdometry::setSrcFrame, src/lidar_odometry.cpp:29-41) ------- */
+int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n);         /* host pointer (H2D copy) */
+int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n); /* device-resident input */
+
+/* ---- A1: segmentation ratio for every point, index order, origin / NaN skipped
+ *      (replaces the loop at src/lidar_odometry.cpp:53-126). idx/ratio caller-sized >= n. --- */
+int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out);
+
+/* ---- A2: keypoint selection = libstdc++ std::sort(ratio) tail (src/lidar_odometry.cpp:131-153).
+ *      Partial introsort: returns exactly the elements/order std::sort leaves in the last k slots. */
+int bshot_select_topk(const int32_t* idx, const float* ratio, int n, int k, int32_t* kp_idx, float* kp_ratio,
+                      int* k_out);
+
+/* ---- A3: ISS keypoints of the current cloud (src/lidar_odometry.cpp:447-461), index order -- */
+int bshot_iss(bshot_ctx* c, int32_t* kp_idx, int cap, int* n_out);
+
+/* ---- A4-A7: normals (persistent mis-indexed array, include/bshot_bits.h:43-94) + SHOT LRF +
+ *      352-bin histogram (bshot_bits.h:113-135) + B-SHOT binarisation (bshot_bits.h:144-278).
+ *      shot (K x 352) and rf (K x 9) are optional (nullable) outputs. */
+int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf, uint32_t* bits);
+/* normals array readback (N x 4: nx, ny, nz, curvature) for tests */
+int bshot_get_normals(bshot_ctx* c, float* out, int n);
+
+/* ---- A9: brute-force Hamming matching, first-index argmin both ways + mutual check
+ *      (src/lidar_odometry.cpp:210-242, minVect include/bshot_bits.h:6-20). -------------- */
+int bshot_match(bshot_ctx* c, const uint32_t* a, int na, const uint32_t* b, int nb, int32_t* left_nn,
+                int32_t* right_nn, int32_t* corr_q, int32_t* corr_m, int* n_corr);
+
+/* ---- A10: RANSAC rejection (src/lidar_odometry.cpp:251-261; PCL SampleConsensus semantics).
+ *      Returns 1 when a model was found, 0 on PCL's identity/all-correspondences fallback. -- */
+int bshot_ransac(const float* src, int ns, const float* tgt, int nt, const int32_t* corr_q, const int32_t* corr_m,
+                 int n_corr, int max_iter, double thresh, float* T_out, int32_t* inl_q, int32_t* inl_m, int* n_inl);
+
+/* ---- A11: point-to-point ICP (PCL IterativeClosestPoint defaults, src/lidar_odometry.cpp:291-297).
+ *      src is already transformed by the initial guess; T_out = ICP final transformation. ---- */
+int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T_out,
+              int* iters);
+
+/* ---- Headless odometry (test/odometry_test.cpp:159-194 frame loop over LidarOdometry) ----- */
+typedef struct bshot_odom bshot_odom;
+typedef struct {
+    int n_points, n_valid_ratios, n_keypoints, n_iss, n_target, n_mutual, n_inliers, icp_iters, gated;
+    float h_diff, t_diff;
+    float T_ransac[16];
+    float pose[16];
+    int map_size;
+    float repeat_sr, repeat_iss;
+} bshot_frame_stats;
+
+int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p);
+void bshot_odom_destroy(bshot_odom* o);
+const char* bshot_odom_last_error(const bshot_odom* o);
+/* one sweep through extract + describe + match + RANSAC + gate + ICP + map update */
+int bshot_odom_process(bshot_odom* o, const float* xyz, int n, bshot_frame_stats* st);
+int bshot_odom_process_device(bshot_odom* o, const float* d_xyz, int n, bshot_frame_stats* st);
+int bshot_odom_get_keypoints(bshot_odom* o, float* xyz, int cap);
+int bshot_odom_get_ratios(bshot_odom* o, float* r, int cap);
+int bshot_odom_get_bits(bshot_odom* o, uint32_t* bits, int cap);
+int bshot_odom_get_target(bshot_odom* o, float* xyz, uint32_t* bits, int cap);
+int bshot_odom_get_inliers(bshot_odom* o, int32_t* q, int32_t* m, int cap);
+int bshot_odom_get_iss(bshot_odom* o, float* xyz, int cap);
+bshot_ctx* bshot_odom_ctx(bshot_odom* o);
+
+/* Map replication (throughput mode, BASELINE config 4): export the last frame's map delta
+ * (K x (xyz, ratio, 11 words) = 60 B records) and import another sequence's delta into a replica. */
+int bshot_odom_map_delta(bshot_odom* o, float* rec, int cap);
+int bshot_odom_replica_insert(bshot_odom* o, int replica, const float* rec, int n);
+int bshot_odom_replica_size(bshot_odom* o, int replica);
+
+/* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's
+ *      stream since the last reset. Stage ids below. */
+enum {
+    BSHOT_STAGE_GRID = 0,
+    BSHOT_STAGE_SR = 1,
+    BSHOT_STAGE_ISS = 2,
+    BSHOT_STAGE_NORMALS = 3,
+    BSHOT_STAGE_SHOT_GATHER = 4,
+    BSHOT_STAGE_SHOT_SORT = 5,
+    BSHOT_STAGE_LRF = 6,
+    BSHOT_STAGE_HIST = 7,
+    BSHOT_STAGE_MATCH = 8,
+    BSHOT_STAGE_ICP = 9,
+    BSHOT_NSTAGES = 10
+};
+int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n);
+void bshot_stage_reset(bshot_ctx* c);
+void bshot_set_timing(bshot_ctx* c, int enabled);
+/* algorithmic work counters of the last describe/SR calls (pair counts), see DESIGN.md §roofline */
+int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

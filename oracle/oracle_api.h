@@ -1,0 +1,74 @@
+/* oracle_api.h -- TEST INFRASTRUCTURE ONLY. C ABI of the CPU restatement (the oracle).
+ * Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+ * PARITY UNPINNED vs PCL (see oracle_core.h). Matrices are row-major 4x4 float. */
+#ifndef BSHOT_ORACLE_API_H
+#define BSHOT_ORACLE_API_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    float seg_radius;       /* 3000  src/lidar_odometry.cpp:68 */
+    int seg_max_nn;         /* 300   :70 */
+    int sr_type;            /* 0 CV, 1 CVS, 2 CVSN  include/lidar_odometry.h:47 */
+    int num_keypoints;      /* 600   src/lidar_odometry.cpp:138 */
+    float iss_salient;      /* 60    :452 */
+    float iss_nonmax;       /* 40    :453 */
+    double iss_gamma21;     /* 0.975 :454 */
+    double iss_gamma32;     /* 0.975 :455 */
+    int iss_min_nn;         /* 5     :456 */
+    float normal_radius;    /* 3000  :174 */
+    int normal_max_nn;      /* 300   include/bshot_bits.h:66 */
+    float shot_radius;      /* 3000  src/lidar_odometry.cpp:175 */
+    float map_range;        /* 100000 :198 */
+    int ransac_max_iter;    /* 2000  :254 */
+    double ransac_thresh;   /* 1500  :256 */
+    int icp_max_iter;       /* 10 (PCL default) */
+    int run_icp;            /* 1     test/odometry_test.cpp:41 */
+    int run_iss;            /* 1 (ISS runs every frame, :164-170) */
+} oracle_params;
+
+typedef struct {
+    int n_points, n_valid_ratios, n_keypoints, n_iss, n_target, n_mutual, n_inliers, icp_iters, gated;
+    float h_diff, t_diff;
+    float T_ransac[16];
+    float pose[16];
+    int map_size;
+    float repeat_sr, repeat_iss; /* kpEvaluation rates (src/lidar_odometry.cpp:392-445) */
+} oracle_frame_stats;
+
+int oracle_seg_ratio(const float* xyz, int n, float radius, int max_nn, int sr_type, int32_t* idx_out,
+                     float* ratio_out, int* n_out);
+int oracle_select_keypoints(const int32_t* idx, const float* ratio, int n, int k, int32_t* kp_idx, float* kp_ratio,
+                            int* k_out);
+int oracle_iss(const float* xyz, int n, float salient, float nonmax, double g21, double g32, int min_nn,
+               int32_t* out_idx, int cap, int* n_out, double* third_eig);
+int oracle_normals(const float* xyz, int n, const float* kps, int k, float radius, int max_nn, float* normals);
+int oracle_shot(const float* xyz, int n, const float* normals, const float* kps, int k, float radius, float* shot,
+                float* rf_out);
+int oracle_binarize(const float* shot, int k, uint32_t* bits);
+int oracle_match(const uint32_t* a, int na, const uint32_t* b, int nb, int32_t* left, int32_t* right,
+                 int32_t* corr_q, int32_t* corr_m, int* ncorr);
+int oracle_ransac(const float* src_xyz, int ns, const float* tgt_xyz, int nt, const int32_t* corr_q,
+                  const int32_t* corr_m, int ncorr, int max_iter, double thresh, float* T_out, int32_t* inl_q,
+                  int32_t* inl_m, int* n_inl);
+int oracle_icp(const float* src_xyz, int ns, const float* tgt_xyz, int nt, int max_iter, float* T_final,
+               int* iters);
+
+void oracle_default_params(oracle_params* p);
+void* oracle_odom_create(const oracle_params* p);
+void oracle_odom_destroy(void* h);
+int oracle_odom_process(void* h, const float* xyz, int n, oracle_frame_stats* st);
+/* per-frame artefacts of the last processed frame; return count (or -needed if cap too small) */
+int oracle_odom_get_keypoints(void* h, float* xyz, int cap);
+int oracle_odom_get_ratios(void* h, float* r, int cap);
+int oracle_odom_get_bits(void* h, uint32_t* bits, int cap);
+int oracle_odom_get_target(void* h, float* xyz, uint32_t* bits, int cap);
+int oracle_odom_get_inliers(void* h, int32_t* q, int32_t* m, int cap);
+int oracle_odom_get_iss(void* h, float* xyz, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
