@@ -54,7 +54,7 @@ ABI_SYMBOLS = [
     "bshot_odom_get_keypoints", "bshot_odom_get_ratios", "bshot_odom_get_bits", "bshot_odom_get_target",
     "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
     "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
-    "bshot_set_timing", "bshot_work_counters",
+    "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs",
 ]
 
 _lib = None
@@ -203,6 +203,11 @@ class Context:
 
     def sync(self):
         self._chk(self.L.bshot_sync(self.h), "sync")
+
+    def radius_pairs(self, R):
+        t = ctypes.c_int64()
+        self._chk(self.L.bshot_radius_pairs(self.h, ctypes.c_float(R), ctypes.byref(t)), "radius_pairs")
+        return t.value
 
 
 def select_topk(idx, ratio, k):

@@ -425,6 +425,26 @@ void bshot_set_timing(bshot_ctx* c, int enabled) {
     if (c) c->timing = enabled != 0;
 }
 
+int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total) {
+    if (!c || !total) return BSHOT_EINVAL;
+    *total = 0;
+    if (c->n == 0) return BSHOT_OK;
+    if (!c->grids_ok) return c->fail("bshot_radius_pairs: no cloud", BSHOT_ESTATE);
+    DBuf<int> cnt;
+    DBuf<long long> offs;
+    HIPCHK(cnt.ensure(c->n), "alloc counts");
+    HIPCHK(offs.ensure(c->n + 1), "alloc offs");
+    const bsh::DevGrid& g = R <= c->prm.iss_salient * 1.5f && c->grid_iss.n == c->n ? c->grid_iss : c->grid_big;
+    HIPCHK(launch_shot_count(g, c->d_xyz, c->n, R, cnt.p, offs.p, c->stream), "radius count");
+    long long t = 0;
+    HIPCHK(hipMemcpyAsync(&t, offs.p + c->n, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync");
+    cnt.release();
+    offs.release();
+    *total = t;
+    return BSHOT_OK;
+}
+
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n) {
     if (!c) return BSHOT_EINVAL;
     for (int i = 0; i < n && i < 8; ++i) out[i] = c->work[i];

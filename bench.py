@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""bench.py -- sweeps/s of the B-SHOT odometry hot path on MI355X (BASELINE.json metric).
+
+One "step" = one synthetic Velodyne-64 sweep (N ~= 130k points, float32 mm, already resident in
+HBM) through extract (SR + top-K + ISS) + describe (normals + SHOT LRF + histogram + B-SHOT) +
+match (map query + Hamming) + RANSAC + gate + ICP + map update, i.e. bshot_odom_process_device.
+Workload = BASELINE config 2 sizes (130k-pt HDL-64 sweep, 2048 keypoints) run as a sequence so
+every step also matches against the map (configs[2] semantics).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+GPU, each running its own sequence (scene seed 42 + rank): frames shard with no data-path
+collective ("scaling": "weak"). --map-bcast additionally all-gathers every frame's map delta
+(K x 60 B) over RCCL and inserts it into per-rank replica maps (BASELINE config 4).
+
+Prints ONE JSON line (rank 0). Roofline / cpu_baseline fields: DESIGN.md "Measurement".
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "b-shot-slam_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import bshot_py  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--keypoints", type=int, default=2048)
+    ap.add_argument("--sensor", type=int, default=0, help="0 HDL-64 (130k), 1 VLP-128 style (256k)")
+    ap.add_argument("--shot-radius", type=float, default=3000.0)
+    ap.add_argument("--map-bcast", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import torch
+
+    dev = torch.device("cuda", local)
+    params = bshot_py.default_params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
+    nframes = a.warmup + a.steps
+    seed = 42 + rank
+    # synthetic sequence for this rank, uploaded to HBM before timing
+    t0 = time.time()
+    frames = []
+    for f in range(nframes):
+        pc, _ = bshot_py.synth_sweep(f, sensor=a.sensor, seed=seed)
+        frames.append(torch.from_numpy(pc).to(dev))
+    torch.cuda.synchronize(dev)
+    gen_s = time.time() - t0
+    npts = [int(x.shape[0]) for x in frames]
+
+    odo = bshot_py.Odometry(device=local, params=params)
+    tot_pts = 0
+
+    def step(i):
+        st = odo.process_device(frames[i].data_ptr(), npts[i])
+        if a.map_bcast and world > 1:
+            rec = torch.from_numpy(odo.map_delta()).to(dev)
+            k = torch.tensor([rec.shape[0]], device=dev)
+            ks = [torch.zeros_like(k) for _ in range(world)]
+            dist.all_gather(ks, k)
+            kmax = int(max(int(x) for x in ks))
+            pad = torch.zeros((kmax, 15), dtype=torch.float32, device=dev)
+            pad[: rec.shape[0]] = rec
+            bufs = [torch.zeros_like(pad) for _ in range(world)]
+            dist.all_gather(bufs, pad)
+            for r in range(world):
+                if r != rank:
+                    odo.replica_insert(r, bufs[r][: int(ks[r])].cpu().numpy())
+        return st
+
+    for i in range(a.warmup):
+        step(i)
+    odo.set_timing(True)
+    odo.stage_reset()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stats = []
+    for i in range(a.warmup, nframes):
+        stats.append(step(i))
+        tot_pts += npts[i]
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    stages = odo.stage_times()
+    odo.set_timing(False)
+    el_max = el
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+    sweeps = a.steps * world
+    value = sweeps / el_max
+
+    # ---- roofline of the dominant kernel: SURVEY.md §8(d) algorithmic bytes / event-timed launches
+    ctx = bshot_py.Context(local, params)
+    last = frames[-1]
+    ctx.set_cloud_device(last.data_ptr(), npts[-1])
+    P_sr = ctx.radius_pairs(params.seg_radius)
+    k_eff = float(np.mean([s.n_keypoints for s in stats]))
+    m_eff = float(np.mean([s.n_target for s in stats]))
+    icp_it = float(np.mean([s.icp_iters for s in stats]))
+    n_eff = float(np.mean(npts[a.warmup:]))
+    ctx.close()
+    dom = max(stages.items(), key=lambda kv: kv[1][0])
+    per_launch_ms = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in stages.items()}
+    # algorithmic bytes per launch (DESIGN.md "Measurement"): pair-gather convention
+    alg = {
+        "seg_ratio": 12.0 * P_sr + 8.0 * n_eff,
+        "match": 88.0 * k_eff * m_eff,
+        "icp": 12.0 * (k_eff + m_eff),
+    }
+    dname = dom[0]
+    roof = None
+    if dname in alg and per_launch_ms[dname] > 0:
+        ach = alg[dname] / (per_launch_ms[dname] * 1e-3) / 1e9
+        roof = {"kernel": dname, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "alg_bytes_per_launch": alg[dname], "ms_per_launch": round(per_launch_ms[dname], 4)}
+
+    # ---- CPU baseline: the oracle (CPU restatement of the reference algorithm), rank 0 only
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        import oracle_ref
+        op = oracle_ref.params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
+        od = oracle_ref.Odometry(op)
+        nf = a.cpu_frames
+        t1 = time.perf_counter()
+        for f in range(nf):
+            od.process(frames[f].cpu().numpy())
+        ct = time.perf_counter() - t1
+        cpu = {"value": round(nf / ct, 4), "unit": "sweeps/s", "cores": os.cpu_count(), "kind": "port",
+               "sample": f"first {nf} sweeps of the same synthetic HDL-64 sequence, full path, oracle/ C++ "
+                         f"restatement (PCL unavailable); SR/ISS/Hamming/RANSAC/ICP 1 thread, SHOT/normals OpenMP",
+               "cpu": platform.processor() or platform.machine()}
+
+    if rank == 0:
+        if a.profile_stages:
+            print(json.dumps({k: [round(v[0], 3), v[1]] for k, v in stages.items()}), file=sys.stderr)
+        line = {
+            "metric": "Velodyne-64 sweeps/sec (extract+match+ICP)",
+            "value": round(value, 3),
+            "unit": "sweeps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el_max / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{'HDL-64' if a.sensor == 0 else 'VLP-128'} synthetic sequence, "
+                                   f"{int(n_eff)} pts/sweep, K={a.keypoints}, SHOT r={a.shot_radius:g} mm, "
+                                   f"full extract+describe+match+RANSAC+ICP+map per sweep",
+                       "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
+                       "icp_iters": icp_it, "parallelism": f"frame-shard x{world}" +
+                       (" + RCCL map bcast" if a.map_bcast else "")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stage_ms_per_sweep": {k: round(v[0] / a.steps, 4) for k, v in stages.items()},
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

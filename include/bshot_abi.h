@@ -149,6 +149,9 @@ void bshot_stage_reset(bshot_ctx* c);
 void bshot_set_timing(bshot_ctx* c, int enabled);
 /* algorithmic work counters of the last describe/SR calls (pair counts), see DESIGN.md §roofline */
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
+/* instrumentation (outside timed regions): sum over all points of the current cloud of
+ * |B(p, R)| (strict d2 < R^2, self included) -> the P_sr / P_iss work figures of SURVEY.md §8(d). */
+int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total);
 
 #ifdef __cplusplus
 }
