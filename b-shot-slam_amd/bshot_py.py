@@ -26,6 +26,7 @@ class Params(ctypes.Structure):
         ("normal_radius", ctypes.c_float), ("normal_max_nn", ctypes.c_int), ("shot_radius", ctypes.c_float),
         ("map_range", ctypes.c_float), ("ransac_max_iter", ctypes.c_int), ("ransac_thresh", ctypes.c_double),
         ("icp_max_iter", ctypes.c_int), ("run_icp", ctypes.c_int), ("run_iss", ctypes.c_int),
+        ("run_kp_eval", ctypes.c_int),
     ]
 
 
@@ -36,11 +37,13 @@ class FrameStats(ctypes.Structure):
         ("n_inliers", ctypes.c_int), ("icp_iters", ctypes.c_int), ("gated", ctypes.c_int),
         ("h_diff", ctypes.c_float), ("t_diff", ctypes.c_float), ("T_ransac", ctypes.c_float * 16),
         ("pose", ctypes.c_float * 16), ("map_size", ctypes.c_int), ("repeat_sr", ctypes.c_float),
-        ("repeat_iss", ctypes.c_float),
+        ("repeat_iss", ctypes.c_float), ("host_ms", ctypes.c_float * 8),
     ]
+    HOST_PHASES = ["extract", "iss", "describe", "match", "ransac", "icp", "map", "kp_eval"]
 
     def as_dict(self):
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("T_ransac", "pose")}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("T_ransac", "pose", "host_ms")}
+        d["host_ms"] = dict(zip(self.HOST_PHASES, list(self.host_ms)))
         d["T_ransac"] = np.array(self.T_ransac, np.float32).reshape(4, 4)
         d["pose"] = np.array(self.pose, np.float32).reshape(4, 4)
         return d
@@ -54,7 +57,7 @@ ABI_SYMBOLS = [
     "bshot_odom_get_keypoints", "bshot_odom_get_ratios", "bshot_odom_get_bits", "bshot_odom_get_target",
     "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
     "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
-    "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs",
+    "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
 ]
 
 _lib = None
@@ -203,6 +206,11 @@ class Context:
 
     def sync(self):
         self._chk(self.L.bshot_sync(self.h), "sync")
+
+    def knn_stats(self):
+        w = (ctypes.c_int64 * 16)()
+        self._chk(self.L.bshot_debug_knn_stats(self.h, w, 16), "knn_stats")
+        return list(w)
 
     def radius_pairs(self, R):
         t = ctypes.c_int64()

@@ -47,7 +47,7 @@ struct bshot_ctx {
     DBuf<float> xyz;          // owned copy (host input path)
     const float* d_xyz = nullptr;
     DBuf<float4> pts4;
-    bsh::DevGrid grid_big, grid_iss;
+    bsh::DevGrid grid_fine, grid_coarse, grid_iss;  // cells seg_radius/8, seg_radius/2, iss_salient
     bool grids_ok = false;
 
     // per-point outputs

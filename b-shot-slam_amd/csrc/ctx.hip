@@ -66,7 +66,8 @@ int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n) {
     HIPCHK(c->pts4.ensure(n > 0 ? n : 1), "alloc pts4");
     if (n == 0) return BSHOT_OK;
     c->stage_begin(BSHOT_STAGE_GRID);
-    HIPCHK(grid_build(c->grid_big, d_xyz, n, c->prm.seg_radius * 0.25f, c->pts4.p, c->stream), "grid build (SR)");
+    HIPCHK(grid_build(c->grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, c->pts4.p, c->stream), "grid build (fine)");
+    HIPCHK(grid_build(c->grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, c->pts4.p, c->stream), "grid build (coarse)");
     c->stage_end();
     c->grids_ok = true;
     return BSHOT_OK;
@@ -79,7 +80,7 @@ int ctx_seg_ratio_dev(bshot_ctx* c) {
     if (c->n == 0) return BSHOT_OK;
     HIPCHK(hipMemsetAsync(c->errw.p, 0, sizeof(int), c->stream), "memset err");
     c->stage_begin(BSHOT_STAGE_SR);
-    HIPCHK(launch_seg_ratio(c->grid_big, c->pts4.p, c->n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+    HIPCHK(launch_seg_ratio(c->grid_fine, c->grid_coarse, c->pts4.p, c->n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
                             c->ratio.p, c->errw.p, c->stream),
            "seg_ratio launch");
     c->stage_end();
@@ -122,13 +123,13 @@ int ctx_describe_dev(bshot_ctx* c, int k) {
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
     c->stage_begin(BSHOT_STAGE_NORMALS);
-    HIPCHK(launch_normals(c->grid_big, c->pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
+    HIPCHK(launch_normals(c->grid_fine, c->grid_coarse, c->pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
                           c->normals.p, c->errw.p, c->stream),
            "normals launch");
     c->stage_end();
     const float R = c->prm.shot_radius;
     c->stage_begin(BSHOT_STAGE_SHOT_GATHER);
-    HIPCHK(launch_shot_count(c->grid_big, c->kps.p, k, R, c->counts.p, c->offs.p, c->stream), "shot count");
+    HIPCHK(launch_shot_count(c->grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, c->stream), "shot count");
     c->stage_end();
     long long total = 0;
     HIPCHK(hipMemcpyAsync(&total, c->offs.p + k, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H total");
@@ -137,7 +138,7 @@ int ctx_describe_dev(bshot_ctx* c, int k) {
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
     c->stage_begin(BSHOT_STAGE_SHOT_GATHER);
-    HIPCHK(launch_shot_gather(c->grid_big, c->kps.p, k, R, c->offs.p, c->seg.p, c->stream), "shot gather");
+    HIPCHK(launch_shot_gather(c->grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, c->stream), "shot gather");
     c->stage_end();
     c->stage_begin(BSHOT_STAGE_SHOT_SORT);
     HIPCHK(launch_shot_sort(c->offs.p, k, R, c->seg.p, c->segtmp.p, c->stream), "shot sort");
@@ -234,6 +235,7 @@ void bshot_default_params(bshot_params* p) {
     p->iss_salient = 60.f; p->iss_nonmax = 40.f; p->iss_gamma21 = 0.975; p->iss_gamma32 = 0.975; p->iss_min_nn = 5;
     p->normal_radius = 3000.f; p->normal_max_nn = 300; p->shot_radius = 3000.f; p->map_range = 100000.f;
     p->ransac_max_iter = 2000; p->ransac_thresh = 1500.0; p->icp_max_iter = 10; p->run_icp = 1; p->run_iss = 1;
+    p->run_kp_eval = 0;
 }
 
 int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
@@ -261,7 +263,8 @@ void bshot_destroy(bshot_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     c->resolve_events();
     for (auto e : c->evpool) (void)hipEventDestroy(e);
-    grid_free(c->grid_big);
+    grid_free(c->grid_fine);
+    grid_free(c->grid_coarse);
     grid_free(c->grid_iss);
     c->xyz.release(); c->pts4.release(); c->ratio.release(); c->third.release(); c->issflag.release();
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
@@ -434,7 +437,7 @@ int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total) {
     DBuf<long long> offs;
     HIPCHK(cnt.ensure(c->n), "alloc counts");
     HIPCHK(offs.ensure(c->n + 1), "alloc offs");
-    const bsh::DevGrid& g = R <= c->prm.iss_salient * 1.5f && c->grid_iss.n == c->n ? c->grid_iss : c->grid_big;
+    const bsh::DevGrid& g = R <= c->prm.iss_salient * 1.5f && c->grid_iss.n == c->n ? c->grid_iss : c->grid_coarse;
     HIPCHK(launch_shot_count(g, c->d_xyz, c->n, R, cnt.p, offs.p, c->stream), "radius count");
     long long t = 0;
     HIPCHK(hipMemcpyAsync(&t, offs.p + c->n, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H");
@@ -443,6 +446,25 @@ int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total) {
     offs.release();
     *total = t;
     return BSHOT_OK;
+}
+
+int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
+    if (!c || !out) return BSHOT_EINVAL;
+    if (!c->grids_ok) return c->fail("bshot_debug_knn_stats: no cloud", BSHOT_ESTATE);
+    DBuf<unsigned long long> k;
+    HIPCHK(k.ensure(16), "alloc kst");
+    HIPCHK(c->ratio.ensure(c->n), "alloc ratio");
+    HIPCHK(c->errw.ensure(1), "alloc err");
+    HIPCHK(hipMemsetAsync(k.p, 0, 16 * sizeof(unsigned long long), c->stream), "memset");
+    HIPCHK(launch_seg_ratio(c->grid_fine, c->grid_coarse, c->pts4.p, c->n, c->prm.seg_radius, c->prm.seg_max_nn,
+                            c->prm.sr_type, c->ratio.p, c->errw.p, c->stream, k.p),
+           "seg_ratio (stats)");
+    unsigned long long h[16];
+    HIPCHK(hipMemcpyAsync(h, k.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync");
+    k.release();
+    for (int i = 0; i < n && i < 16; ++i) out[i] = (int64_t)h[i];
+    return 16;
 }
 
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n) {

@@ -27,8 +27,7 @@ namespace bsk {
 #define SB_BUCKETS 1024
 
 struct CandLds {
-    unsigned int cstart[64];
-    int coff[64];
+    int mark[64];
 };
 
 __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __restrict__ kps, int k, float R,
@@ -40,7 +39,7 @@ __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __r
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         int c = 0;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))
-            for_candidates(g, lds[wave].cstart, lds[wave].coff, kx, ky, kz, R, R2,
+            for_candidates(g, lds[wave].mark, kx, ky, kz, R, R2,
                            [&](bool v, float, unsigned int) { c += __popcll(__ballot(v)); });
         if (lane == 0) counts[q] = c;
     }
@@ -75,14 +74,14 @@ __global__ void __launch_bounds__(256) k_shot_gather(GridView g, const float* __
                                                      const long long* __restrict__ offs,
                                                      unsigned long long* __restrict__ seg) {
     __shared__ CandLds lds[4];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = threadIdx.x >> 6;
     const float R2 = (float)((double)R * (double)R);
     for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         if (!(__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))) continue;
         unsigned long long* out = seg + offs[q];
         int cnt = 0;
-        for_candidates(g, lds[wave].cstart, lds[wave].coff, kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
+        for_candidates(g, lds[wave].mark, kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
             const unsigned long long m = __ballot(v);
             if (v) {
                 const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
@@ -406,19 +405,32 @@ __global__ void __launch_bounds__(64) k_shot_hist(const float4* __restrict__ pts
                         }
                     }
                 }
+                // ordered application: neighbour r's (<= 5, pairwise distinct) bins in one ds_add
+                // instruction, neighbours in rank order (LDS executes one wave's ops in issue
+                // order). Lanes 0..4 each own one record slot; 16 records are loaded into VGPRs
+                // per batch (one LDS wait), then issued as 16 back-to-back ds_add_f32. Unused
+                // records add +0.0f to padding slot 360.
 #pragma unroll
-                for (int j = 0; j < 5; ++j) { rbin[lane * 5 + j] = bins[j]; rval[lane * 5 + j] = vals[j]; }
-                __builtin_amdgcn_wave_barrier();
-                const int cnt = min(64, n - c0);
-                // ordered application: neighbour r's (<= 5, pairwise distinct) bins in one
-                // instruction, neighbours in rank order (LDS executes one wave's ops in order)
-                for (int r = 0; r < cnt; ++r) {
-                    if (lane < 5) {
-                        const int bn = rbin[r * 5 + lane];
-                        if (bn >= 0) atomicAdd(&hist[bn], rval[r * 5 + lane]);
-                    }
-                    __builtin_amdgcn_wave_barrier();
+                for (int j = 0; j < 5; ++j) {
+                    rbin[lane * 5 + j] = bins[j] < 0 ? 360 : bins[j];
+                    rval[lane * 5 + j] = bins[j] < 0 ? 0.f : vals[j];
                 }
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 5) {
+#pragma unroll
+                    for (int g = 0; g < 64; g += 16) {
+                        int bb[16];
+                        float vv[16];
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) {
+                            bb[u] = rbin[(g + u) * 5 + lane];
+                            vv[u] = rval[(g + u) * 5 + lane];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) atomicAdd(&hist[bb[u]], vv[u]);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -427,7 +439,13 @@ __global__ void __launch_bounds__(64) k_shot_hist(const float4* __restrict__ pts
         if (good) {
             double acc = 0.0;
             if (lane == 0)
-                for (int j = 0; j < 352; ++j) { const float h = hist[j]; acc = acc + (double)(h * h); }
+                for (int j = 0; j < 352; j += 8) {
+                    float h[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) h[u] = hist[j + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = acc + (double)(h[u] * h[u]);
+                }
             acc = __shfl(acc, 0, 64);
             const float fa = (float)sqrt(acc);
 #pragma unroll

@@ -20,8 +20,7 @@ namespace bsk {
 struct IssLds {
     unsigned long long list[ISS_CAP];
     double dd[3][ISS_CAP / 2];
-    unsigned int cstart[64];
-    int coff[64];
+    int mark[64];
 };
 
 __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, const float4* __restrict__ pts4, int n,
@@ -40,7 +39,7 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
         double out = 0.0;
         if (__builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
             int cnt = 0;
-            for_candidates(g, L->cstart, L->coff, c.x, c.y, c.z, salient, r2, [&](bool v, float d2, unsigned int idx) {
+            for_candidates(g, L->mark, c.x, c.y, c.z, salient, r2, [&](bool v, float d2, unsigned int idx) {
                 const unsigned long long m = __ballot(v);
                 if (v) {
                     const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),

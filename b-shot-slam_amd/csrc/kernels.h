@@ -6,10 +6,10 @@
 
 namespace bsh {
 
-hipError_t launch_seg_ratio(const DevGrid& g, const float4* pts4, int n, float radius, int max_nn, int sr_type,
-                            float* ratio, int* err, hipStream_t s);
-hipError_t launch_normals(const DevGrid& g, const float4* pts4, const float* kps, int k, float radius, int max_nn,
-                          float4* normals, int* err, hipStream_t s);
+hipError_t launch_seg_ratio(const DevGrid& gf, const DevGrid& gc, const float4* pts4, int n, float radius, int max_nn,
+                            int sr_type, float* ratio, int* err, hipStream_t s, unsigned long long* kst = nullptr);
+hipError_t launch_normals(const DevGrid& gf, const DevGrid& gc, const float4* pts4, const float* kps, int k,
+                          float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* err, hipStream_t s);
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,

@@ -1,16 +1,16 @@
-// knn.hip -- exact radius-capped k-NN on the hashed grid + the two kernels built on it:
+// knn.hip -- exact radius-capped k-NN on the hashed grids + the two kernels built on it:
 //   * k_seg_ratio : A1, segmentation ratio of every point (src/lidar_odometry.cpp:53-126)
 //   * k_normals   : A4, keypoint normals (include/bshot_bits.h:43-94, pcl::computePointNormal)
 //
 // Selection semantics (FLANN KNNRadiusResultSet, sorted): the max_nn smallest (d2, idx) with
 // d2 < r2, in ascending (d2, idx) order. One wavefront per query:
-//   1. radius ladder rs in {r/4, r/2, r}: LDS histogram of d2 over [0, rs^2); stop at the first rs
-//      with >= max_nn hits (then every one of the max_nn nearest lies inside rs) -- exact;
-//   2. histogram refinement (<= 3 levels of 512 buckets) until the boundary bucket fits;
-//   3. collect the prefix into LDS (<= 1024 u64 keys (d2bits<<32 | idx)), bitonic sort;
+//   1. radius ladder rs in {r/8, r/4 (fine grid, cell r/8), r/2, r (coarse grid, cell r/2)}: LDS
+//      histogram of d2 over [0, rs^2); stop at the first rs with >= max_nn hits (then every one of
+//      the max_nn nearest lies strictly inside rs) -- exact;
+//   2. the histogram's crossing bucket bounds the prefix; refine (<= 3 levels x 512 buckets) only
+//      if prefix + boundary bucket exceed the 1024-entry LDS list;
+//   3. collect the prefix into LDS as u64 keys (d2 bits << 32 | idx), bitonic sort;
 //   4. ordered float reductions in rank order exactly as PCL (computeCentroid, covariance).
-// Candidates are streamed cell by cell: 64 cells per round are looked up (one per lane), a wave
-// prefix sum flattens their runs, lanes read consecutive float4s of each run (coalesced).
 #include <hip/hip_runtime.h>
 
 #include "bshot_math.h"
@@ -26,21 +26,20 @@ namespace bsk {
 
 struct KnnLds {
     unsigned int hist[KNN_NB];
+    unsigned int boff[KNN_NB + 1];
+    int mark[64];
     unsigned long long list[KNN_CAP];
-    unsigned int cstart[64];
-    int coff[64];
 };
 
 __device__ __forceinline__ int bucket_of(float d2, float lo, float sc) {
-    float v = (d2 - lo) * sc;
+    const float v = (d2 - lo) * sc;
     int b = (int)v;
     if (!(v >= 0.f)) b = 0;
     if (b > KNN_NB - 1) b = KNN_NB - 1;
     return b;
 }
 
-// wave: find bucket B where the cumulative count crosses `need` (1-based); returns B and the
-// count strictly below B in *below.
+// wave: bucket B where the cumulative count reaches `need` (1-based); *below = count before B
 __device__ __forceinline__ int hist_cross(KnnLds* L, int need, int* below) {
     const int lane = lane_id();
     int s = 0;
@@ -48,14 +47,13 @@ __device__ __forceinline__ int hist_cross(KnnLds* L, int need, int* below) {
     for (int j = 0; j < KNN_NB / 64; ++j) s += (int)L->hist[lane * (KNN_NB / 64) + j];
     int tot;
     const int ex = wave_excl_scan(s, tot);
-    // lane whose range contains the crossing
     const bool mine = ex < need && ex + s >= need;
     const unsigned long long m = __ballot(mine);
     const int owner = m ? (int)__ffsll((long long)m) - 1 : 63;
     int B = 0, bl = 0;
     if (lane == owner) {
         int acc = ex;
-        B = lane * (KNN_NB / 64);
+        B = lane * (KNN_NB / 64) + (KNN_NB / 64) - 1;
         for (int j = 0; j < KNN_NB / 64; ++j) {
             const int h = (int)L->hist[lane * (KNN_NB / 64) + j];
             if (acc + h >= need) { B = lane * (KNN_NB / 64) + j; break; }
@@ -76,20 +74,23 @@ __device__ __forceinline__ void hist_clear(KnnLds* L) {
 }
 
 // Exact selection: leaves the `*need` nearest (d2, idx) sorted in L->list[0, *need).
-// Returns false when the neighbourhood is pathological (> KNN_CAP exactly tied keys at the
-// boundary after 3 refinement levels) -- reported through the error word.
-__device__ bool knn_select(const GridView& g, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
-                           int* need_out) {
+// Returns false when > KNN_CAP keys tie at the boundary after 3 refinement levels (reported).
+// kst (nullable): diagnostic work counters, see bshot_debug_knn_stats()
+__device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, float qx, float qy, float qz, float r,
+                           int max_nn, int* need_out, unsigned long long* kst, const unsigned long long** sorted) {
+    unsigned long long chunks = 0;
     const int lane = lane_id();
     const float r2 = (float)((double)r * (double)r);
-    float rs = r * 0.25f, rs2 = r2;
+    float rs = r, rs2 = r2;
     int total = 0;
-    for (int step = 0; step < 3; ++step) {
-        rs = step == 0 ? r * 0.25f : (step == 1 ? r * 0.5f : r);
-        rs2 = step == 2 ? r2 : (float)((double)rs * (double)rs);
+    int step = 0;
+    for (; step < 4; ++step) {
+        rs = step == 0 ? r * 0.125f : (step == 1 ? r * 0.25f : (step == 2 ? r * 0.5f : r));
+        rs2 = step == 3 ? r2 : (float)((double)rs * (double)rs);
         hist_clear(L);
         const float sc = (float)KNN_NB / rs2;
-        for_candidates(g, L->cstart, L->coff, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+        for_candidates(step < 2 ? gf : gc, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+            ++chunks;
             if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
         });
         __builtin_amdgcn_wave_barrier();
@@ -99,22 +100,24 @@ __device__ bool knn_select(const GridView& g, KnnLds* L, float qx, float qy, flo
         total = wave_sum_i(s);
         if (total >= max_nn) break;
     }
+    if (step > 3) step = 3;
+    const GridView& g = step < 2 ? gf : gc;
     const int need = total < max_nn ? total : max_nn;
     *need_out = need;
     if (need == 0) return true;
-    // bucket path bound: collect candidates with path <= (B[0..lev-1]) lexicographically
     int B[3] = {KNN_NB, KNN_NB, KNN_NB};
     float lo[3] = {0.f, 0.f, 0.f}, sc[3] = {(float)KNN_NB / rs2, 0.f, 0.f};
     int levels = 0;
-    int count_le = total;  // number of candidates the collect pass will take
-    if (total > KNN_CAP) {
+    if (total > need) {
         int below_acc = 0;
         float w = rs2;
         for (int lev = 0; lev < 3; ++lev) {
             if (lev > 0) {
                 hist_clear(L);
                 const int lv = lev;
-                for_candidates(g, L->cstart, L->coff, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+                if (kst && lane == 0) atomicAdd(&kst[7], 1ull);
+                for_candidates(g, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+                    ++chunks;
                     if (!v) return;
                     int b = bucket_of(d2, lo[0], sc[0]);
                     if (b != B[0]) return;
@@ -129,22 +132,88 @@ __device__ bool knn_select(const GridView& g, KnnLds* L, float qx, float qy, flo
             const int Bl = hist_cross(L, need - below_acc, &below);
             B[lev] = Bl;
             levels = lev + 1;
-            const int inb = (int)L->hist[Bl];
             below_acc += below;
-            count_le = below_acc + inb;
-            if (count_le <= KNN_CAP) break;
+            if (below_acc + (int)L->hist[Bl] <= KNN_CAP) break;
             if (lev == 2) return false;
-            // next level range inside bucket Bl
             const float wb = w / (float)KNN_NB;
             lo[lev + 1] = lo[lev] + (float)Bl * wb;
             sc[lev + 1] = (float)KNN_NB / wb;
             w = wb;
         }
     }
-    // collect pass
-    int cnt = 0;
+    // collect the prefix (bucket path <= B lexicographically)
     const int lv = levels;
-    for_candidates(g, L->cstart, L->coff, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+    const int Bmax = lv >= 1 ? B[0] : KNN_NB - 1;
+    int cnt = 0;
+    if (lv <= 1) {
+        // bucket counting sort: level-0 buckets order the prefix by d2; exact (d2, idx) rank inside
+        // each bucket (buckets hold ~1-2 keys). Offsets from the histogram of the final ladder step.
+        int s8 = 0;
+#pragma unroll
+        for (int j = 0; j < KNN_NB / 64; ++j) {
+            const int b = lane * (KNN_NB / 64) + j;
+            s8 += b <= Bmax ? (int)L->hist[b] : 0;
+        }
+        int tot;
+        (void)wave_excl_scan(s8, tot);
+        cnt = tot;
+    }
+    if (lv <= 1 && cnt <= KNN_CAP / 2) {
+        {
+            int s8 = 0;
+#pragma unroll
+            for (int j = 0; j < KNN_NB / 64; ++j) {
+                const int b = lane * (KNN_NB / 64) + j;
+                s8 += b <= Bmax ? (int)L->hist[b] : 0;
+            }
+            int tot;
+            int run = wave_excl_scan(s8, tot);
+#pragma unroll
+            for (int j = 0; j < KNN_NB / 64; ++j) {
+                const int b = lane * (KNN_NB / 64) + j;
+                const int h = b <= Bmax ? (int)L->hist[b] : 0;
+                L->boff[b] = (unsigned)run;
+                L->hist[b] = (unsigned)run;  // cursor
+                run += h;
+            }
+            if (lane == 63) L->boff[KNN_NB] = (unsigned)tot;
+            __builtin_amdgcn_wave_barrier();
+        }
+        const float sc0 = sc[0];
+        for_candidates(g, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+            ++chunks;
+            if (v) {
+                const int b = bucket_of(d2, 0.f, sc0);
+                if (b <= Bmax) {
+                    const unsigned pos = atomicAdd(&L->hist[b], 1u);
+                    L->list[pos] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+                }
+            }
+        });
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long* out = L->list + KNN_CAP / 2;
+        for (int i = lane; i < cnt; i += 64) {
+            const unsigned long long key = L->list[i];
+            const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
+            const unsigned s0 = L->boff[b], e0 = L->boff[b + 1];
+            unsigned rank = 0;
+            for (unsigned j = s0; j < e0; ++j) rank += L->list[j] < key ? 1u : 0u;
+            out[s0 + rank] = key;
+        }
+        __builtin_amdgcn_wave_barrier();
+        *sorted = out;
+        if (kst && lane == 0) {
+            atomicAdd(&kst[0], 1ull);
+            atomicAdd(&kst[1 + step], 1ull);
+            atomicAdd(&kst[5], chunks);
+            atomicAdd(&kst[9], (unsigned long long)need);
+            atomicAdd(&kst[10], (unsigned long long)total);
+        }
+        return true;
+    }
+    cnt = 0;
+    for_candidates(g, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        ++chunks;
         bool take = v;
         if (take && lv > 0) {
             const int b0 = bucket_of(d2, lo[0], sc[0]);
@@ -159,7 +228,8 @@ __device__ bool knn_select(const GridView& g, KnnLds* L, float qx, float qy, flo
         }
         const unsigned long long m = __ballot(take);
         if (take) {
-            const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
             if (slot < KNN_CAP) L->list[slot] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
         }
         cnt += __popcll(m);
@@ -167,17 +237,74 @@ __device__ bool knn_select(const GridView& g, KnnLds* L, float qx, float qy, flo
     if (cnt > KNN_CAP) return false;
     int P = 64;
     while (P < cnt) P <<= 1;
+    if (kst && lane == 0) {
+        atomicAdd(&kst[0], 1ull);
+        atomicAdd(&kst[1 + step], 1ull);
+        atomicAdd(&kst[5], chunks);
+        atomicAdd(&kst[8], (unsigned long long)P);
+        atomicAdd(&kst[9], (unsigned long long)need);
+        atomicAdd(&kst[10], (unsigned long long)total);
+    }
     for (int i = cnt + lane; i < P; i += 64) L->list[i] = ~0ull;
     __builtin_amdgcn_wave_barrier();
     wave_bitonic(L->list, P);
+    *sorted = L->list;
     return true;
 }
 
+// sequential float sum of a[0, n) in index order (8 loads in flight, dependent adds)
+__device__ __forceinline__ float seq_sum(const float* a, int n) {
+    float acc = 0.f;
+    int r = 0;
+    for (; r + 8 <= n; r += 8) {
+        const float a0 = a[r], a1 = a[r + 1], a2 = a[r + 2], a3 = a[r + 3];
+        const float a4 = a[r + 4], a5 = a[r + 5], a6 = a[r + 6], a7 = a[r + 7];
+        acc = acc + a0; acc = acc + a1; acc = acc + a2; acc = acc + a3;
+        acc = acc + a4; acc = acc + a5; acc = acc + a6; acc = acc + a7;
+    }
+    for (; r < n; ++r) acc = acc + a[r];
+    return acc;
+}
+
+__device__ __forceinline__ float seq_dot(const float* a, const float* b, int n) {
+    float acc = 0.f;
+    int r = 0;
+    for (; r + 4 <= n; r += 4) {
+        const float p0 = a[r] * b[r], p1 = a[r + 1] * b[r + 1], p2 = a[r + 2] * b[r + 2], p3 = a[r + 3] * b[r + 3];
+        acc = acc + p0; acc = acc + p1; acc = acc + p2; acc = acc + p3;
+    }
+    for (; r < n; ++r) acc = acc + a[r] * b[r];
+    return acc;
+}
+
+// gather neighbour coordinates (rank order) into the LDS list region as 3 float arrays of 512
+__device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, const float4* __restrict__ pts4, int need,
+                                           float* fl) {
+    const int lane = lane_id();
+    unsigned int myidx[KNN_CAP / 128];
+#pragma unroll
+    for (int j = 0; j < KNN_CAP / 128; ++j) {
+        const int r = lane + 64 * j;
+        myidx[j] = r < need ? (unsigned int)(sorted[r] & 0xFFFFFFFFu) : 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < KNN_CAP / 128; ++j) {
+        const int r = lane + 64 * j;
+        if (r < need) {
+            const float4 p = pts4[myidx[j]];
+            fl[r] = p.x; fl[512 + r] = p.y; fl[1024 + r] = p.z;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ------------------------------------------------------------------------------------------
-// A1: segmentation ratio of every point
-__global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView g, const float4* __restrict__ pts4, int n,
-                                                              float radius, int max_nn, int sr_type,
-                                                              float* __restrict__ ratio, int* __restrict__ err) {
+// A1: segmentation ratio of every point. max_nn <= 512 (host-checked).
+__global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView gf, GridView gc, const float4* __restrict__ pts4,
+                                                              int n, float radius, int max_nn, int sr_type,
+                                                              float* __restrict__ ratio, int* __restrict__ err,
+                                                              unsigned long long* __restrict__ kst) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
@@ -186,7 +313,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView g, const 
     const int xg = b & 7, gi = b >> 3, ng = (G + 7 - xg) >> 3;
     const int per = (n + 7) >> 3;
     const int q_begin = xg * per, q_end = min(n, q_begin + per);
-    float* fl = reinterpret_cast<float*>(L->list);  // reused after selection: x[0..511], y, z...
+    float* fl = reinterpret_cast<float*>(L->list);
     for (int q = q_begin + gi * KNN_WAVES + wave; q < q_end; q += ng * KNN_WAVES) {
         const float4 sp = pts4[q];
         float out = __builtin_nanf("");
@@ -194,45 +321,24 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView g, const 
         const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
         if (!origin && fin) {
             int need = 0;
-            if (!knn_select(g, L, sp.x, sp.y, sp.z, radius, max_nn, &need)) {
+            const unsigned long long* sorted = nullptr;
+            if (!knn_select(gf, gc, L, sp.x, sp.y, sp.z, radius, max_nn, &need, kst, &sorted)) {
                 if (lane == 0) atomicOr(err, 1);
             } else if (need > 0) {
-                // gather neighbour coordinates (rank order) into LDS (overlaying the key list)
-                unsigned int myidx[KNN_CAP / 64];
-#pragma unroll
-                for (int j = 0; j < KNN_CAP / 64; ++j) {
-                    const int r = lane + 64 * j;
-                    myidx[j] = r < need ? (unsigned int)(L->list[r] & 0xFFFFFFFFu) : 0u;
-                }
-                __builtin_amdgcn_wave_barrier();
-                float px[KNN_CAP / 64], py[KNN_CAP / 64], pz[KNN_CAP / 64];
-#pragma unroll
-                for (int j = 0; j < KNN_CAP / 64; ++j) {
-                    const int r = lane + 64 * j;
-                    if (r < need) {
-                        const float4 p = pts4[myidx[j]];
-                        px[j] = p.x; py[j] = p.y; pz[j] = p.z;
-                        fl[r] = p.x; fl[512 + r] = p.y; fl[1024 + r] = p.z;
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
+                gather_xyz(sorted, pts4, need, fl);
                 // pcl::computeCentroid: sequential float sums in rank order (lanes 0,1,2)
                 float acc = 0.f;
-                if (lane < 3) {
-                    const float* src = fl + 512 * lane;
-                    for (int r = 0; r < need; ++r) acc = acc + src[r];
-                }
+                if (lane < 3) acc = seq_sum(fl + 512 * lane, need);
                 const float fn = (float)need;
                 const float cx = __shfl(acc, 0, 64) / fn, cy = __shfl(acc, 1, 64) / fn, cz = __shfl(acc, 2, 64) / fn;
                 const float tx = sp.x - cx, ty = sp.y - cy, tz = sp.z - cz;
                 if (sr_type == 0) {
                     int pos = 0, neg = 0;
-#pragma unroll
-                    for (int j = 0; j < KNN_CAP / 64; ++j) {
-                        const int r = lane + 64 * j;
+                    for (int r0 = 0; r0 < need; r0 += 64) {
+                        const int r = r0 + lane;
                         bool p = false, m = false;
                         if (r < need) {
-                            const float vx = px[j] - sp.x, vy = py[j] - sp.y, vz = pz[j] - sp.z;
+                            const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
                             const float dot = (tx * vx + ty * vy) + tz * vz;
                             p = dot > 0.f;
                             m = dot < 0.f;
@@ -242,17 +348,15 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView g, const 
                     }
                     const float fp = (float)pos, fm = (float)neg;
                     out = 1.0f - fminf(fp, fm) / fmaxf(fp, fm);
-                    if (fp != fp || fm != fm) out = __builtin_nanf("");
                 } else {
                     // CVS / CVSN: per-neighbour terms in parallel, sequential float sum in rank order
                     const float ctn = sqrtf((tx * tx + ty * ty) + tz * tz);
-                    float* term = fl + 1536;  // 512 entries
+                    float* term = fl + 1536;
                     unsigned int* use = reinterpret_cast<unsigned int*>(L->hist);
-#pragma unroll
-                    for (int j = 0; j < KNN_CAP / 64; ++j) {
-                        const int r = lane + 64 * j;
-                        if (r < need && r < 512) {
-                            const float vx = px[j] - sp.x, vy = py[j] - sp.y, vz = pz[j] - sp.z;
+                    for (int r0 = 0; r0 < need; r0 += 64) {
+                        const int r = r0 + lane;
+                        if (r < need) {
+                            const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
                             const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
                             const float dot = (tx * vx + ty * vy) + tz * vz;
                             use[r] = (ctn == 0.f || vn == 0.f) ? 0u : 1u;
@@ -276,7 +380,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView g, const 
 
 // ------------------------------------------------------------------------------------------
 // A4: normals of K keypoints written to slots [0, K) of the persistent N-sized array
-__global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView g, const float4* __restrict__ pts4,
+__global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView gf, GridView gc, const float4* __restrict__ pts4,
                                                             const float* __restrict__ kps, int k, float radius,
                                                             int max_nn, float4* __restrict__ normals,
                                                             int* __restrict__ err) {
@@ -288,42 +392,20 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView g, const fl
     for (int q = blockIdx.x * KNN_WAVES + wave; q < k; q += gridDim.x * KNN_WAVES) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         float nx = qn, ny = qn, nz = qn, curv = qn;
-        bool write_nan_all = true;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
             int need = 0;
-            if (!knn_select(g, L, kx, ky, kz, radius, max_nn, &need)) {
+            const unsigned long long* sorted = nullptr;
+            if (!knn_select(gf, gc, L, kx, ky, kz, radius, max_nn, &need, nullptr, &sorted)) {
                 if (lane == 0) atomicOr(err, 2);
             } else if (need > 0) {
-                write_nan_all = false;
                 if (need >= 3) {
-                    unsigned int myidx[KNN_CAP / 64];
-#pragma unroll
-                    for (int j = 0; j < KNN_CAP / 64; ++j) {
-                        const int r = lane + 64 * j;
-                        myidx[j] = r < need ? (unsigned int)(L->list[r] & 0xFFFFFFFFu) : 0u;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                    for (int j = 0; j < KNN_CAP / 64; ++j) {
-                        const int r = lane + 64 * j;
-                        if (r < need) {
-                            const float4 p = pts4[myidx[j]];
-                            fl[r] = p.x; fl[512 + r] = p.y; fl[1024 + r] = p.z;
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    // pcl::computeMeanAndCovarianceMatrix: 9 float accumulators, rank order
+                    gather_xyz(sorted, pts4, need, fl);
+                    // pcl::computeMeanAndCovarianceMatrix: 9 float accumulators in rank order
                     float acc = 0.f;
                     if (lane < 9) {
                         const int a = lane < 6 ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
                         const int bsel = lane < 6 ? (lane < 3 ? lane : (lane < 5 ? lane - 2 : 2)) : -1;
-                        const float* A = fl + 512 * a;
-                        if (bsel >= 0) {
-                            const float* Bv = fl + 512 * bsel;
-                            for (int r = 0; r < need; ++r) acc = acc + A[r] * Bv[r];
-                        } else {
-                            for (int r = 0; r < need; ++r) acc = acc + A[r];
-                        }
+                        acc = bsel >= 0 ? seq_dot(fl + 512 * a, fl + 512 * bsel, need) : seq_sum(fl + 512 * a, need);
                     }
                     float ac[9];
 #pragma unroll
@@ -350,7 +432,6 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView g, const fl
                 if (cth < 0.f) { nx *= -1.f; ny *= -1.f; nz *= -1.f; }
             }
         }
-        (void)write_nan_all;
         if (lane == 0) normals[q] = make_float4(nx, ny, nz, curv);
         __builtin_amdgcn_wave_barrier();
     }
@@ -362,22 +443,24 @@ size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES; }
 
 namespace bsh {
 
-hipError_t launch_seg_ratio(const bsh::DevGrid& g, const float4* pts4, int n, float radius, int max_nn, int sr_type,
-                            float* ratio, int* err, hipStream_t s) {
+hipError_t launch_seg_ratio(const DevGrid& gf, const DevGrid& gc, const float4* pts4, int n, float radius, int max_nn,
+                            int sr_type, float* ratio, int* err, hipStream_t s, unsigned long long* kst) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     if (blocks > 8 * 256 * 4) blocks = 8 * 256 * 4;
     blocks = (blocks + 7) & ~7;
-    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(g.view(), pts4, n, radius, max_nn, sr_type, ratio, err);
+    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(gf.view(), gc.view(), pts4, n, radius, max_nn, sr_type, ratio,
+                                                         err, kst);
     return hipGetLastError();
 }
 
-hipError_t launch_normals(const bsh::DevGrid& g, const float4* pts4, const float* kps, int k, float radius, int max_nn,
-                          float4* normals, int* err, hipStream_t s) {
+hipError_t launch_normals(const DevGrid& gf, const DevGrid& gc, const float4* pts4, const float* kps, int k,
+                          float radius, int max_nn, float4* normals, int* err, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (k + KNN_WAVES - 1) / KNN_WAVES;
-    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(g.view(), pts4, kps, k, radius, max_nn, normals, err);
+    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(gf.view(), gc.view(), pts4, kps, k, radius, max_nn, normals,
+                                                       err);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 
 #include "../csrc/ctx.h"
 #include "geom.h"
+#include "../../include/bshot/tic_toc.h"
 
 namespace myslam {
 
@@ -87,6 +88,7 @@ static PointCloudXYZ gather_points(bshot_ctx* c, const std::vector<int32_t>& idx
 
 void LidarOdometry::extractKeypoints() {
     zero_stats(stats_);
+    TicToc t_ex;
     const int n = src_n_;
     stats_.n_points = n;
     // A1 + A2 (src/lidar_odometry.cpp:51-153)
@@ -106,6 +108,8 @@ void LidarOdometry::extractKeypoints() {
     }
     cloud1_kps_ = *src_->getKeypoints();
     cloud2_kps_ = *ref_->getKeypoints();
+    stats_.host_ms[0] = (float)t_ex.toc();
+    TicToc t_iss;
     // A3 ISS (src/lidar_odometry.cpp:164-170): computed every frame, used by kpEvaluation only
     isskps_src.clear();
     if (prm_.run_iss) {
@@ -117,10 +121,12 @@ void LidarOdometry::extractKeypoints() {
     }
     stats_.n_iss = (int)isskps_src.size();
     if (isInitial()) isskps_ref = isskps_src;
+    stats_.host_ms[1] = (float)t_iss.toc();
 }
 
 void LidarOdometry::computeDescriptors() {
     // A4-A7 (src/lidar_odometry.cpp:173-184); keypoints are already on the device (ctx->kps)
+    TicToc t_d;
     const int k = (int)cloud1_kps_.size();
     check(bsh::ctx_describe_dev(ctx_, k), "describe");
     std::vector<uint32_t> words(11 * (size_t)(k > 0 ? k : 1));
@@ -141,10 +147,12 @@ void LidarOdometry::computeDescriptors() {
         desc->push_back(cloud1_bshot_[i].bits);
     }
     src_->setDescriptors(desc);
+    stats_.host_ms[2] = (float)t_d.toc();
 }
 
 void LidarOdometry::featureMatching() {
     // src/lidar_odometry.cpp:186-265
+    TicToc t_m;
     if (isInitial()) {
         passSrc2Ref();
         ref_->setKeypoints(src_->getKeypoints());
@@ -166,6 +174,8 @@ void LidarOdometry::featureMatching() {
     int nc = 0;
     check(bshot_match(ctx_, a.data(), na, b.data(), nb, left.data(), right.data(), cq.data(), cm.data(), &nc), "match");
     stats_.n_mutual = nc;
+    stats_.host_ms[3] = (float)t_m.toc();
+    TicToc t_r;
     // RANSAC rejection (maxIter 2000, threshold 1500 mm)
     std::vector<int32_t> iq(nc > 0 ? nc : 1), im(nc > 0 ? nc : 1);
     int ni = 0;
@@ -177,6 +187,7 @@ void LidarOdometry::featureMatching() {
     corr_.resize(ni);
     for (int i = 0; i < ni; ++i) corr_[i] = std::make_pair(iq[i], im[i]);
     stats_.n_inliers = ni;
+    stats_.host_ms[4] = (float)t_r.toc();
 }
 
 void LidarOdometry::evaluateEstimation() {
@@ -199,6 +210,7 @@ void LidarOdometry::evaluateEstimation() {
         shouldUpdateMap = true;
     }
     // ICP always runs (:291-297), source = cloud1 keypoints transformed by T_est
+    TicToc t_icp;
     const int k = (int)cloud1_kps_.size(), m = (int)cloud2_kps_.size();
     std::vector<float> src(3 * (size_t)(k > 0 ? k : 1));
     for (int i = 0; i < k; ++i) {
@@ -209,6 +221,7 @@ void LidarOdometry::evaluateEstimation() {
     int iters = 0;
     check(bshot_icp(ctx_, src.data(), k, m ? &cloud2_kps_[0][0] : nullptr, m, prm_.icp_max_iter, Ticp, &iters), "icp");
     stats_.icp_iters = iters;
+    stats_.host_ms[5] = (float)t_icp.toc();
     Matrix4f F;
     std::memcpy(F.m, Ticp, sizeof(Ticp));
     T_best_ = run_icp_ ? F * T_est : T_j;
@@ -225,6 +238,7 @@ void LidarOdometry::poseEstimation() { src_->setPose(T_best_); }
 
 void LidarOdometry::updateMap() {
     // src/lidar_odometry.cpp:344-376 (shouldUpdateMap is never read by the reference)
+    TicToc t_map;
     const Matrix3f R = T_best_.block33();
     const Vector3f T = T_best_.topRightCorner();
     Frame::PCPtr kps = src_->getKeypoints();
@@ -237,6 +251,7 @@ void LidarOdometry::updateMap() {
     std::memcpy(stats_.T_ransac, T_ransac_.m, sizeof(stats_.T_ransac));
     std::memcpy(stats_.pose, T_best_.m, sizeof(stats_.pose));
     stats_.map_size = globalMap_.size();
+    stats_.host_ms[6] = (float)t_map.toc();
 }
 
 void LidarOdometry::updateCorrespondence() {
@@ -263,8 +278,10 @@ static float repeat_rate(const PointCloudXYZ& src, const PointCloudXYZ& ref) {
 
 void LidarOdometry::kpEvaluation() {
     // src/lidar_odometry.cpp:392-445: 1-NN repeatability (<= 30 mm) of SR and ISS keypoints
+    TicToc t_kp;
     stats_.repeat_sr = repeat_rate(*src_->getKeypoints(), *ref_->getKeypoints());
     stats_.repeat_iss = repeat_rate(isskps_src, isskps_ref);
+    stats_.host_ms[7] = (float)t_kp.toc();
 }
 
 PointCloudXYZ LidarOdometry::issKpDetection(const PointCloudXYZ& kps) {

@@ -40,7 +40,7 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     lo.featureMatching();
     lo.evaluateEstimation();
     lo.poseEstimation();
-    lo.kpEvaluation();
+    if (o->lo->params().run_kp_eval) lo.kpEvaluation();
     lo.updateMap();
     lo.updateCorrespondence();
     if (st) *st = lo.lastStats();

@@ -27,19 +27,13 @@ class bshot_descriptor {
 
 namespace myslam {
 // bit j of the bitset <-> bit (j % 32) of word j / 32 (11 words); the same layout the C ABI uses.
-inline void bits_to_words(const std::bitset<352>& b, uint32_t w[11]) {
-    for (int q = 0; q < 11; ++q) {
-        uint32_t x = 0;
-        for (int j = 0; j < 32; ++j)
-            if (b.test(q * 32 + j)) x |= 1u << j;
-        w[q] = x;
-    }
-}
+// libstdc++ stores std::bitset<352> as unsigned long[6] with bit j at word j/64, bit j%64, so on
+// little-endian x86-64 its first 44 bytes ARE the 11 words (checked in tests/test_host.py).
+static_assert(sizeof(std::bitset<352>) == 48, "unexpected std::bitset<352> layout");
+inline void bits_to_words(const std::bitset<352>& b, uint32_t w[11]) { std::memcpy(w, &b, 44); }
 inline std::bitset<352> words_to_bits(const uint32_t w[11]) {
     std::bitset<352> b;
-    for (int q = 0; q < 11; ++q)
-        for (int j = 0; j < 32; ++j)
-            if ((w[q] >> j) & 1u) b.set(q * 32 + j);
+    std::memcpy(&b, w, 44);
     return b;
 }
 }  // namespace myslam

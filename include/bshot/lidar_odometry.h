@@ -62,6 +62,7 @@ class LidarOdometry {
 
     // extensions (not in the reference)
     const bshot_frame_stats& lastStats() const { return stats_; }
+    const bshot_params& params() const { return prm_; }
     bshot_ctx* context() { return ctx_; }
     const std::vector<float>& segRatios() const { return seg_ratios_; }
     const PointCloudXYZ& targetKeypoints() const { return cloud2_kps_; }

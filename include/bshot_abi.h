@@ -48,6 +48,7 @@ typedef struct {
     int icp_max_iter;     /* 10    (PCL IterativeClosestPoint default, :293-297) */
     int run_icp;          /* 1     test/odometry_test.cpp:41, include/lidar_odometry.h:50 */
     int run_iss;          /* 1     ISS runs every frame (src/lidar_odometry.cpp:164-170) */
+    int run_kp_eval;      /* 0     kpEvaluation per frame: kp_test yes (test/kp_test.cpp:166), odometry_test no */
 } bshot_params;
 
 void bshot_default_params(bshot_params* p);
@@ -107,6 +108,9 @@ typedef struct {
     float pose[16];
     int map_size;
     float repeat_sr, repeat_iss;
+    /* host wall ms per phase (TicToc, include/tic_toc.h): extract(SR+topK), iss, describe,
+       match (map query + Hamming), ransac, icp, map update, kp_eval */
+    float host_ms[8];
 } bshot_frame_stats;
 
 int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p);
@@ -152,6 +156,10 @@ int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
 /* instrumentation (outside timed regions): sum over all points of the current cloud of
  * |B(p, R)| (strict d2 < R^2, self included) -> the P_sr / P_iss work figures of SURVEY.md §8(d). */
 int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total);
+/* diagnostic: re-run the SR kernel with work counters: [0] queries, [1..4] ladder step reached
+ * (r/8, r/4, r/2, r), [5] 64-candidate chunks streamed, [7] refinement passes, [8] sum of bitonic
+ * sizes, [9] sum of selected neighbours, [10] sum of in-radius candidates at the final step. */
+int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n);
 
 #ifdef __cplusplus
 }
