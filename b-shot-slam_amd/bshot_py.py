@@ -58,6 +58,8 @@ ABI_SYMBOLS = [
     "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
     "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
     "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
+    "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
+    "bshot_map_block_id",
 ]
 
 _lib = None
@@ -74,6 +76,8 @@ def lib():
         _lib.bshot_odom_last_error.restype = ctypes.c_char_p
         _lib.bshot_stream.restype = P
         _lib.bshot_odom_ctx.restype = P
+        _lib.bshot_map_create.restype = P
+        _lib.bshot_map_block_id.restype = ctypes.c_uint64
     return _lib
 
 
@@ -347,6 +351,42 @@ class Odometry:
 
     def stage_reset(self):
         self.L.bshot_stage_reset(P(self.context()))
+
+
+class KeypointMap:
+    """Host keypoint map (myslam::Map) through the C ABI; no GPU needed."""
+
+    def __init__(self):
+        self.L = lib()
+        self.h = P(self.L.bshot_map_create())
+
+    def __del__(self):
+        try:
+            self.L.bshot_map_destroy(self.h)
+        except Exception:
+            pass
+
+    def add(self, xyz, ratio, bits):
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        bits = np.ascontiguousarray(bits, np.uint32)
+        return self.L.bshot_map_add(self.h, _ptr(xyz), ctypes.c_float(ratio), _ptr(bits))
+
+    def query(self, pos, rng=100000.0, cap=1 << 16):
+        pos = np.ascontiguousarray(pos, np.float32)
+        xyz = np.zeros((cap, 3), np.float32)
+        bits = np.zeros((cap, 11), np.uint32)
+        n = self.L.bshot_map_query(self.h, _ptr(pos), ctypes.c_float(rng), _ptr(xyz), _ptr(bits), cap)
+        if n < 0:
+            return self.query(pos, rng, -n)
+        return xyz[:n].copy(), bits[:n].copy()
+
+    def size(self):
+        return self.L.bshot_map_size(self.h)
+
+    @staticmethod
+    def block_id(pos):
+        pos = np.ascontiguousarray(pos, np.float32)
+        return int(lib().bshot_map_block_id(_ptr(pos)))
 
 
 # ---------------------------------------------------------------- synthetic input (not the product)

@@ -6,6 +6,7 @@
 #include "../../include/bshot/keypoint.h"
 #include "../../include/bshot/mymap.h"
 #include "geom.h"
+#include "../../include/bshot_abi.h"
 
 namespace myslam {
 
@@ -129,3 +130,45 @@ void Map::getBlockKeypoints(std::vector<KPointCloud>& kpc) {
 }
 
 }  // namespace myslam
+
+// ---------------------------------------------------------------- host-only Map C ABI
+struct bshot_map {
+    myslam::Map m;
+};
+
+extern "C" {
+
+bshot_map* bshot_map_create(void) { return new bshot_map(); }
+void bshot_map_destroy(bshot_map* m) { delete m; }
+
+int bshot_map_add(bshot_map* m, const float* xyz, float ratio, const uint32_t* bits11) {
+    if (!m || !xyz || !bits11) return BSHOT_EINVAL;
+    myslam::Vector3f p(xyz[0], xyz[1], xyz[2]);
+    bshot_descriptor d;
+    d.bits = myslam::words_to_bits(bits11);
+    m->m.addKeypoint(myslam::Keypoint::createKeypoint(p, ratio, d));
+    return BSHOT_OK;
+}
+
+int bshot_map_query(bshot_map* m, const float* pos, float range, float* xyz, uint32_t* bits, int cap) {
+    if (!m || !pos) return BSHOT_EINVAL;
+    myslam::PointCloudXYZ k;
+    std::vector<bshot_descriptor> d;
+    m->m.getKeypoints(myslam::Vector3f(pos[0], pos[1], pos[2]), range, k, d);
+    const int n = (int)k.size();
+    if (n > cap) return -n;
+    for (int i = 0; i < n; ++i) {
+        if (xyz) { xyz[3 * i] = k[i][0]; xyz[3 * i + 1] = k[i][1]; xyz[3 * i + 2] = k[i][2]; }
+        if (bits) myslam::bits_to_words(d[i].bits, bits + 11 * (size_t)i);
+    }
+    return n;
+}
+
+int bshot_map_size(bshot_map* m) { return m ? m->m.size() : 0; }
+
+uint64_t bshot_map_block_id(const float* pos) {
+    myslam::Map tmp;
+    return (uint64_t)tmp.getBlockID(myslam::Vector3f(pos[0], pos[1], pos[2]));
+}
+
+}  // extern "C"

@@ -133,6 +133,18 @@ int bshot_odom_map_delta(bshot_odom* o, float* rec, int cap);
 int bshot_odom_replica_insert(bshot_odom* o, int replica, const float* rec, int n);
 int bshot_odom_replica_size(bshot_odom* o, int replica);
 
+/* ---- Keypoint map (host; include/mymap.h:9-51, src/mymap.cpp, src/keypoint.cpp): the same
+ *      unordered_map blocks, hasher, 10 mm keypoint grid and 800 mm suppression. No GPU needed. */
+typedef struct bshot_map bshot_map;
+bshot_map* bshot_map_create(void);
+void bshot_map_destroy(bshot_map* m);
+/* Keypoint::createKeypoint(pos, ratio, bits) + Map::addKeypoint */
+int bshot_map_add(bshot_map* m, const float* xyz, float ratio, const uint32_t* bits11);
+/* Map::getKeypoints(pos, range): returns count (or -needed when cap is too small) */
+int bshot_map_query(bshot_map* m, const float* pos, float range, float* xyz, uint32_t* bits, int cap);
+int bshot_map_size(bshot_map* m);
+uint64_t bshot_map_block_id(const float* pos);
+
 /* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's
  *      stream since the last reset. Stage ids below. */
 enum {

@@ -56,6 +56,12 @@ int oracle_ransac(const float* src_xyz, int ns, const float* tgt_xyz, int nt, co
 int oracle_icp(const float* src_xyz, int ns, const float* tgt_xyz, int nt, int max_iter, float* T_final,
                int* iters);
 
+/* test hooks: exact radius search (FLANN semantics), Jacobi eigen, umeyama */
+int oracle_radius_search(const float* xyz, int n, const float* q, float radius, int max_nn, int32_t* idx,
+                         float* d2, int cap);
+void oracle_eig3(const double* a9, double* w3, double* v9);
+void oracle_umeyama(const double* src, const double* dst, int n, int use_float, double* T16);
+
 void oracle_default_params(oracle_params* p);
 void* oracle_odom_create(const oracle_params* p);
 void oracle_odom_destroy(void* h);

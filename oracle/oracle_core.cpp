@@ -725,3 +725,34 @@ int oracle_icp(const float* src_xyz, int ns, const float* tgt_xyz, int nt, int m
 }
 
 }  // extern "C"
+
+extern "C" {
+
+int oracle_radius_search(const float* xyz, int n, const float* q, float radius, int max_nn, int32_t* idx, float* d2,
+                         int cap) {
+    const P3* pts = reinterpret_cast<const P3*>(xyz);
+    Grid g(pts, n, radius * 0.25f);
+    std::vector<std::pair<float, int>> nn;
+    const P3 qq = {q[0], q[1], q[2]};
+    if (max_nn > 0) g.radius_knn(qq, radius, max_nn, nn);
+    else g.radius_all(qq, (float)((double)radius * (double)radius), nn);
+    const int m = (int)nn.size();
+    for (int i = 0; i < m && i < cap; ++i) { idx[i] = nn[i].second; d2[i] = nn[i].first; }
+    return m;
+}
+
+void oracle_eig3(const double* a9, double* w3, double* v9) { o_jacobi3(a9, w3, v9); }
+
+void oracle_umeyama(const double* src, const double* dst, int n, int use_float, double* T16) {
+    if (use_float) {
+        std::vector<float> s(3 * (size_t)n), d(3 * (size_t)n);
+        for (int i = 0; i < 3 * n; ++i) { s[i] = (float)src[i]; d[i] = (float)dst[i]; }
+        float T[16];
+        o_umeyama<float>(s.data(), d.data(), n, T);
+        for (int i = 0; i < 16; ++i) T16[i] = T[i];
+    } else {
+        o_umeyama<double>(src, dst, n, T16);
+    }
+}
+
+}  // extern "C"

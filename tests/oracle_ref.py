@@ -214,3 +214,30 @@ class Odometry:
         if n < 0:
             return self.inliers(-n)
         return q[:n].copy(), m[:n].copy()
+
+
+def radius_search(xyz, q, radius, max_nn=0, cap=1 << 20):
+    """Exact radius search with FLANN semantics: d2 = ((dx*dx+dy*dy)+dz*dz) in float, d2 < r^2,
+    sorted by (d2, idx); max_nn > 0 keeps the max_nn nearest."""
+    xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+    q = np.ascontiguousarray(q, np.float32).reshape(3)
+    idx = np.zeros(cap, np.int32)
+    d2 = np.zeros(cap, np.float32)
+    m = lib().oracle_radius_search(_p(xyz), len(xyz), _p(q), ctypes.c_float(radius), max_nn, _p(idx), _p(d2), cap)
+    return idx[:m].copy(), d2[:m].copy()
+
+
+def eig3(a):
+    a = np.ascontiguousarray(a, np.float64).reshape(9)
+    w = np.zeros(3, np.float64)
+    v = np.zeros(9, np.float64)
+    lib().oracle_eig3(_p(a), _p(w), _p(v))
+    return w, v.reshape(3, 3)
+
+
+def umeyama(src, dst, use_float=False):
+    src = np.ascontiguousarray(src, np.float64).reshape(-1, 3)
+    dst = np.ascontiguousarray(dst, np.float64).reshape(-1, 3)
+    T = np.zeros(16, np.float64)
+    lib().oracle_umeyama(_p(src), _p(dst), len(src), int(use_float), _p(T))
+    return T.reshape(4, 4)

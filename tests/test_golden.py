@@ -1,0 +1,106 @@
+"""Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py from the oracle).
+
+CPU: the oracle still reproduces its committed vectors (regression pin of the restatement).
+GPU: the product path, called through the C ABI, reproduces the same vectors bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+import bshot_py
+import oracle_ref as orc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def stages():
+    return _load("stages_8k.npz")
+
+
+@pytest.fixture(scope="module")
+def seq():
+    return _load("sequence_3f.npz")
+
+
+def _u(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+# ----------------------------------------------------------------------------- oracle (CPU)
+def test_oracle_reproduces_stage_fixture(stages):
+    g = stages
+    k = int(g["k"])
+    for tag in ("a", "b"):
+        xyz = g[f"xyz_{tag}"]
+        sr_idx, sr_ratio = orc.seg_ratio(xyz)
+        assert np.array_equal(sr_idx, g[f"sr_idx_{tag}"]) and np.array_equal(_u(sr_ratio), _u(g[f"sr_ratio_{tag}"]))
+        kp_idx, _ = orc.select_topk(sr_idx, sr_ratio, k)
+        assert np.array_equal(kp_idx, g[f"kp_idx_{tag}"])
+        kps = xyz[kp_idx]
+        nrm = orc.normals(xyz, kps)
+        assert np.array_equal(_u(nrm), _u(g[f"normals_{tag}"]))
+        shot, rf = orc.shot(xyz, nrm, kps)
+        assert np.array_equal(_u(shot), _u(g[f"shot_{tag}"])) and np.array_equal(_u(rf), _u(g[f"rf_{tag}"]))
+        assert np.array_equal(orc.binarize(shot), g[f"bits_{tag}"])
+        assert np.array_equal(orc.iss(xyz)[0], g[f"iss_idx_{tag}"])
+    left, right, cq, cm = orc.match(g["bits_b"], g["bits_a"])
+    for a, b in ((left, "left"), (right, "right"), (cq, "corr_q"), (cm, "corr_m")):
+        assert np.array_equal(a, g[b])
+
+
+def test_oracle_reproduces_sequence_fixture(seq):
+    od = orc.Odometry(orc.params(num_keypoints=int(seq["k"])))
+    for f in range(3):
+        st = od.process(seq[f"xyz_{f}"])
+        assert np.array_equal(_u(np.array(st.pose, np.float32)), _u(seq[f"pose_{f}"].reshape(-1)))
+        assert np.array_equal(_u(np.array(st.T_ransac, np.float32)), _u(seq[f"T_ransac_{f}"].reshape(-1)))
+        assert np.array_equal(od.keypoints(), seq[f"kps_{f}"]) and np.array_equal(od.bits(), seq[f"bits_{f}"])
+        q, m = od.inliers()
+        assert np.array_equal(q, seq[f"inl_q_{f}"]) and np.array_equal(m, seq[f"inl_m_{f}"])
+
+
+# ----------------------------------------------------------------------------- product (GPU)
+@pytest.mark.gpu
+def test_gpu_reproduces_stage_fixture(stages):
+    g = stages
+    k = int(g["k"])
+    bits = {}
+    for tag in ("a", "b"):
+        ctx = bshot_py.Context(0)  # fresh context: the persistent normals array starts zeroed
+        xyz = g[f"xyz_{tag}"]
+        ctx.set_cloud(xyz)
+        sr_idx, sr_ratio = ctx.seg_ratio()
+        assert np.array_equal(sr_idx, g[f"sr_idx_{tag}"]) and np.array_equal(_u(sr_ratio), _u(g[f"sr_ratio_{tag}"]))
+        kp_idx, _ = bshot_py.select_topk(sr_idx, sr_ratio, k)
+        assert np.array_equal(kp_idx, g[f"kp_idx_{tag}"])
+        b, shot, rf = ctx.describe(xyz[kp_idx])
+        assert np.array_equal(_u(ctx.normals(len(xyz))), _u(g[f"normals_{tag}"]))
+        assert np.array_equal(_u(rf), _u(g[f"rf_{tag}"]))
+        assert np.array_equal(_u(shot), _u(g[f"shot_{tag}"]))
+        assert np.array_equal(b, g[f"bits_{tag}"])
+        assert np.array_equal(ctx.iss(), g[f"iss_idx_{tag}"])
+        bits[tag] = b
+        left, right, cq, cm = ctx.match(g["bits_b"], g["bits_a"])
+        for a, nm in ((left, "left"), (right, "right"), (cq, "corr_q"), (cm, "corr_m")):
+            assert np.array_equal(a, g[nm])
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_reproduces_sequence_fixture(seq):
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=int(seq["k"])))
+    for f in range(3):
+        st = od.process(seq[f"xyz_{f}"])
+        assert np.array_equal(od.keypoints(), seq[f"kps_{f}"]), f
+        assert np.array_equal(od.bits(), seq[f"bits_{f}"]), f
+        q, m = od.inliers()
+        assert np.array_equal(q, seq[f"inl_q_{f}"]) and np.array_equal(m, seq[f"inl_m_{f}"]), f
+        assert np.array_equal(_u(np.array(st.T_ransac, np.float32)), _u(seq[f"T_ransac_{f}"].reshape(-1))), f
+        assert np.array_equal(_u(np.array(st.pose, np.float32)), _u(seq[f"pose_{f}"].reshape(-1))), f
+    od.close()

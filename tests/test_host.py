@@ -1,0 +1,102 @@
+"""Host-side product code (no GPU): top-K selection, RANSAC, keypoint map, bitset layout --
+each checked against the oracle or against the reference formula restated here."""
+import numpy as np
+import pytest
+
+import bshot_py
+import oracle_ref as orc
+
+
+# ----------------------------------------------------------------------------- top-K (std::sort tail)
+@pytest.mark.parametrize("n,k,levels", [(5, 600, 0), (1000, 600, 0), (20000, 600, 7), (129000, 2048, 50),
+                                        (129000, 600, 0), (3000, 2048, 3)])
+def test_select_topk_matches_std_sort(n, k, levels):
+    """bshot_select_topk must reproduce libstdc++ std::sort's (unstable) tail order exactly
+    (src/lidar_odometry.cpp:131-153), including the order among equal ratios."""
+    rng = np.random.default_rng(n + k + levels)
+    r = rng.random(n).astype(np.float32)
+    if levels:
+        r = (np.floor(r * levels) / levels).astype(np.float32)  # heavy ties
+    idx = rng.permutation(n * 2)[:n].astype(np.int32)
+    gi, gr = bshot_py.select_topk(idx, r, k)
+    ei, er = orc.select_topk(idx, r, k)
+    assert np.array_equal(gi, ei) and np.array_equal(gr, er)
+
+
+# ----------------------------------------------------------------------------- RANSAC
+def _corr_set(seed, n_src=800, n_corr=400, inlier_frac=0.6, noise=30.0):
+    rng = np.random.default_rng(seed)
+    src = (rng.random((n_src, 3)) * 60000 - 30000).astype(np.float32)
+    a = rng.normal() * 0.05
+    R = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+    t = rng.normal(size=3) * 800
+    tgt = (src @ R.T + t + rng.normal(size=src.shape) * noise).astype(np.float32)
+    cq = rng.permutation(n_src)[:n_corr].astype(np.int32)
+    cm = cq.copy()
+    bad = rng.random(n_corr) > inlier_frac
+    cm[bad] = rng.integers(0, n_src, bad.sum())
+    return src, tgt, cq, cm
+
+
+@pytest.mark.parametrize("seed,frac", [(1, 0.6), (2, 0.3), (3, 0.9), (4, 0.05)])
+def test_ransac_matches_oracle(seed, frac):
+    src, tgt, cq, cm = _corr_set(seed, inlier_frac=frac)
+    rc, T, iq, im = bshot_py.ransac(src, tgt, cq, cm)
+    orc_rc, oT, oq, om = orc.ransac(src, tgt, cq, cm)
+    assert rc == orc_rc
+    assert np.array_equal(T.view(np.uint32), oT.view(np.uint32))
+    assert np.array_equal(iq, oq) and np.array_equal(im, om)
+
+
+def test_ransac_degenerate():
+    src, tgt, cq, cm = _corr_set(5, n_corr=2)
+    for ncorr in (0, 1, 2):
+        rc, T, iq, _ = bshot_py.ransac(src, tgt, cq[:ncorr], cm[:ncorr])
+        orc_rc, oT, oq, _ = orc.ransac(src, tgt, cq[:ncorr], cm[:ncorr])
+        assert rc == orc_rc and np.array_equal(T, oT) and len(iq) == len(oq)
+
+
+# ----------------------------------------------------------------------------- keypoint map
+def _block_id_ref(p, prec=10000):
+    """src/mymap.cpp:95-105: bitset<64>(int(round(p/prec))*prec), 21 bits per axis."""
+    g = [int(np.round(np.float32(x) / np.float32(prec))) * prec for x in p]
+    i = ((g[0] & 0xFFFFFFFFFFFFFFFF) << 42) & (0x1FFFFF << 42)
+    j = ((g[1] & 0xFFFFFFFFFFFFFFFF) << 21) & (0x1FFFFF << 21)
+    k = (g[2] & 0xFFFFFFFFFFFFFFFF) & 0x1FFFFF
+    return i | j | k
+
+
+def test_block_id_packing():
+    for p in [(0, 0, 0), (4999, -4999, 1), (5001, 15000, -25001), (-123456, 987654, -1730), (1e6, -1e6, 3e5)]:
+        assert bshot_py.KeypointMap.block_id(np.array(p, np.float32)) == _block_id_ref(p), p
+
+
+def test_map_quantisation_and_suppression():
+    m = bshot_py.KeypointMap()
+    bits = np.arange(11, dtype=np.uint32) * np.uint32(0x01010101)
+    m.add([-15.7, 29.99, 1005.0], 0.5, bits)       # -> (-10, 20, 1000): trunc toward zero, 10 mm grid
+    xyz, b = m.query([0, 0, 0])
+    assert np.array_equal(xyz, [[-10, 20, 1000]]) and np.array_equal(b[0], bits)
+    m.add([300.0, 20.0, 1000.0], 0.4, bits)        # within 800 mm, ratio <= existing -> rejected
+    assert m.size() == 1
+    m.add([300.0, 20.0, 1000.0], 0.6, bits)        # higher ratio -> kept
+    assert m.size() == 2
+    m.add([-12.0, 25.0, 1001.0], 0.9, bits ^ 1)    # same quantised position, better ratio -> replaces
+    assert m.size() == 2
+    m.add([9000.0, 20.0, 1000.0], 0.1, bits)       # > 800 mm away -> kept despite low ratio
+    m.add([60000.0, 0, 0], 0.1, bits)               # another block
+    assert m.size() == 4
+    xyz, _ = m.query([0, 0, 0], 20000.0)           # range query excludes the far block
+    assert len(xyz) == 3
+    xyz, _ = m.query([60000, 0, 0], 1000.0)
+    assert np.array_equal(xyz, [[60000, 0, 0]])
+
+
+def test_bitset_layout_roundtrip():
+    """bit j of bitset<352> <-> word j/32, bit j%32 (bitset<352> stored as 6 x u64 on x86-64)."""
+    m = bshot_py.KeypointMap()
+    rng = np.random.default_rng(1)
+    words = rng.integers(0, 2 ** 32, 11, dtype=np.uint64).astype(np.uint32)
+    m.add([0, 0, 0], 0.5, words)
+    _, b = m.query([0, 0, 0])
+    assert np.array_equal(b[0], words)

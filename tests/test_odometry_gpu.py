@@ -1,0 +1,69 @@
+"""Whole-frame parity: the product odometry loop (bshot_odom, the odometry_test drop-in) against the
+oracle's restatement of src/lidar_odometry.cpp:155-376 on full-size synthetic sweeps.
+
+Contract: pose |dt| <= 1 mm and |dtheta| <= 1e-4 rad per frame. Because both
+sides follow one documented operation order, every artefact (keypoints, ratios, bits, target,
+inliers, T_ransac, pose) is additionally asserted bit-exact."""
+import numpy as np
+import pytest
+
+import bshot_py
+import oracle_ref as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _u(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _rot_err(A, B):
+    R = A[:3, :3].astype(np.float64).T @ B[:3, :3].astype(np.float64)
+    return float(np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1)))
+
+
+def _run_pair(frames, sensor=0, **kw):
+    od = bshot_py.Odometry(0, bshot_py.default_params(**kw))
+    oo = orc.Odometry(orc.params(**kw))
+    try:
+        for f in frames:
+            xyz, _ = bshot_py.synth_sweep(f, sensor=sensor)
+            st = od.process(xyz)
+            so = oo.process(xyz)
+            for name in ("n_points", "n_valid_ratios", "n_keypoints", "n_iss", "n_target", "n_mutual", "n_inliers",
+                         "icp_iters", "gated", "map_size"):
+                assert getattr(st, name) == getattr(so, name), (f, name, getattr(st, name), getattr(so, name))
+            assert np.array_equal(od.keypoints(), oo.keypoints()), f
+            assert np.array_equal(_u(od.ratios()), _u(oo.ratios())), f
+            assert np.array_equal(od.bits(), oo.bits()), f
+            assert np.array_equal(od.iss(), oo.iss()), f
+            tx, tb = od.target()
+            ox, ob = oo.target()
+            assert np.array_equal(tx, ox) and np.array_equal(tb, ob), f
+            q, m = od.inliers()
+            oq, om = oo.inliers()
+            assert np.array_equal(q, oq) and np.array_equal(m, om), f
+            P = np.array(st.pose, np.float32).reshape(4, 4)
+            Po = np.array(so.pose, np.float32).reshape(4, 4)
+            # contract floor, then the bit-exact expectation
+            assert np.abs(P[:3, 3] - Po[:3, 3]).max() <= 1.0 and _rot_err(P, Po) <= 1e-4, f
+            assert np.array_equal(_u(np.array(st.T_ransac)), _u(np.array(so.T_ransac))), f
+            assert np.array_equal(_u(P), _u(Po)), f
+    finally:
+        od.close()
+
+
+def test_odometry_hdl64_k600():
+    _run_pair(range(4))
+
+
+def test_odometry_hdl64_k2048():
+    _run_pair(range(10, 13), num_keypoints=2048)
+
+
+def test_odometry_vlp128_cvsn():
+    _run_pair(range(2), sensor=1, sr_type=2)
+
+
+def test_odometry_no_icp_no_iss():
+    _run_pair(range(3), run_icp=0, run_iss=0)
