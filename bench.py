@@ -28,6 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "b-shot-slam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import bshot_py  # noqa: E402
+from dist_map import exchange_map_delta  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
@@ -80,18 +81,8 @@ def main():
     def step(i):
         st = odo.process_device(frames[i].data_ptr(), npts[i])
         if a.map_bcast and world > 1:
-            rec = torch.from_numpy(odo.map_delta()).to(dev)
-            k = torch.tensor([rec.shape[0]], device=dev)
-            ks = [torch.zeros_like(k) for _ in range(world)]
-            dist.all_gather(ks, k)
-            kmax = int(max(int(x) for x in ks))
-            pad = torch.zeros((kmax, 15), dtype=torch.float32, device=dev)
-            pad[: rec.shape[0]] = rec
-            bufs = [torch.zeros_like(pad) for _ in range(world)]
-            dist.all_gather(bufs, pad)
-            for r in range(world):
-                if r != rank:
-                    odo.replica_insert(r, bufs[r][: int(ks[r])].cpu().numpy())
+            for r, rec in exchange_map_delta(odo.map_delta(), dist, dev):
+                odo.replica_insert(r, rec)
         return st
 
     for i in range(a.warmup):
@@ -150,6 +141,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         import oracle_ref
+        # thread counts mirror the reference: SR, ISS, Hamming, RANSAC, ICP single-threaded;
+        # normals and SHOT OpenMP with min(12, nproc) threads (include/bshot_bits.h:62,120)
+        nthr = oracle_ref.set_threads(min(12, os.cpu_count() or 1))
         op = oracle_ref.params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
         od = oracle_ref.Odometry(op)
         nf = a.cpu_frames
@@ -157,10 +151,11 @@ def main():
         for f in range(nf):
             od.process(frames[f].cpu().numpy())
         ct = time.perf_counter() - t1
-        cpu = {"value": round(nf / ct, 4), "unit": "sweeps/s", "cores": os.cpu_count(), "kind": "port",
-               "sample": f"first {nf} sweeps of the same synthetic HDL-64 sequence, full path, oracle/ C++ "
-                         f"restatement (PCL unavailable); SR/ISS/Hamming/RANSAC/ICP 1 thread, SHOT/normals OpenMP",
-               "cpu": platform.processor() or platform.machine()}
+        cpu = {"value": round(nf / ct, 4), "unit": "sweeps/s", "cores": nthr, "kind": "port",
+               "sample": f"first {nf} sweeps of the same synthetic sequence (N~{int(n_eff)}, K={a.keypoints}), full "
+                         f"path, oracle/ C++ restatement (PCL unavailable); {ct:.1f} s; SR/ISS/Hamming/RANSAC/ICP "
+                         f"1 thread, normals/SHOT {nthr} OpenMP threads as in the reference",
+               "cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()}
 
     if rank == 0:
         if a.profile_stages:

@@ -62,6 +62,10 @@ int oracle_radius_search(const float* xyz, int n, const float* q, float radius, 
 void oracle_eig3(const double* a9, double* w3, double* v9);
 void oracle_umeyama(const double* src, const double* dst, int n, int use_float, double* T16);
 
+/* OpenMP threads for the stages the reference runs with OpenMP (normals, SHOT) */
+void oracle_set_threads(int n);
+int oracle_get_threads(void);
+
 void oracle_default_params(oracle_params* p);
 void* oracle_odom_create(const oracle_params* p);
 void oracle_odom_destroy(void* h);

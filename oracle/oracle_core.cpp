@@ -7,6 +7,9 @@
 #include <cstring>
 #include <limits>
 #include <random>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "oracle_api.h"
 #include "oracle_math.h"
@@ -221,9 +224,11 @@ int oracle_normals(const float* xyz, int n, const float* kps, int k, float radiu
     const P3* pts = reinterpret_cast<const P3*>(xyz);
     const P3* kp = reinterpret_cast<const P3*>(kps);
     Grid g(pts, n, radius * 0.25f);
-    std::vector<std::pair<float, int>> nn;
     const float qn = std::numeric_limits<float>::quiet_NaN();
-    for (int i = 0; i < k && i < n; ++i) {
+    // NormalEstimationOMP (include/bshot_bits.h:62): keypoints are independent
+#pragma omp parallel for schedule(dynamic, 8)
+    for (int i = 0; i < std::min(k, n); ++i) {
+        std::vector<std::pair<float, int>> nn;
         float* o = normals + 4 * i;
         if (!finite3(kp[i])) { o[0] = o[1] = o[2] = o[3] = qn; continue; }
         g.radius_knn(kp[i], radius, max_nn, nn);
@@ -283,24 +288,45 @@ static inline float dot4f(float a0, float a1, float a2, float b0, float b1, floa
 // (x axis, y axis, z axis). Returns false when the LRF is NaN.
 static bool lrf_one(const P3* pts, const P3& c, const std::vector<std::pair<float, int>>& nn, double R,
                     float rf[9]) {
+    // Weighted covariance (PCL getLocalRF, double). PCL sums in kd-tree (unsorted) order, so the
+    // summation order is a free convention; ours (DESIGN.md "Numerics"): neighbours in (d2, idx)
+    // rank order, split into chunks of 64 ranks, each chunk reduced by the xor-butterfly tree
+    // (offsets 32, 16, ..., 1; excluded ranks contribute 0), chunk sums added in chunk order.
     std::vector<double> vij;
     vij.reserve(nn.size() * 3);
-    double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    double sum = 0.0;
+    double tot[7] = {0, 0, 0, 0, 0, 0, 0};
     int valid = 0;
-    for (const auto& e : nn) {
-        const P3& p = pts[e.second];
-        if (p.x == c.x && p.y == c.y && p.z == c.z) continue;
-        const double v[3] = {(double)(p.x - c.x), (double)(p.y - c.y), (double)(p.z - c.z)};
-        const double w = R - std::sqrt((double)e.first);
-        for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) cov[a * 3 + b] = cov[a * 3 + b] + w * (v[a] * v[b]);
-        sum += w;
-        vij.push_back(v[0]); vij.push_back(v[1]); vij.push_back(v[2]);
-        ++valid;
+    const size_t nch = (nn.size() + 63) / 64;
+    for (size_t ch = 0; ch < nch; ++ch) {
+        double lane[64][7];
+        for (int l = 0; l < 64; ++l) {
+            for (int j = 0; j < 7; ++j) lane[l][j] = 0.0;
+            const size_t r = ch * 64 + l;
+            if (r >= nn.size()) continue;
+            const P3& p = pts[nn[r].second];
+            if (p.x == c.x && p.y == c.y && p.z == c.z) continue;
+            const double vx = (double)(p.x - c.x), vy = (double)(p.y - c.y), vz = (double)(p.z - c.z);
+            const double w = R - std::sqrt((double)nn[r].first);
+            lane[l][0] = w * (vx * vx); lane[l][1] = w * (vx * vy); lane[l][2] = w * (vx * vz);
+            lane[l][3] = w * (vy * vy); lane[l][4] = w * (vy * vz); lane[l][5] = w * (vz * vz);
+            lane[l][6] = w;
+            vij.push_back(vx); vij.push_back(vy); vij.push_back(vz);
+            ++valid;
+        }
+        // butterfly: lane l and lane l^off both hold lane[l] + lane[l^off] (IEEE + commutes),
+        // so halving in place gives lane 0's final value
+        for (int off = 32; off > 0; off >>= 1)
+            for (int l = 0; l < off; ++l)
+                for (int j = 0; j < 7; ++j) lane[l][j] = lane[l][j] + lane[l + off][j];
+        for (int j = 0; j < 7; ++j) tot[j] = tot[j] + lane[0][j];
     }
+    const double sum = tot[6];
+    double cov[9];
+    cov[0] = tot[0]; cov[1] = tot[1]; cov[2] = tot[2];
+    cov[4] = tot[3]; cov[5] = tot[4]; cov[8] = tot[5];
+    cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
     if (valid < 5) return false;
-    for (int a = 0; a < 9; ++a) cov[a] = cov[a] / sum;
+    for (int a = 0; a < 9; ++a) cov[a] = cov[a] / sum;  // cov[3,6,7] mirror cov[1,2,5] exactly
     double ev[3], evec[9];
     o_jacobi3(cov, ev, evec);
     if (!std::isfinite(ev[0]) || !std::isfinite(ev[1]) || !std::isfinite(ev[2])) return false;
@@ -739,6 +765,22 @@ int oracle_radius_search(const float* xyz, int n, const float* q, float radius, 
     const int m = (int)nn.size();
     for (int i = 0; i < m && i < cap; ++i) { idx[i] = nn[i].second; d2[i] = nn[i].first; }
     return m;
+}
+
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : 1);
+#else
+    (void)n;
+#endif
+}
+
+int oracle_get_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
 }
 
 void oracle_eig3(const double* a9, double* w3, double* v9) { o_jacobi3(a9, w3, v9); }

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: GPU parity tests, smoke, bench line, rocprofv3 kernel stats, HBM PMC passes.
+# Every GPU step has its own time limit and the chain stops at the first failure.
+# usage (from the repo root, via gpurun): bash scripts/gpu_round.sh [tag]
+set -u
+TAG=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+cd $R
+echo "[gpu_round] $(date +%T) pytest -m gpu" &&
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu_$TAG.log 2>&1 &&
+tail -3 $O/pytest_gpu_$TAG.log &&
+echo "[gpu_round] $(date +%T) smoke" &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 &&
+cat $O/smoke_$TAG.log &&
+echo "[gpu_round] $(date +%T) bench" &&
+timeout -k 10 600 python bench.py --profile-stages > $O/bench_$TAG.json 2> $O/bench_$TAG.err &&
+cat $O/bench_$TAG.json &&
+cd /tmp && export TMPDIR=/tmp &&
+echo "[gpu_round] $(date +%T) rocprofv3 kernel trace" &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o trace --output-format csv -- \
+    python3 $R/bench.py --no-cpu-baseline > $O/prof_bench_$TAG.json 2> $O/prof_bench_$TAG.err &&
+echo "[gpu_round] $(date +%T) pmc FETCH_SIZE" &&
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o fetch --output-format csv -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_fetch_$TAG.log 2>&1 &&
+echo "[gpu_round] $(date +%T) pmc WRITE_SIZE" &&
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$TAG -o write --output-format csv -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_write_$TAG.log 2>&1 &&
+echo "[gpu_round] $(date +%T) done"

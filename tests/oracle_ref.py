@@ -241,3 +241,9 @@ def umeyama(src, dst, use_float=False):
     T = np.zeros(16, np.float64)
     lib().oracle_umeyama(_p(src), _p(dst), len(src), int(use_float), _p(T))
     return T.reshape(4, 4)
+
+
+def set_threads(n):
+    """OpenMP threads for the oracle's normals/SHOT stages (the reference's OpenMP stages)."""
+    lib().oracle_set_threads(int(n))
+    return lib().oracle_get_threads()
