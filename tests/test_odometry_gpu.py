@@ -18,8 +18,9 @@ def _u(a):
 
 
 def _rot_err(A, B):
-    R = A[:3, :3].astype(np.float64).T @ B[:3, :3].astype(np.float64)
-    return float(np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1)))
+    """Angle between two rotations from the chordal distance (well conditioned near 0)."""
+    d = np.linalg.norm(A[:3, :3].astype(np.float64) - B[:3, :3].astype(np.float64))
+    return float(2.0 * np.arcsin(min(1.0, d / (2.0 * np.sqrt(2.0)))))
 
 
 def _run_pair(frames, sensor=0, **kw):
