@@ -33,6 +33,22 @@ from dist_map import exchange_map_delta  # noqa: E402
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
+def pmc_traffic(stage):
+    """HBM bytes per launch of the stage's kernel from the newest committed PMC summary
+    (profiles/rNN_pmc.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE, separate passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    try:
+        k = json.load(open(files[-1]))["kernels"].get(f"bsk::k_{stage}")
+        if not k:
+            return None, None
+        return round(k.get("hbm_read_bytes", 0.0) + k.get("hbm_write_bytes", 0.0)), os.path.relpath(files[-1], ROOT)
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,9 +149,12 @@ def main():
     roof = None
     if dname in alg and per_launch_ms[dname] > 0:
         ach = alg[dname] / (per_launch_ms[dname] * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(dname)
         roof = {"kernel": dname, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
-                "alg_bytes_per_launch": alg[dname], "ms_per_launch": round(per_launch_ms[dname], 4)}
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": tsrc, "alg_bytes_per_launch": alg[dname],
+                "ms_per_launch": round(per_launch_ms[dname], 4),
+                "convention": "SURVEY.md 8(d) pair-gather bytes; DESIGN.md section 4"}
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference algorithm), rank 0 only
     cpu = None
