@@ -26,20 +26,17 @@ namespace bsk {
 
 #define SB_BUCKETS 1024
 
-struct CandLds {
-    int mark[64];
-};
-
 __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __restrict__ kps, int k, float R,
                                                     int* __restrict__ counts) {
     __shared__ CandLds lds[4];
     const int wave = threadIdx.x >> 6, lane = lane_id();
+    cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
     for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         int c = 0;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))
-            for_candidates(g, lds[wave].mark, kx, ky, kz, R, R2,
+            for_candidates(g, &lds[wave], kx, ky, kz, R, R2,
                            [&](bool v, float, unsigned int) { c += __popcll(__ballot(v)); });
         if (lane == 0) counts[q] = c;
     }
@@ -75,13 +72,14 @@ __global__ void __launch_bounds__(256) k_shot_gather(GridView g, const float* __
                                                      unsigned long long* __restrict__ seg) {
     __shared__ CandLds lds[4];
     const int wave = threadIdx.x >> 6;
+    cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
     for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         if (!(__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))) continue;
         unsigned long long* out = seg + offs[q];
         int cnt = 0;
-        for_candidates(g, lds[wave].mark, kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
+        for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
             const unsigned long long m = __ballot(v);
             if (v) {
                 const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),

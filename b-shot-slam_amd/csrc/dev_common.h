@@ -67,24 +67,45 @@ __device__ __forceinline__ float d2_flann(float qx, float qy, float qz, float px
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
-// wave-wide exclusive prefix sum of an int (64 lanes)
+// ---- wave-wide scans on DPP (no LDS round trip): Hillis-Steele inside each 16-lane row
+// (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1/3 and row_bcast:31 into rows 2/3.
+// Lanes whose DPP source lies outside the row read the identity. Call from converged code.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int identity, int v) {
+    return __builtin_amdgcn_update_dpp(identity, v, CTRL, ROWS, 0xf, false);
+}
+
+__device__ __forceinline__ int wave_incl_add_i(int v) {
+    v += dpp_i<0x111, 0xf>(0, v);
+    v += dpp_i<0x112, 0xf>(0, v);
+    v += dpp_i<0x114, 0xf>(0, v);
+    v += dpp_i<0x118, 0xf>(0, v);
+    v += dpp_i<0x142, 0xa>(0, v);
+    v += dpp_i<0x143, 0xc>(0, v);
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_max_i(int v) {
+    const int I = -2147483647 - 1;
+    v = max(v, dpp_i<0x111, 0xf>(I, v));
+    v = max(v, dpp_i<0x112, 0xf>(I, v));
+    v = max(v, dpp_i<0x114, 0xf>(I, v));
+    v = max(v, dpp_i<0x118, 0xf>(I, v));
+    v = max(v, dpp_i<0x142, 0xa>(I, v));
+    v = max(v, dpp_i<0x143, 0xc>(I, v));
+    return v;
+}
+
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// wave-wide exclusive prefix sum of an int (64 lanes); total = sum over the wave (uniform)
 __device__ __forceinline__ int wave_excl_scan(int v, int& total) {
-    const int lane = lane_id();
-    int x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    total = __shfl(x, 63, 64);
+    const int x = wave_incl_add_i(v);
+    total = readlane_i(x, 63);
     return x - v;
 }
 
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
+__device__ __forceinline__ int wave_sum_i(int v) { return readlane_i(wave_incl_add_i(v), 63); }
 
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll

@@ -20,7 +20,7 @@ namespace bsk {
 struct IssLds {
     unsigned long long list[ISS_CAP];
     double dd[3][ISS_CAP / 2];
-    int mark[64];
+    CandLds cand;
 };
 
 __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, const float4* __restrict__ pts4, int n,
@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     IssLds* L = reinterpret_cast<IssLds*>(smem) + wave;
+    cand_init(&L->cand);
     const float r2 = (float)((double)salient * (double)salient);
     const int G = gridDim.x, b = blockIdx.x;
     const int xg = b & 7, gi = b >> 3, ng = (G + 7 - xg) >> 3;
@@ -39,7 +40,7 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
         double out = 0.0;
         if (__builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
             int cnt = 0;
-            for_candidates(g, L->mark, c.x, c.y, c.z, salient, r2, [&](bool v, float d2, unsigned int idx) {
+            for_candidates<1>(g, &L->cand, c.x, c.y, c.z, salient, r2, [&](bool v, float d2, unsigned int idx) {
                 const unsigned long long m = __ballot(v);
                 if (v) {
                     const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),

@@ -20,15 +20,17 @@
 
 namespace bsk {
 
-#define KNN_NB 512
+#define KNN_NB 256
 #define KNN_CAP 1024
+#define KNN_SCAT 512
 #define KNN_WAVES 2
 
 struct KnnLds {
     unsigned int hist[KNN_NB];
-    unsigned int boff[KNN_NB + 1];
-    int mark[64];
-    unsigned long long list[KNN_CAP];
+    unsigned int boff[KNN_NB + 4];
+    CandLds cand;
+    unsigned long long list[KNN_CAP];   // in-radius keys of the last ladder step; then the sorted result
+    unsigned long long scat[KNN_SCAT];  // bucket-grouped prefix (counting-sort scatter target)
 };
 
 __device__ __forceinline__ int bucket_of(float d2, float lo, float sc) {
@@ -37,6 +39,10 @@ __device__ __forceinline__ int bucket_of(float d2, float lo, float sc) {
     if (!(v >= 0.f)) b = 0;
     if (b > KNN_NB - 1) b = KNN_NB - 1;
     return b;
+}
+
+__device__ __forceinline__ unsigned long long knn_key(float d2, unsigned int idx) {
+    return ((unsigned long long)__float_as_uint(d2) << 32) | idx;
 }
 
 // wave: bucket B where the cumulative count reaches `need` (1-based); *below = count before B
@@ -61,8 +67,8 @@ __device__ __forceinline__ int hist_cross(KnnLds* L, int need, int* below) {
         }
         bl = acc;
     }
-    B = __shfl(B, owner, 64);
-    *below = __shfl(bl, owner, 64);
+    B = readlane_i(B, owner);
+    *below = readlane_i(bl, owner);
     return B;
 }
 
@@ -73,9 +79,54 @@ __device__ __forceinline__ void hist_clear(KnnLds* L) {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Exact selection: leaves the `*need` nearest (d2, idx) sorted in L->list[0, *need).
+// counting-sort offsets of buckets [0, Bmax]: boff[b] = start, hist[b] = cursor; returns the
+// number of keys in those buckets
+__device__ __forceinline__ int prefix_offsets(KnnLds* L, int Bmax) {
+    const int lane = lane_id();
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < KNN_NB / 64; ++j) {
+        const int b = lane * (KNN_NB / 64) + j;
+        s += b <= Bmax ? (int)L->hist[b] : 0;
+    }
+    int tot;
+    int run = wave_excl_scan(s, tot);
+    if (tot <= KNN_SCAT) {
+#pragma unroll
+        for (int j = 0; j < KNN_NB / 64; ++j) {
+            const int b = lane * (KNN_NB / 64) + j;
+            const int h = b <= Bmax ? (int)L->hist[b] : 0;
+            L->boff[b] = (unsigned)run;
+            L->hist[b] = (unsigned)run;
+            run += h;
+        }
+        if (lane == 63) L->boff[KNN_NB] = (unsigned)tot;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return tot;
+}
+
+// keys scattered bucket-grouped in scat[0, tot) -> exact (d2, idx) order in list[0, tot)
+__device__ __forceinline__ void rank_into_list(KnnLds* L, int tot, float sc0) {
+    const int lane = lane_id();
+    for (int i = lane; i < tot; i += 64) {
+        const unsigned long long key = L->scat[i];
+        const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
+        const unsigned s0 = L->boff[b], e0 = L->boff[b + 1];
+        unsigned rank = 0;
+        for (unsigned j = s0; j < e0; ++j) rank += L->scat[j] < key ? 1u : 0u;
+        L->list[s0 + rank] = key;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Exact selection: leaves the `*need` nearest (d2, idx) sorted in (*sorted)[0, *need).
 // Returns false when > KNN_CAP keys tie at the boundary after 3 refinement levels (reported).
 // kst (nullable): diagnostic work counters, see bshot_debug_knn_stats()
+//
+// Fast path: the ladder step that first holds >= max_nn points also stored every in-radius key
+// in LDS (ballot compaction while histogramming), so when they fit (<= KNN_CAP) the selection is
+// a counting sort over LDS only -- no second pass over the candidates.
 __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, float qx, float qy, float qz, float r,
                            int max_nn, int* need_out, unsigned long long* kst, const unsigned long long** sorted) {
     unsigned long long chunks = 0;
@@ -89,15 +140,20 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
         rs2 = step == 3 ? r2 : (float)((double)rs * (double)rs);
         hist_clear(L);
         const float sc = (float)KNN_NB / rs2;
-        for_candidates(step < 2 ? gf : gc, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+        int cnt = 0;
+        for_candidates(step < 2 ? gf : gc, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             ++chunks;
             if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
+            const unsigned long long m = __ballot(v);
+            if (v) {
+                const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (slot < KNN_CAP) L->list[slot] = knn_key(d2, idx);
+            }
+            cnt += __popcll(m);
         });
         __builtin_amdgcn_wave_barrier();
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < KNN_NB / 64; ++j) s += (int)L->hist[lane + 64 * j];
-        total = wave_sum_i(s);
+        total = cnt;
         if (total >= max_nn) break;
     }
     if (step > 3) step = 3;
@@ -105,10 +161,45 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
     const int need = total < max_nn ? total : max_nn;
     *need_out = need;
     if (need == 0) return true;
+    const float sc0 = (float)KNN_NB / rs2;
+    if (kst && lane == 0) {
+        atomicAdd(&kst[0], 1ull);
+        atomicAdd(&kst[1 + step], 1ull);
+        atomicAdd(&kst[9], (unsigned long long)need);
+        atomicAdd(&kst[10], (unsigned long long)total);
+    }
+
+    // ---- fast path: every in-radius key is in L->list
+    if (total <= KNN_CAP) {
+        int Bmax = KNN_NB - 1;
+        if (total > need) {
+            int below;
+            Bmax = hist_cross(L, need, &below);
+        }
+        const int tot = prefix_offsets(L, Bmax);
+        if (tot <= KNN_SCAT) {
+            for (int i = lane; i < total; i += 64) {
+                const unsigned long long key = L->list[i];
+                const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
+                if (b <= Bmax) L->scat[atomicAdd(&L->hist[b], 1u)] = key;
+            }
+            __builtin_amdgcn_wave_barrier();
+            rank_into_list(L, tot, sc0);
+            *sorted = L->list;
+            if (kst && lane == 0) atomicAdd(&kst[5], chunks);
+            return true;
+        }
+        // a boundary bucket too crowded for the scatter buffer: refine by streaming (rare)
+    }
+    if (kst && lane == 0) atomicAdd(&kst[11], 1ull);
+
+    // ---- streaming path: > KNN_CAP keys in radius, or a crowded boundary bucket
     int B[3] = {KNN_NB, KNN_NB, KNN_NB};
-    float lo[3] = {0.f, 0.f, 0.f}, sc[3] = {(float)KNN_NB / rs2, 0.f, 0.f};
+    float lo[3] = {0.f, 0.f, 0.f}, sc[3] = {sc0, 0.f, 0.f};
     int levels = 0;
     if (total > need) {
+        // the level-0 histogram of the final ladder step is intact here: prefix_offsets only
+        // rewrites it when the prefix fits the scatter buffer
         int below_acc = 0;
         float w = rs2;
         for (int lev = 0; lev < 3; ++lev) {
@@ -116,7 +207,7 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
                 hist_clear(L);
                 const int lv = lev;
                 if (kst && lane == 0) atomicAdd(&kst[7], 1ull);
-                for_candidates(g, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+                for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
                     ++chunks;
                     if (!v) return;
                     int b = bucket_of(d2, lo[0], sc[0]);
@@ -133,86 +224,40 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
             B[lev] = Bl;
             levels = lev + 1;
             below_acc += below;
-            if (below_acc + (int)L->hist[Bl] <= KNN_CAP) break;
-            if (lev == 2) return false;
+            if (below_acc + (int)L->hist[Bl] <= KNN_SCAT) break;
+            if (lev == 2) {
+                if (below_acc + (int)L->hist[Bl] <= KNN_CAP) break;
+                return false;
+            }
             const float wb = w / (float)KNN_NB;
             lo[lev + 1] = lo[lev] + (float)Bl * wb;
             sc[lev + 1] = (float)KNN_NB / wb;
             w = wb;
         }
     }
-    // collect the prefix (bucket path <= B lexicographically)
     const int lv = levels;
-    const int Bmax = lv >= 1 ? B[0] : KNN_NB - 1;
-    int cnt = 0;
     if (lv <= 1) {
-        // bucket counting sort: level-0 buckets order the prefix by d2; exact (d2, idx) rank inside
-        // each bucket (buckets hold ~1-2 keys). Offsets from the histogram of the final ladder step.
-        int s8 = 0;
-#pragma unroll
-        for (int j = 0; j < KNN_NB / 64; ++j) {
-            const int b = lane * (KNN_NB / 64) + j;
-            s8 += b <= Bmax ? (int)L->hist[b] : 0;
-        }
-        int tot;
-        (void)wave_excl_scan(s8, tot);
-        cnt = tot;
-    }
-    if (lv <= 1 && cnt <= KNN_CAP / 2) {
-        {
-            int s8 = 0;
-#pragma unroll
-            for (int j = 0; j < KNN_NB / 64; ++j) {
-                const int b = lane * (KNN_NB / 64) + j;
-                s8 += b <= Bmax ? (int)L->hist[b] : 0;
-            }
-            int tot;
-            int run = wave_excl_scan(s8, tot);
-#pragma unroll
-            for (int j = 0; j < KNN_NB / 64; ++j) {
-                const int b = lane * (KNN_NB / 64) + j;
-                const int h = b <= Bmax ? (int)L->hist[b] : 0;
-                L->boff[b] = (unsigned)run;
-                L->hist[b] = (unsigned)run;  // cursor
-                run += h;
-            }
-            if (lane == 63) L->boff[KNN_NB] = (unsigned)tot;
-            __builtin_amdgcn_wave_barrier();
-        }
-        const float sc0 = sc[0];
-        for_candidates(g, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
-            ++chunks;
-            if (v) {
-                const int b = bucket_of(d2, 0.f, sc0);
-                if (b <= Bmax) {
-                    const unsigned pos = atomicAdd(&L->hist[b], 1u);
-                    L->list[pos] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+        // level-0 histogram is current: counting sort of the prefix, streamed
+        const int Bmax = lv >= 1 ? B[0] : KNN_NB - 1;
+        const int tot = prefix_offsets(L, Bmax);
+        if (tot <= KNN_SCAT) {
+            for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+                ++chunks;
+                if (v) {
+                    const int b = bucket_of(d2, 0.f, sc0);
+                    if (b <= Bmax) L->scat[atomicAdd(&L->hist[b], 1u)] = knn_key(d2, idx);
                 }
-            }
-        });
-        __builtin_amdgcn_wave_barrier();
-        unsigned long long* out = L->list + KNN_CAP / 2;
-        for (int i = lane; i < cnt; i += 64) {
-            const unsigned long long key = L->list[i];
-            const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
-            const unsigned s0 = L->boff[b], e0 = L->boff[b + 1];
-            unsigned rank = 0;
-            for (unsigned j = s0; j < e0; ++j) rank += L->list[j] < key ? 1u : 0u;
-            out[s0 + rank] = key;
+            });
+            __builtin_amdgcn_wave_barrier();
+            rank_into_list(L, tot, sc0);
+            *sorted = L->list;
+            if (kst && lane == 0) atomicAdd(&kst[5], chunks);
+            return true;
         }
-        __builtin_amdgcn_wave_barrier();
-        *sorted = out;
-        if (kst && lane == 0) {
-            atomicAdd(&kst[0], 1ull);
-            atomicAdd(&kst[1 + step], 1ull);
-            atomicAdd(&kst[5], chunks);
-            atomicAdd(&kst[9], (unsigned long long)need);
-            atomicAdd(&kst[10], (unsigned long long)total);
-        }
-        return true;
     }
-    cnt = 0;
-    for_candidates(g, L->mark, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+    // general path: collect the (refined) prefix and bitonic-sort it
+    int cnt = 0;
+    for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
         ++chunks;
         bool take = v;
         if (take && lv > 0) {
@@ -230,7 +275,7 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
         if (take) {
             const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            if (slot < KNN_CAP) L->list[slot] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+            if (slot < KNN_CAP) L->list[slot] = knn_key(d2, idx);
         }
         cnt += __popcll(m);
     });
@@ -238,12 +283,8 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
     int P = 64;
     while (P < cnt) P <<= 1;
     if (kst && lane == 0) {
-        atomicAdd(&kst[0], 1ull);
-        atomicAdd(&kst[1 + step], 1ull);
         atomicAdd(&kst[5], chunks);
         atomicAdd(&kst[8], (unsigned long long)P);
-        atomicAdd(&kst[9], (unsigned long long)need);
-        atomicAdd(&kst[10], (unsigned long long)total);
     }
     for (int i = cnt + lane; i < P; i += 64) L->list[i] = ~0ull;
     __builtin_amdgcn_wave_barrier();
@@ -308,6 +349,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView gf, GridV
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
+    cand_init(&L->cand);
     // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD group a contiguous query range
     const int G = gridDim.x, b = blockIdx.x;
     const int xg = b & 7, gi = b >> 3, ng = (G + 7 - xg) >> 3;
@@ -387,6 +429,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView gf, GridVie
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
+    cand_init(&L->cand);
     float* fl = reinterpret_cast<float*>(L->list);
     const float qn = __builtin_nanf("");
     for (int q = blockIdx.x * KNN_WAVES + wave; q < k; q += gridDim.x * KNN_WAVES) {
