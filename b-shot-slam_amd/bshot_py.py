@@ -59,7 +59,7 @@ ABI_SYMBOLS = [
     "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
     "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
-    "bshot_map_block_id",
+    "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
 ]
 
 _lib = None
@@ -135,6 +135,9 @@ class Context:
         self.n = len(xyz)
         self._chk(self.L.bshot_set_cloud(self.h, _ptr(xyz), self.n), "set_cloud")
 
+    def prefetch_cloud_device(self, dptr, n):
+        self._chk(self.L.bshot_prefetch_cloud_device(self.h, P(dptr), n), "prefetch_cloud_device")
+
     def set_cloud_device(self, dptr, n):
         self.n = n
         self._chk(self.L.bshot_set_cloud_device(self.h, P(dptr), n), "set_cloud_device")
@@ -193,6 +196,9 @@ class Context:
 
     def set_timing(self, on):
         self.L.bshot_set_timing(self.h, 1 if on else 0)
+
+    def set_option(self, name, value):
+        self._chk(self.L.bshot_set_option(self.h, name.encode(), int(value)), "set_option")
 
     def stage_times(self):
         ms = (ctypes.c_double * NSTAGES)()
@@ -283,6 +289,10 @@ class Odometry:
         self._chk(self.L.bshot_odom_process(self.h, _ptr(xyz), len(xyz), ctypes.byref(st)), "odom_process")
         return st
 
+    def set_next_device(self, dptr, n):
+        """Lookahead: the device cloud the next process_device call will receive."""
+        self._chk(self.L.bshot_odom_set_next_device(self.h, P(dptr), n), "odom_set_next_device")
+
     def process_device(self, dptr, n):
         st = FrameStats()
         self._chk(self.L.bshot_odom_process_device(self.h, P(dptr), n, ctypes.byref(st)), "odom_process_device")
@@ -345,6 +355,10 @@ class Odometry:
         nl = (ctypes.c_int64 * NSTAGES)()
         self.L.bshot_stage_times(P(self.context()), ms, nl, NSTAGES)
         return {STAGE_NAMES[i]: (ms[i], nl[i]) for i in range(NSTAGES)}
+
+    def set_option(self, name, value):
+        if self.L.bshot_set_option(P(self.context()), name.encode(), int(value)) < 0:
+            raise BshotError(f"set_option {name}")
 
     def set_timing(self, on):
         self.L.bshot_set_timing(P(self.context()), 1 if on else 0)

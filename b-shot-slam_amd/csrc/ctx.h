@@ -30,31 +30,83 @@ struct DBuf {
     }
 };
 
+// pinned host staging (async D2H), grow-only
+template <typename T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = n + n / 4 + 64;
+        hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * c, hipHostMallocDefault);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 struct StageEv {
     int stage;
     hipEvent_t a, b;
 };
 
+// Everything that belongs to one input cloud: float4 copy, radius-ladder and ISS grids, SR ratios,
+// ISS results, and their pinned host copies. The context holds the current cloud and a prefetch
+// slot; adopting a prefetched cloud swaps the two (pointer swaps, no copies).
+struct CloudState {
+    const float* d_xyz = nullptr;
+    int n = 0;
+    DBuf<float> xyz;  // owned copy (host input path)
+    DBuf<float4> pts4;
+    // radius-ladder grids (cells seg_radius/16, /8, /4, /2) and the ISS grid (cell iss_salient)
+    bsh::DevGrid grid_l16, grid_fine, grid_l4, grid_coarse, grid_iss;
+    const bsh::DevGrid* ladder[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool grids_ok = false;
+    bool prefetched = false;  // loaded (and SR/ISS launched) ahead of use on the side stream
+    int sr_state = 0;         // 0 not launched, 1 launched (results land in h_ratio at ev_sr)
+    int iss_state = 0;        // 0 not launched, 1 launched (results land in h_flag at ev_iss)
+    DBuf<float> ratio;
+    DBuf<double> third;
+    DBuf<unsigned char> issflag;
+    DBuf<int> issovf;  // ISS overflow list: [0] = count, [1..] = point indices
+    DBuf<int> errw;    // [0] SR error bits, [1] ISS error bits
+    PinBuf<float> h_ratio;
+    PinBuf<unsigned char> h_flag;
+    PinBuf<int> h_err;  // [0] SR, [1] ISS
+    hipEvent_t ev_loaded = nullptr, ev_sr = nullptr, ev_iss = nullptr;
+    void fix_ladder(bool four) {
+        ladder[0] = four ? &grid_l16 : &grid_fine;
+        ladder[1] = &grid_fine;
+        ladder[2] = four ? &grid_l4 : &grid_coarse;
+        ladder[3] = &grid_coarse;
+    }
+    void release();
+};
+
 struct bshot_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // main: describe, match, ICP, and everything synchronous
+    hipStream_t side = nullptr;    // side: ISS and prefetched clouds
     bshot_params prm;
     std::string err;
     bool timing = false;
 
-    // cloud
-    int n = 0;
-    DBuf<float> xyz;          // owned copy (host input path)
-    const float* d_xyz = nullptr;
-    DBuf<float4> pts4;
-    bsh::DevGrid grid_fine, grid_coarse, grid_iss;  // cells seg_radius/8, seg_radius/2, iss_salient
-    bool grids_ok = false;
+    CloudState cs;  // current cloud
+    CloudState pf;  // prefetch slot
 
-    // per-point outputs
-    DBuf<float> ratio;
-    DBuf<double> third;
-    DBuf<unsigned char> issflag;
-    DBuf<int> errw;
+    // tuning knobs (bshot_set_option): results never depend on them
+    int opt_ladder4 = 0;  // 1: one grid per ladder step (cell = step radius / 2); 0: two grids
+    int opt_sr_hint = 0;  // 1: SR waves start the ladder at the previous query step
+    int opt_side_reserve = 32;  // CUs the side stream may not use (kept for the main stream)
+
+    DBuf<int> errw;  // describe-stage error bits (normals)
 
     // persistent normals (include/bshot_bits.h:59): logical size + grow-only storage
     DBuf<float4> normals;
@@ -69,10 +121,10 @@ struct bshot_ctx {
     DBuf<int> ok;
     DBuf<unsigned int> bits;
 
-    // match
-    DBuf<unsigned int> ma, mb;
-    DBuf<unsigned long long> lbest, rbest;
-    DBuf<int> left, right, mflag;
+    // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag
+    DBuf<unsigned int> ma;
+    DBuf<unsigned long long> lbest;
+    DBuf<int> left;
 
     // icp
     DBuf<float> isrc, itgt3;
@@ -83,9 +135,13 @@ struct bshot_ctx {
     DBuf<int> gidx;
     DBuf<float> gout;
 
-    // host staging
-    std::vector<float> h_ratio;
-    std::vector<unsigned char> h_flag;
+    // pinned staging of per-frame host<->device transfers (pageable copies stall behind other
+    // streams' work)
+    PinBuf<uint32_t> p_a, p_bits;
+    PinBuf<int> p_left, p_gidx, p_err;
+    PinBuf<float> p_g3, p_src, p_tgt;
+    PinBuf<unsigned long long> p_best;
+    PinBuf<long long> p_i64;
 
     // instrumentation
     std::vector<StageEv> pending;
@@ -96,20 +152,25 @@ struct bshot_ctx {
 
     int fail(const char* what, hipError_t e);
     int fail(const std::string& what, int code);
-    void stage_begin(int st);
-    void stage_end();
-    void resolve_events();
+    void stage_begin(int st, hipStream_t s = nullptr);
+    void stage_end(hipStream_t s = nullptr);
+    void resolve_events(bool wait = false);
     hipEvent_t get_ev();
 };
 
 namespace bsh {
 // internal entry points shared by the C ABI and the odometry driver
-int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n);
-int ctx_seg_ratio_dev(bshot_ctx* c);                    // writes c->ratio (device), no sync
-int ctx_iss_dev(bshot_ctx* c);                          // writes c->issflag (device), no sync
+int ctx_make_side_stream(bshot_ctx* c);
+int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n);  // adopts a matching prefetch
+int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n);   // grids + SR + ISS on the side stream
+int ctx_sr_launch(bshot_ctx* c);   // SR of the current cloud (main stream) unless already launched
+int ctx_iss_launch(bshot_ctx* c);  // ISS of the current cloud (side stream) unless already launched
 int ctx_describe_dev(bshot_ctx* c, int k);              // keypoints in c->kps; bits in c->bits
 int ctx_match_dev(bshot_ctx* c, int na, int nb);        // descriptors in c->ma / c->mb
 // H2D indices, gather xyz of pts4[idx] into dst (device, k x 3); async
 int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst);
+int ctx_sync_main(bshot_ctx* c);
+// device gather of cloud points -> host (pinned staging), synchronous
+int ctx_gather_host(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst, float* out);
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters);
 }  // namespace bsh

@@ -33,18 +33,38 @@ hipEvent_t bshot_ctx::get_ev() {
     (void)hipEventCreate(&e);
     return e;
 }
-void bshot_ctx::stage_begin(int st) {
+void bshot_ctx::stage_begin(int st, hipStream_t s) {
     if (!timing) return;
-    StageEv s{st, get_ev(), get_ev()};
-    (void)hipEventRecord(s.a, stream);
-    pending.push_back(s);
+    StageEv e{st, get_ev(), get_ev()};
+    (void)hipEventRecord(e.a, s ? s : stream);
+    pending.push_back(e);
 }
-void bshot_ctx::stage_end() {
+void bshot_ctx::stage_end(hipStream_t s) {
     if (!timing || pending.empty()) return;
-    (void)hipEventRecord(pending.back().b, stream);
+    (void)hipEventRecord(pending.back().b, s ? s : stream);
 }
-void bshot_ctx::resolve_events() {
+
+void CloudState::release() {
+    bsh::grid_free(grid_l16);
+    bsh::grid_free(grid_l4);
+    bsh::grid_free(grid_fine);
+    bsh::grid_free(grid_coarse);
+    bsh::grid_free(grid_iss);
+    xyz.release(); pts4.release(); ratio.release(); third.release(); issflag.release(); issovf.release();
+    errw.release(); h_ratio.release(); h_flag.release(); h_err.release();
+    for (hipEvent_t* e : {&ev_loaded, &ev_sr, &ev_iss})
+        if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
+}
+// harvest finished stage-event pairs; wait=true blocks on all of them (stage_times queries).
+// Without wait, pairs still in flight (e.g. the side stream's lookahead) stay pending, so
+// instrumentation never serialises the two streams.
+void bshot_ctx::resolve_events(bool wait) {
+    std::vector<StageEv> keep;
     for (auto& s : pending) {
+        if (!wait && hipEventQuery(s.b) != hipSuccess) {
+            keep.push_back(s);
+            continue;
+        }
         float ms = 0.f;
         if (hipEventSynchronize(s.b) == hipSuccess && hipEventElapsedTime(&ms, s.a, s.b) == hipSuccess) {
             stage_ms[s.stage] += ms;
@@ -53,60 +73,166 @@ void bshot_ctx::resolve_events() {
         evpool.push_back(s.a);
         evpool.push_back(s.b);
     }
-    pending.clear();
+    pending.swap(keep);
 }
 
 namespace bsh {
 
-int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n) {
-    if (n < 0) return c->fail("bshot_set_cloud: n < 0", BSHOT_EINVAL);
-    c->n = n;
-    c->d_xyz = d_xyz;
-    c->grids_ok = false;
-    HIPCHK(c->pts4.ensure(n > 0 ? n : 1), "alloc pts4");
-    if (n == 0) return BSHOT_OK;
-    c->stage_begin(BSHOT_STAGE_GRID);
-    HIPCHK(grid_build(c->grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, c->pts4.p, c->stream), "grid build (fine)");
-    HIPCHK(grid_build(c->grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, c->pts4.p, c->stream), "grid build (coarse)");
-    c->stage_end();
-    c->grids_ok = true;
+// side stream restricted to all but opt_side_reserve CUs, which stay free for the main stream
+int ctx_make_side_stream(bshot_ctx* c) {
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+        c->side = nullptr;
+    }
+    hipDeviceProp_t prop;
+    int ncu = 0;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) ncu = prop.multiProcessorCount;
+    const int keep = ncu - c->opt_side_reserve;
+    if (c->opt_side_reserve > 0 && ncu > 0 && keep >= 8) {
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < keep; ++i) mask[i / 32] |= 1u << (i % 32);
+        if (hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data()) == hipSuccess)
+            return BSHOT_OK;
+    }
+    return hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess ? BSHOT_OK : BSHOT_EHIP;
+}
+
+static hipError_t ensure_events(CloudState& s) {
+    for (hipEvent_t* e : {&s.ev_loaded, &s.ev_sr, &s.ev_iss})
+        if (!*e) {
+            hipError_t r = hipEventCreateWithFlags(e, hipEventDisableTiming);
+            if (r != hipSuccess) return r;
+        }
+    return hipSuccess;
+}
+
+// float4 copy + radius-ladder grids of one cloud, on stream st
+static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hipStream_t st) {
+    if (n < 0) return c->fail("set_cloud: n < 0", BSHOT_EINVAL);
+    s.n = n;
+    s.d_xyz = d_xyz;
+    s.grids_ok = false;
+    s.prefetched = false;
+    s.sr_state = 0;
+    s.iss_state = 0;
+    HIPCHK(ensure_events(s), "events");
+    HIPCHK(s.pts4.ensure(n > 0 ? n : 1), "alloc pts4");
+    HIPCHK(s.errw.ensure(2), "alloc err");
+    if (n > 0) {
+        c->stage_begin(BSHOT_STAGE_GRID, st);
+        HIPCHK(grid_build(s.grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, s.pts4.p, st), "grid build (r/8)");
+        HIPCHK(grid_build(s.grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, s.pts4.p, st), "grid build (r/2)");
+        if (c->opt_ladder4) {
+            HIPCHK(grid_build(s.grid_l16, d_xyz, n, c->prm.seg_radius * 0.0625f, s.pts4.p, st), "grid build (r/16)");
+            HIPCHK(grid_build(s.grid_l4, d_xyz, n, c->prm.seg_radius * 0.25f, s.pts4.p, st), "grid build (r/4)");
+        }
+        c->stage_end(st);
+    }
+    s.fix_ladder(c->opt_ladder4 != 0);
+    HIPCHK(hipEventRecord(s.ev_loaded, st), "record loaded");
+    s.grids_ok = true;
     return BSHOT_OK;
 }
 
-int ctx_seg_ratio_dev(bshot_ctx* c) {
+// SR of cloud s on stream st; ratios and error word land in pinned host memory at s.ev_sr
+static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     if (c->prm.seg_max_nn < 1 || c->prm.seg_max_nn > 512) return c->fail("seg_max_nn must be in [1, 512]", BSHOT_EINVAL);
-    HIPCHK(c->ratio.ensure(c->n > 0 ? c->n : 1), "alloc ratio");
-    HIPCHK(c->errw.ensure(1), "alloc err");
-    if (c->n == 0) return BSHOT_OK;
-    HIPCHK(hipMemsetAsync(c->errw.p, 0, sizeof(int), c->stream), "memset err");
-    c->stage_begin(BSHOT_STAGE_SR);
-    HIPCHK(launch_seg_ratio(c->grid_fine, c->grid_coarse, c->pts4.p, c->n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                            c->ratio.p, c->errw.p, c->stream),
-           "seg_ratio launch");
-    c->stage_end();
+    const int n = s.n;
+    HIPCHK(s.ratio.ensure(n > 0 ? n : 1), "alloc ratio");
+    HIPCHK(s.h_ratio.ensure(n > 0 ? n : 1), "alloc pinned ratio");
+    HIPCHK(s.h_err.ensure(2), "alloc pinned err");
+    HIPCHK(hipMemsetAsync(s.errw.p, 0, sizeof(int), st), "memset err");
+    if (n > 0) {
+        c->stage_begin(BSHOT_STAGE_SR, st);
+        HIPCHK(launch_seg_ratio(s.ladder, s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+                                c->opt_sr_hint, s.ratio.p, s.errw.p, st),
+               "seg_ratio launch");
+        c->stage_end(st);
+        HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
+    }
+    HIPCHK(hipMemcpyAsync(s.h_err.p, s.errw.p, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
+    HIPCHK(hipEventRecord(s.ev_sr, st), "record sr");
+    s.sr_state = 1;
     return BSHOT_OK;
 }
 
-int ctx_iss_dev(bshot_ctx* c) {
-    HIPCHK(c->third.ensure(c->n > 0 ? c->n : 1), "alloc third");
-    HIPCHK(c->issflag.ensure(c->n > 0 ? c->n : 1), "alloc issflag");
-    HIPCHK(c->errw.ensure(1), "alloc err");
-    if (c->n == 0) return BSHOT_OK;
-    HIPCHK(hipMemsetAsync(c->errw.p, 0, sizeof(int), c->stream), "memset err");
-    c->stage_begin(BSHOT_STAGE_ISS);
-    HIPCHK(grid_build(c->grid_iss, c->d_xyz, c->n, c->prm.iss_salient, c->pts4.p, c->stream), "grid build (ISS)");
-    HIPCHK(launch_iss(c->grid_iss, c->pts4.p, c->n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
-                      c->prm.iss_gamma21, c->prm.iss_gamma32, c->third.p, c->issflag.p, c->errw.p, c->stream),
-           "iss launch");
-    c->stage_end();
+// ISS of cloud s on stream st; flags and error word land in pinned host memory at s.ev_iss
+static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
+    const int n = s.n;
+    HIPCHK(s.third.ensure(n > 0 ? n : 1), "alloc third");
+    HIPCHK(s.issflag.ensure(n > 0 ? n : 1), "alloc issflag");
+    HIPCHK(s.issovf.ensure((size_t)n + 1), "alloc iss overflow");
+    HIPCHK(s.h_flag.ensure(n > 0 ? n : 1), "alloc pinned flags");
+    HIPCHK(s.h_err.ensure(2), "alloc pinned err");
+    HIPCHK(hipMemsetAsync(s.errw.p + 1, 0, sizeof(int), st), "memset err");
+    if (n > 0) {
+        c->stage_begin(BSHOT_STAGE_ISS, st);
+        HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient, s.pts4.p, st), "grid build (ISS)");
+        HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
+                          c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.errw.p + 1, st),
+               "iss launch");
+        c->stage_end(st);
+        HIPCHK(hipMemcpyAsync(s.h_flag.p, s.issflag.p, n, hipMemcpyDeviceToHost, st), "D2H iss");
+    }
+    HIPCHK(hipMemcpyAsync(s.h_err.p + 1, s.errw.p + 1, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
+    HIPCHK(hipEventRecord(s.ev_iss, st), "record iss");
+    s.iss_state = 1;
     return BSHOT_OK;
+}
+
+int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n) {
+    if (c->pf.prefetched && c->pf.d_xyz == d_xyz && c->pf.n == n && n > 0) {
+        std::swap(c->cs, c->pf);
+        c->cs.fix_ladder(c->opt_ladder4 != 0);
+        c->pf.fix_ladder(c->opt_ladder4 != 0);
+        c->cs.prefetched = false;
+        c->pf.prefetched = false;
+        HIPCHK(hipStreamWaitEvent(c->stream, c->cs.ev_loaded, 0), "wait prefetch");
+        return BSHOT_OK;
+    }
+    // the side stream may still read this cloud's buffers (ISS of the previous cloud)
+    if (c->cs.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->stream, c->cs.ev_iss, 0), "wait iss");
+    return cloud_load(c, c->cs, d_xyz, n, c->stream);
+}
+
+int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
+    if (n <= 0) return BSHOT_OK;
+    // the prefetch slot holds an older cloud; let work already queued on the main stream finish first
+    hipEvent_t e = c->get_ev();
+    HIPCHK(hipEventRecord(e, c->stream), "record");
+    HIPCHK(hipStreamWaitEvent(c->side, e, 0), "wait main");
+    c->evpool.push_back(e);
+    int rc = cloud_load(c, c->pf, d_xyz, n, c->side);
+    if (rc) return rc;
+    rc = cloud_sr(c, c->pf, c->side);
+    if (rc) return rc;
+    if (c->prm.run_iss) {
+        rc = cloud_iss(c, c->pf, c->side);
+        if (rc) return rc;
+    }
+    c->pf.prefetched = true;
+    return BSHOT_OK;
+}
+
+int ctx_sr_launch(bshot_ctx* c) {
+    if (!c->cs.grids_ok) return c->fail("seg_ratio: no cloud set", BSHOT_ESTATE);
+    if (c->cs.sr_state == 1) return BSHOT_OK;
+    return cloud_sr(c, c->cs, c->stream);
+}
+
+int ctx_iss_launch(bshot_ctx* c) {
+    if (!c->cs.grids_ok) return c->fail("iss: no cloud set", BSHOT_ESTATE);
+    if (c->cs.iss_state == 1) return BSHOT_OK;
+    HIPCHK(hipStreamWaitEvent(c->side, c->cs.ev_loaded, 0), "wait cloud");
+    return cloud_iss(c, c->cs, c->side);
 }
 
 // keypoints already in c->kps (device, k x 3)
 int ctx_describe_dev(bshot_ctx* c, int k) {
     if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > 512)
         return c->fail("normal_max_nn must be in [1, 512]", BSHOT_EINVAL);
-    const int n = c->n;
+    const int n = c->cs.n;
     // persistent normals array: resize(n) keeps [0, min) and value-initialises new slots
     HIPCHK(c->normals.ensure(std::max(n, std::max(k, 1))), "alloc normals");
     if (n > c->normals_size)
@@ -123,47 +249,44 @@ int ctx_describe_dev(bshot_ctx* c, int k) {
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
     c->stage_begin(BSHOT_STAGE_NORMALS);
-    HIPCHK(launch_normals(c->grid_fine, c->grid_coarse, c->pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
+    HIPCHK(launch_normals(c->cs.ladder, c->cs.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
                           c->normals.p, c->errw.p, c->stream),
            "normals launch");
     c->stage_end();
     const float R = c->prm.shot_radius;
     c->stage_begin(BSHOT_STAGE_SHOT_GATHER);
-    HIPCHK(launch_shot_count(c->grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, c->stream), "shot count");
+    HIPCHK(launch_shot_count(c->cs.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, c->stream), "shot count");
     c->stage_end();
-    long long total = 0;
-    HIPCHK(hipMemcpyAsync(&total, c->offs.p + k, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H total");
+    HIPCHK(c->p_i64.ensure(1), "alloc pinned");
+    HIPCHK(hipMemcpyAsync(c->p_i64.p, c->offs.p + k, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H total");
     HIPCHK(hipStreamSynchronize(c->stream), "sync total");
+    const long long total = c->p_i64.p[0];
     c->work[0] = total;
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
     c->stage_begin(BSHOT_STAGE_SHOT_GATHER);
-    HIPCHK(launch_shot_gather(c->grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, c->stream), "shot gather");
+    HIPCHK(launch_shot_gather(c->cs.grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, c->stream), "shot gather");
     c->stage_end();
     c->stage_begin(BSHOT_STAGE_SHOT_SORT);
     HIPCHK(launch_shot_sort(c->offs.p, k, R, c->seg.p, c->segtmp.p, c->stream), "shot sort");
     c->stage_end();
     c->stage_begin(BSHOT_STAGE_LRF);
-    HIPCHK(launch_lrf(c->pts4.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, c->stream), "lrf");
+    HIPCHK(launch_lrf(c->cs.pts4.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, c->stream), "lrf");
     c->stage_end();
     c->stage_begin(BSHOT_STAGE_HIST);
-    HIPCHK(launch_shot_hist(c->pts4.p, c->normals.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, c->shot.p,
+    HIPCHK(launch_shot_hist(c->cs.pts4.p, c->normals.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, c->shot.p,
                             c->bits.p, c->stream),
            "shot hist");
     c->stage_end();
     return BSHOT_OK;
 }
 
+// descriptors in c->ma (a rows then b rows); results in c->left (left | right | flag)
 int ctx_match_dev(bshot_ctx* c, int na, int nb) {
-    HIPCHK(c->lbest.ensure(na > 0 ? na : 1), "alloc lbest");
-    HIPCHK(c->rbest.ensure(nb > 0 ? nb : 1), "alloc rbest");
-    HIPCHK(c->left.ensure(na > 0 ? na : 1), "alloc left");
-    HIPCHK(c->right.ensure(nb > 0 ? nb : 1), "alloc right");
-    HIPCHK(c->mflag.ensure(na > 0 ? na : 1), "alloc mflag");
+    HIPCHK(c->lbest.ensure((size_t)na + nb + 1), "alloc best");
+    HIPCHK(c->left.ensure(2 * (size_t)na + nb + 1), "alloc match out");
     c->stage_begin(BSHOT_STAGE_MATCH);
-    HIPCHK(launch_match(c->ma.p, na, c->mb.p, nb, c->lbest.p, c->rbest.p, c->left.p, c->right.p, c->mflag.p,
-                        c->stream),
-           "match launch");
+    HIPCHK(launch_match(c->ma.p, na, c->ma.p + 11 * (size_t)na, nb, c->lbest.p, c->left.p, c->stream), "match launch");
     c->stage_end();
     return BSHOT_OK;
 }
@@ -172,8 +295,25 @@ int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst) {
     HIPCHK(c->gidx.ensure(k > 0 ? k : 1), "alloc gidx");
     HIPCHK(dst.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc gather out");
     if (k <= 0) return BSHOT_OK;
-    HIPCHK(hipMemcpyAsync(c->gidx.p, h_idx, sizeof(int) * k, hipMemcpyHostToDevice, c->stream), "H2D idx");
-    HIPCHK(launch_gather(c->pts4.p, c->gidx.p, k, dst.p, c->stream), "gather");
+    HIPCHK(c->p_gidx.ensure(k), "alloc pinned idx");
+    std::memcpy(c->p_gidx.p, h_idx, sizeof(int) * k);
+    HIPCHK(hipMemcpyAsync(c->gidx.p, c->p_gidx.p, sizeof(int) * k, hipMemcpyHostToDevice, c->stream), "H2D idx");
+    HIPCHK(launch_gather(c->cs.pts4.p, c->gidx.p, k, dst.p, c->stream), "gather");
+    return BSHOT_OK;
+}
+
+int ctx_gather_host(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst, float* out) {
+    int rc = ctx_gather(c, h_idx, k, dst);
+    if (rc || k <= 0) return rc;
+    HIPCHK(c->p_g3.ensure(3 * (size_t)k), "alloc pinned gather");
+    HIPCHK(hipMemcpyAsync(c->p_g3.p, dst.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, c->stream), "D2H gather");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync gather");
+    std::memcpy(out, c->p_g3.p, sizeof(float) * 3 * k);
+    return BSHOT_OK;
+}
+
+int ctx_sync_main(bshot_ctx* c) {
+    HIPCHK(hipStreamSynchronize(c->stream), "sync");
     return BSHOT_OK;
 }
 
@@ -181,31 +321,44 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
     bg::Mat4f fin = bg::Mat4f::identity();
     int it = 0;
     if (ns >= 3 && nt > 0) {
-        HIPCHK(c->isrc.ensure(3 * (size_t)ns), "alloc icp src");
+        // device: src double buffer (moved in place by each iteration's kernel), best double buffer
+        HIPCHK(c->isrc.ensure(6 * (size_t)ns), "alloc icp src");
         HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
-        HIPCHK(c->ibest.ensure(ns), "alloc icp best");
+        HIPCHK(c->ibest.ensure(2 * (size_t)ns), "alloc icp best");
         HIPCHK(c->itgt3.ensure(3 * (size_t)std::max(nt, 1)), "alloc icp staging");
-        HIPCHK(hipMemcpyAsync(c->itgt3.p, tgt, sizeof(float) * 3 * nt, hipMemcpyHostToDevice, c->stream), "H2D tgt");
+        HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
+        HIPCHK(c->p_src.ensure(3 * (size_t)ns), "alloc pinned src");
+        HIPCHK(c->p_best.ensure(ns), "alloc pinned best");
+        std::memcpy(c->p_tgt.p, tgt, sizeof(float) * 3 * nt);
+        std::memcpy(c->p_src.p, src, sizeof(float) * 3 * ns);
+        HIPCHK(hipMemcpyAsync(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * nt, hipMemcpyHostToDevice, c->stream),
+               "H2D tgt");
+        HIPCHK(hipMemcpyAsync(c->isrc.p, c->p_src.p, sizeof(float) * 3 * ns, hipMemcpyHostToDevice, c->stream),
+               "H2D src");
+        HIPCHK(hipMemsetAsync(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
         HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
-        std::vector<unsigned long long> best(ns);
+        const unsigned long long* best = c->p_best.p;
         double prev_mse = 1.7976931348623157e308;
+        bg::Mat4f Ts = bg::Mat4f::identity();
         while (true) {
-            HIPCHK(hipMemcpyAsync(c->isrc.p, cur.data(), sizeof(float) * 3 * ns, hipMemcpyHostToDevice, c->stream),
-                   "H2D src");
+            const int b = it & 1;
             c->stage_begin(BSHOT_STAGE_ICP);
-            HIPCHK(launch_icp_nn(c->isrc.p, ns, c->itgt.p, nt, c->ibest.p, c->stream), "icp nn");
+            HIPCHK(launch_icp_iter(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1), Ts.m, it > 0,
+                                   ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b, c->ibest.p + (size_t)ns * (b ^ 1),
+                                   c->stream),
+                   "icp iteration");
             c->stage_end();
-            HIPCHK(hipMemcpyAsync(best.data(), c->ibest.p, sizeof(unsigned long long) * ns, hipMemcpyDeviceToHost,
-                                  c->stream),
+            HIPCHK(hipMemcpyAsync(c->p_best.p, c->ibest.p + (size_t)ns * b, sizeof(unsigned long long) * ns,
+                                  hipMemcpyDeviceToHost, c->stream),
                    "D2H nn");
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
             for (int i = 0; i < ns; ++i) {
                 const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);
                 tb[3 * i] = tgt[3 * j]; tb[3 * i + 1] = tgt[3 * j + 1]; tb[3 * i + 2] = tgt[3 * j + 2];
             }
-            bg::Mat4f Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
-            for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);
+            Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
+            for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);  // the device applies Ts next launch
             fin = bg::mul(Ts, fin);
             ++it;
             if (it >= max_iter) break;
@@ -249,7 +402,12 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
     c->device = device;
     if (p) c->prm = *p;
     else bshot_default_params(&c->prm);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // main stream at the highest priority: its short kernels (match, ICP) run during the host
+    // phases while the side stream's lookahead SR fills the rest of the GPU
+    int lo_prio = 0, hi_prio = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio) != hipSuccess ||
+        bsh::ctx_make_side_stream(c) != BSHOT_OK) {
         delete c;
         return BSHOT_EHIP;
     }
@@ -261,24 +419,28 @@ void bshot_destroy(bshot_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    c->resolve_events();
+    (void)hipStreamSynchronize(c->side);
+    c->resolve_events(true);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
-    grid_free(c->grid_fine);
-    grid_free(c->grid_coarse);
-    grid_free(c->grid_iss);
-    c->xyz.release(); c->pts4.release(); c->ratio.release(); c->third.release(); c->issflag.release();
+    (void)hipStreamSynchronize(c->side);
+    c->cs.release();
+    c->pf.release();
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
     c->seg.release(); c->segtmp.release(); c->rf.release(); c->shot.release(); c->ok.release(); c->bits.release();
-    c->ma.release(); c->mb.release(); c->lbest.release(); c->rbest.release(); c->left.release(); c->right.release();
-    c->mflag.release(); c->gidx.release(); c->gout.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->ma.release(); c->lbest.release(); c->left.release();
+    c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
+    c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
+    c->gidx.release(); c->gout.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->side);
     delete c;
 }
 
 const char* bshot_last_error(const bshot_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int bshot_sync(bshot_ctx* c) {
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return c->fail("sync", hipGetLastError());
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess)
+        return c->fail("sync", hipGetLastError());
     c->resolve_events();
     return BSHOT_OK;
 }
@@ -288,9 +450,12 @@ void* bshot_stream(bshot_ctx* c) { return (void*)c->stream; }
 int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n) {
     if (!c || (n > 0 && !xyz)) return BSHOT_EINVAL;
     (void)hipSetDevice(c->device);
-    HIPCHK(c->xyz.ensure(3 * (size_t)(n > 0 ? n : 1)), "alloc xyz");
-    if (n > 0) HIPCHK(hipMemcpyAsync(c->xyz.p, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, c->stream), "H2D xyz");
-    return ctx_set_cloud_dev(c, c->xyz.p, n);
+    // the current cloud's buffers may still be read by the side stream (its ISS)
+    if (c->cs.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->stream, c->cs.ev_iss, 0), "wait iss");
+    HIPCHK(c->cs.xyz.ensure(3 * (size_t)(n > 0 ? n : 1)), "alloc xyz");
+    if (n > 0)
+        HIPCHK(hipMemcpyAsync(c->cs.xyz.p, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, c->stream), "H2D xyz");
+    return ctx_set_cloud_dev(c, c->cs.xyz.p, n);
 }
 
 int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
@@ -299,23 +464,25 @@ int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
     return ctx_set_cloud_dev(c, d_xyz, n);
 }
 
+int bshot_prefetch_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
+    if (!c || n < 0 || (n > 0 && !d_xyz)) return BSHOT_EINVAL;
+    (void)hipSetDevice(c->device);
+    return ctx_prefetch_dev(c, d_xyz, n);
+}
+
 int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
     if (!c || !n_out) return BSHOT_EINVAL;
-    int rc = ctx_seg_ratio_dev(c);
+    int rc = ctx_sr_launch(c);
     if (rc) return rc;
-    const int n = c->n;
-    c->h_ratio.resize(n > 0 ? n : 1);
-    int herr = 0;
-    if (n > 0) {
-        HIPCHK(hipMemcpyAsync(c->h_ratio.data(), c->ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream), "D2H ratio");
-        HIPCHK(hipMemcpyAsync(&herr, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H err");
-    }
-    HIPCHK(hipStreamSynchronize(c->stream), "sync ratio");
+    CloudState& s = c->cs;
+    HIPCHK(hipEventSynchronize(s.ev_sr), "sync ratio");
     c->resolve_events();
-    if (herr) return c->fail("seg_ratio: neighbourhood with > 1024 exactly tied boundary keys", BSHOT_ECAP);
+    if (s.h_err.p[0]) return c->fail("seg_ratio: neighbourhood with > 1024 exactly tied boundary keys", BSHOT_ECAP);
+    const int n = s.n;
+    const float* h = s.h_ratio.p;
     int m = 0;
     for (int i = 0; i < n; ++i) {
-        const float r = c->h_ratio[i];
+        const float r = h[i];
         if (r != r) continue;  // origin, non-finite or NaN ratio (src/lidar_odometry.cpp:63-64,121-122)
         idx[m] = i;
         ratio[m] = r;
@@ -327,21 +494,16 @@ int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
 
 int bshot_iss(bshot_ctx* c, int32_t* kp_idx, int cap, int* n_out) {
     if (!c || !n_out) return BSHOT_EINVAL;
-    int rc = ctx_iss_dev(c);
+    int rc = ctx_iss_launch(c);
     if (rc) return rc;
-    const int n = c->n;
-    c->h_flag.resize(n > 0 ? n : 1);
-    int herr = 0;
-    if (n > 0) {
-        HIPCHK(hipMemcpyAsync(c->h_flag.data(), c->issflag.p, n, hipMemcpyDeviceToHost, c->stream), "D2H iss");
-        HIPCHK(hipMemcpyAsync(&herr, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H err");
-    }
-    HIPCHK(hipStreamSynchronize(c->stream), "sync iss");
+    CloudState& s = c->cs;
+    HIPCHK(hipEventSynchronize(s.ev_iss), "sync iss");
     c->resolve_events();
-    if (herr & 4) return c->fail("iss: more than 512 neighbours inside the salient radius", BSHOT_ECAP);
+    if (s.h_err.p[1] & 4) return c->fail("iss: more than 512 neighbours inside the salient radius", BSHOT_ECAP);
+    const int n = s.n;
     int m = 0;
     for (int i = 0; i < n; ++i)
-        if (c->h_flag[i]) {
+        if (s.h_flag.p[i]) {
             if (m < cap) kp_idx[m] = i;
             ++m;
         }
@@ -351,7 +513,7 @@ int bshot_iss(bshot_ctx* c, int32_t* kp_idx, int cap, int* n_out) {
 
 int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf, uint32_t* bits) {
     if (!c || k < 0 || (k > 0 && (!kps || !bits))) return BSHOT_EINVAL;
-    if (!c->grids_ok && c->n > 0) return c->fail("bshot_describe: no cloud set", BSHOT_ESTATE);
+    if (!c->cs.grids_ok && c->cs.n > 0) return c->fail("bshot_describe: no cloud set", BSHOT_ESTATE);
     HIPCHK(c->kps.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc kps");
     if (k > 0) HIPCHK(hipMemcpyAsync(c->kps.p, kps, sizeof(float) * 3 * k, hipMemcpyHostToDevice, c->stream), "H2D kps");
     int rc = ctx_describe_dev(c, k);
@@ -382,18 +544,24 @@ int bshot_match(bshot_ctx* c, const uint32_t* a, int na, const uint32_t* b, int 
     if (!c || !n_corr || na < 0 || nb < 0) return BSHOT_EINVAL;
     *n_corr = 0;
     if (na == 0 || nb == 0) return BSHOT_OK;
-    HIPCHK(c->ma.ensure(11 * (size_t)na), "alloc ma");
-    HIPCHK(c->mb.ensure(11 * (size_t)nb), "alloc mb");
-    HIPCHK(hipMemcpyAsync(c->ma.p, a, sizeof(uint32_t) * 11 * na, hipMemcpyHostToDevice, c->stream), "H2D a");
-    HIPCHK(hipMemcpyAsync(c->mb.p, b, sizeof(uint32_t) * 11 * nb, hipMemcpyHostToDevice, c->stream), "H2D b");
+    HIPCHK(c->ma.ensure(11 * ((size_t)na + nb)), "alloc descriptors");
+    HIPCHK(c->p_a.ensure(11 * ((size_t)na + nb)), "alloc pinned descriptors");
+    HIPCHK(c->p_left.ensure(2 * (size_t)na + nb), "alloc pinned match out");
+    std::memcpy(c->p_a.p, a, sizeof(uint32_t) * 11 * na);
+    std::memcpy(c->p_a.p + 11 * (size_t)na, b, sizeof(uint32_t) * 11 * nb);
+    HIPCHK(hipMemcpyAsync(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * ((size_t)na + nb), hipMemcpyHostToDevice,
+                          c->stream),
+           "H2D descriptors");
     int rc = ctx_match_dev(c, na, nb);
     if (rc) return rc;
-    std::vector<int> flag(na);
-    HIPCHK(hipMemcpyAsync(left_nn, c->left.p, sizeof(int) * na, hipMemcpyDeviceToHost, c->stream), "D2H left");
-    HIPCHK(hipMemcpyAsync(right_nn, c->right.p, sizeof(int) * nb, hipMemcpyDeviceToHost, c->stream), "D2H right");
-    HIPCHK(hipMemcpyAsync(flag.data(), c->mflag.p, sizeof(int) * na, hipMemcpyDeviceToHost, c->stream), "D2H flag");
+    HIPCHK(hipMemcpyAsync(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb), hipMemcpyDeviceToHost,
+                          c->stream),
+           "D2H match");
     HIPCHK(hipStreamSynchronize(c->stream), "sync match");
     c->resolve_events();
+    std::memcpy(left_nn, c->p_left.p, sizeof(int) * na);
+    std::memcpy(right_nn, c->p_left.p + na, sizeof(int) * nb);
+    const int* flag = c->p_left.p + na + nb;
     int m = 0;
     for (int i = 0; i < na; ++i)
         if (flag[i]) { corr_q[m] = i; corr_m[m] = left_nn[i]; ++m; }
@@ -410,7 +578,7 @@ int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, 
 
 int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n) {
     if (!c) return BSHOT_EINVAL;
-    c->resolve_events();
+    c->resolve_events(true);
     for (int i = 0; i < n && i < BSHOT_NSTAGES; ++i) {
         if (ms) ms[i] = c->stage_ms[i];
         if (launches) launches[i] = c->stage_n[i];
@@ -420,7 +588,7 @@ int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n) {
 
 void bshot_stage_reset(bshot_ctx* c) {
     if (!c) return;
-    c->resolve_events();
+    c->resolve_events(true);
     for (int i = 0; i < BSHOT_NSTAGES; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
 }
 
@@ -431,16 +599,16 @@ void bshot_set_timing(bshot_ctx* c, int enabled) {
 int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total) {
     if (!c || !total) return BSHOT_EINVAL;
     *total = 0;
-    if (c->n == 0) return BSHOT_OK;
-    if (!c->grids_ok) return c->fail("bshot_radius_pairs: no cloud", BSHOT_ESTATE);
+    if (c->cs.n == 0) return BSHOT_OK;
+    if (!c->cs.grids_ok) return c->fail("bshot_radius_pairs: no cloud", BSHOT_ESTATE);
     DBuf<int> cnt;
     DBuf<long long> offs;
-    HIPCHK(cnt.ensure(c->n), "alloc counts");
-    HIPCHK(offs.ensure(c->n + 1), "alloc offs");
-    const bsh::DevGrid& g = R <= c->prm.iss_salient * 1.5f && c->grid_iss.n == c->n ? c->grid_iss : c->grid_coarse;
-    HIPCHK(launch_shot_count(g, c->d_xyz, c->n, R, cnt.p, offs.p, c->stream), "radius count");
+    HIPCHK(cnt.ensure(c->cs.n), "alloc counts");
+    HIPCHK(offs.ensure(c->cs.n + 1), "alloc offs");
+    const bsh::DevGrid& g = R <= c->prm.iss_salient * 1.5f && c->cs.grid_iss.n == c->cs.n ? c->cs.grid_iss : c->cs.grid_coarse;
+    HIPCHK(launch_shot_count(g, c->cs.d_xyz, c->cs.n, R, cnt.p, offs.p, c->stream), "radius count");
     long long t = 0;
-    HIPCHK(hipMemcpyAsync(&t, offs.p + c->n, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H");
+    HIPCHK(hipMemcpyAsync(&t, offs.p + c->cs.n, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H");
     HIPCHK(hipStreamSynchronize(c->stream), "sync");
     cnt.release();
     offs.release();
@@ -450,14 +618,13 @@ int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total) {
 
 int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
     if (!c || !out) return BSHOT_EINVAL;
-    if (!c->grids_ok) return c->fail("bshot_debug_knn_stats: no cloud", BSHOT_ESTATE);
+    if (!c->cs.grids_ok) return c->fail("bshot_debug_knn_stats: no cloud", BSHOT_ESTATE);
     DBuf<unsigned long long> k;
     HIPCHK(k.ensure(16), "alloc kst");
-    HIPCHK(c->ratio.ensure(c->n), "alloc ratio");
-    HIPCHK(c->errw.ensure(1), "alloc err");
+    HIPCHK(c->cs.ratio.ensure(c->cs.n), "alloc ratio");
     HIPCHK(hipMemsetAsync(k.p, 0, 16 * sizeof(unsigned long long), c->stream), "memset");
-    HIPCHK(launch_seg_ratio(c->grid_fine, c->grid_coarse, c->pts4.p, c->n, c->prm.seg_radius, c->prm.seg_max_nn,
-                            c->prm.sr_type, c->ratio.p, c->errw.p, c->stream, k.p),
+    HIPCHK(launch_seg_ratio(c->cs.ladder, c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+                            c->opt_sr_hint, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p),
            "seg_ratio (stats)");
     unsigned long long h[16];
     HIPCHK(hipMemcpyAsync(h, k.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
@@ -465,6 +632,19 @@ int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
     k.release();
     for (int i = 0; i < n && i < 16; ++i) out[i] = (int64_t)h[i];
     return 16;
+}
+
+int bshot_set_option(bshot_ctx* c, const char* name, int value) {
+    if (!c || !name) return BSHOT_EINVAL;
+    const std::string k(name);
+    if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
+    else if (k == "sr_hint") c->opt_sr_hint = value ? 1 : 0;
+    else if (k == "side_cu_reserve") {
+        c->opt_side_reserve = value < 0 ? 0 : value;
+        return bsh::ctx_make_side_stream(c);
+    }
+    else return c->fail("bshot_set_option: unknown option " + k, BSHOT_EINVAL);
+    return BSHOT_OK;
 }
 
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n) {

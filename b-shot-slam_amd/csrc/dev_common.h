@@ -27,6 +27,11 @@ struct GridView {
     float inv_cell;           // 1 / cell (only used for speed-insensitive cell ranges, see cell_of)
 };
 
+// the four grids of the exact-kNN radius ladder: step s searches radius r / 2^(3-s) on g[s]
+struct LadderGrids {
+    GridView g[4];
+};
+
 __device__ __forceinline__ unsigned long long cell_key(int ix, int iy, int iz) {
     return ((unsigned long long)(unsigned)(ix + (1 << 20)) << 42) | ((unsigned long long)(unsigned)(iy + (1 << 20)) << 21) |
            (unsigned long long)(unsigned)(iz + (1 << 20));
@@ -122,6 +127,15 @@ __device__ __forceinline__ double wave_tree_sum_d(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
     return v;
+}
+
+// diagnostic cycle stamp (debug counters only; never on the product path)
+__device__ __forceinline__ unsigned long long cycle_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
 }
 
 __device__ __forceinline__ unsigned int f2u(float f) { return __float_as_uint(f); }

@@ -6,12 +6,13 @@
 
 namespace bsh {
 
-hipError_t launch_seg_ratio(const DevGrid& gf, const DevGrid& gc, const float4* pts4, int n, float radius, int max_nn,
-                            int sr_type, float* ratio, int* err, hipStream_t s, unsigned long long* kst = nullptr);
-hipError_t launch_normals(const DevGrid& gf, const DevGrid& gc, const float4* pts4, const float* kps, int k,
-                          float radius, int max_nn, float4* normals, int* err, hipStream_t s);
+// g4: the radius-ladder grids, step s searching radius r / 2^(3-s) on g4[s]
+hipError_t launch_seg_ratio(const DevGrid* const* g4, const float4* pts4, int n, float radius, int max_nn, int sr_type,
+                            int hint, float* ratio, int* err, hipStream_t s, unsigned long long* kst = nullptr);
+hipError_t launch_normals(const DevGrid* const* g4, const float4* pts4, const float* kps, int k, float radius,
+                          int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
-                      double g32, double* third, unsigned char* flag, int* err, hipStream_t s);
+                      double g32, double* third, unsigned char* flag, int* ovf, int* err, hipStream_t s);
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s);
 hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
@@ -23,10 +24,12 @@ hipError_t launch_lrf(const float4* pts4, const float* kps, int k, float R, cons
 hipError_t launch_shot_hist(const float4* pts4, const float4* normals, const float* kps, int k, float R,
                             const long long* offs, const unsigned long long* seg, const float* rf, const int* ok,
                             float* shot, unsigned int* bits, hipStream_t s);
-hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* lbest,
-                        unsigned long long* rbest, int* left, int* right, int* flag, hipStream_t s);
+hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
+                        int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
+hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,
+                           int nt, unsigned long long* best, unsigned long long* best_next, hipStream_t s);
 hipError_t launch_icp_nn(const float* src, int ns, const float4* tgt, int nt, unsigned long long* best, hipStream_t s);
 
 }  // namespace bsh

@@ -127,21 +127,25 @@ __device__ __forceinline__ void rank_into_list(KnnLds* L, int tot, float sc0) {
 // Fast path: the ladder step that first holds >= max_nn points also stored every in-radius key
 // in LDS (ballot compaction while histogramming), so when they fit (<= KNN_CAP) the selection is
 // a counting sort over LDS only -- no second pass over the candidates.
-__device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, float qx, float qy, float qz, float r,
-                           int max_nn, int* need_out, unsigned long long* kst, const unsigned long long** sorted) {
+// start_step: first ladder step tried (any step is exact; a later start only costs work);
+// *step_out: the step whose radius delivered the result; *total_out: in-radius count there.
+__device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
+                           int start_step, int* need_out, int* step_out, int* total_out, unsigned long long* kst,
+                           const unsigned long long** sorted) {
     unsigned long long chunks = 0;
     const int lane = lane_id();
+    const unsigned long long ts0 = kst ? cycle_stamp() : 0ull;
     const float r2 = (float)((double)r * (double)r);
     float rs = r, rs2 = r2;
     int total = 0;
-    int step = 0;
+    int step = start_step;
     for (; step < 4; ++step) {
         rs = step == 0 ? r * 0.125f : (step == 1 ? r * 0.25f : (step == 2 ? r * 0.5f : r));
         rs2 = step == 3 ? r2 : (float)((double)rs * (double)rs);
         hist_clear(L);
         const float sc = (float)KNN_NB / rs2;
         int cnt = 0;
-        for_candidates(step < 2 ? gf : gc, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        for_candidates(lg.g[step], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             ++chunks;
             if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
             const unsigned long long m = __ballot(v);
@@ -157,12 +161,16 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
         if (total >= max_nn) break;
     }
     if (step > 3) step = 3;
-    const GridView& g = step < 2 ? gf : gc;
+    const GridView& g = lg.g[step];
     const int need = total < max_nn ? total : max_nn;
     *need_out = need;
+    *step_out = step;
+    *total_out = total;
     if (need == 0) return true;
     const float sc0 = (float)KNN_NB / rs2;
+    const unsigned long long ts1 = kst ? cycle_stamp() : 0ull;
     if (kst && lane == 0) {
+        atomicAdd(&kst[12], ts1 - ts0);
         atomicAdd(&kst[0], 1ull);
         atomicAdd(&kst[1 + step], 1ull);
         atomicAdd(&kst[9], (unsigned long long)need);
@@ -186,7 +194,10 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
             __builtin_amdgcn_wave_barrier();
             rank_into_list(L, tot, sc0);
             *sorted = L->list;
-            if (kst && lane == 0) atomicAdd(&kst[5], chunks);
+            if (kst) {
+                const unsigned long long ts2 = cycle_stamp();
+                if (lane == 0) { atomicAdd(&kst[5], chunks); atomicAdd(&kst[13], ts2 - ts1); }
+            }
             return true;
         }
         // a boundary bucket too crowded for the scatter buffer: refine by streaming (rare)
@@ -251,7 +262,10 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
             __builtin_amdgcn_wave_barrier();
             rank_into_list(L, tot, sc0);
             *sorted = L->list;
-            if (kst && lane == 0) atomicAdd(&kst[5], chunks);
+            if (kst) {
+                const unsigned long long ts2 = cycle_stamp();
+                if (lane == 0) { atomicAdd(&kst[5], chunks); atomicAdd(&kst[14], ts2 - ts1); }
+            }
             return true;
         }
     }
@@ -282,9 +296,13 @@ __device__ bool knn_select(const GridView& gf, const GridView& gc, KnnLds* L, fl
     if (cnt > KNN_CAP) return false;
     int P = 64;
     while (P < cnt) P <<= 1;
-    if (kst && lane == 0) {
-        atomicAdd(&kst[5], chunks);
-        atomicAdd(&kst[8], (unsigned long long)P);
+    if (kst) {
+        const unsigned long long ts2 = cycle_stamp();
+        if (lane == 0) {
+            atomicAdd(&kst[5], chunks);
+            atomicAdd(&kst[8], (unsigned long long)P);
+            atomicAdd(&kst[14], ts2 - ts1);
+        }
     }
     for (int i = cnt + lane; i < P; i += 64) L->list[i] = ~0ull;
     __builtin_amdgcn_wave_barrier();
@@ -342,8 +360,11 @@ __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, con
 
 // ------------------------------------------------------------------------------------------
 // A1: segmentation ratio of every point. max_nn <= 512 (host-checked).
-__global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView gf, GridView gc, const float4* __restrict__ pts4,
-                                                              int n, float radius, int max_nn, int sr_type,
+// hint != 0: a wave starts each query's ladder at the step that served its previous query (one
+// step lower when that step held >= 4 x max_nn points). Consecutive queries of a wave are the same
+// beam a few azimuth columns apart, so their k-NN radii are close; results do not depend on it.
+__global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
+                                                              float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
                                                               unsigned long long* __restrict__ kst) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -356,15 +377,19 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView gf, GridV
     const int per = (n + 7) >> 3;
     const int q_begin = xg * per, q_end = min(n, q_begin + per);
     float* fl = reinterpret_cast<float*>(L->list);
+    int start = 0;
     for (int q = q_begin + gi * KNN_WAVES + wave; q < q_end; q += ng * KNN_WAVES) {
         const float4 sp = pts4[q];
         float out = __builtin_nanf("");
         const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
         const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
         if (!origin && fin) {
-            int need = 0;
+            int need = 0, used = 0, tot = 0;
             const unsigned long long* sorted = nullptr;
-            if (!knn_select(gf, gc, L, sp.x, sp.y, sp.z, radius, max_nn, &need, kst, &sorted)) {
+            const bool ok = knn_select(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
+            const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
+            if (hint) start = (tot >= 4 * max_nn && used > 0) ? used - 1 : used;
+            if (!ok) {
                 if (lane == 0) atomicOr(err, 1);
             } else if (need > 0) {
                 gather_xyz(sorted, pts4, need, fl);
@@ -414,6 +439,10 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView gf, GridV
                     out = fabsf(sum) / (float)need;
                 }
             }
+            if (kst) {
+                const unsigned long long tm1 = cycle_stamp();
+                if (lane == 0) atomicAdd(&kst[15], tm1 - tm0);
+            }
         }
         if (lane == 0) ratio[q] = out;
         __builtin_amdgcn_wave_barrier();
@@ -422,7 +451,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(GridView gf, GridV
 
 // ------------------------------------------------------------------------------------------
 // A4: normals of K keypoints written to slots [0, K) of the persistent N-sized array
-__global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView gf, GridView gc, const float4* __restrict__ pts4,
+__global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(LadderGrids lg, const float4* __restrict__ pts4,
                                                             const float* __restrict__ kps, int k, float radius,
                                                             int max_nn, float4* __restrict__ normals,
                                                             int* __restrict__ err) {
@@ -436,9 +465,9 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(GridView gf, GridVie
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         float nx = qn, ny = qn, nz = qn, curv = qn;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
-            int need = 0;
+            int need = 0, used = 0, tot = 0;
             const unsigned long long* sorted = nullptr;
-            if (!knn_select(gf, gc, L, kx, ky, kz, radius, max_nn, &need, nullptr, &sorted)) {
+            if (!knn_select(lg, L, kx, ky, kz, radius, max_nn, 0, &need, &used, &tot, nullptr, &sorted)) {
                 if (lane == 0) atomicOr(err, 2);
             } else if (need > 0) {
                 if (need >= 3) {
@@ -486,24 +515,29 @@ size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES; }
 
 namespace bsh {
 
-hipError_t launch_seg_ratio(const DevGrid& gf, const DevGrid& gc, const float4* pts4, int n, float radius, int max_nn,
-                            int sr_type, float* ratio, int* err, hipStream_t s, unsigned long long* kst) {
+static LadderGrids ladder(const DevGrid* const* g4) {
+    LadderGrids lg;
+    for (int i = 0; i < 4; ++i) lg.g[i] = g4[i]->view();
+    return lg;
+}
+
+hipError_t launch_seg_ratio(const DevGrid* const* g4, const float4* pts4, int n, float radius, int max_nn, int sr_type,
+                            int hint, float* ratio, int* err, hipStream_t s, unsigned long long* kst) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     if (blocks > 8 * 256 * 4) blocks = 8 * 256 * 4;
     blocks = (blocks + 7) & ~7;
-    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(gf.view(), gc.view(), pts4, n, radius, max_nn, sr_type, ratio,
+    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4), pts4, n, radius, max_nn, sr_type, hint, ratio,
                                                          err, kst);
     return hipGetLastError();
 }
 
-hipError_t launch_normals(const DevGrid& gf, const DevGrid& gc, const float4* pts4, const float* kps, int k,
-                          float radius, int max_nn, float4* normals, int* err, hipStream_t s) {
+hipError_t launch_normals(const DevGrid* const* g4, const float4* pts4, const float* kps, int k, float radius,
+                          int max_nn, float4* normals, int* err, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (k + KNN_WAVES - 1) / KNN_WAVES;
-    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(gf.view(), gc.view(), pts4, kps, k, radius, max_nn, normals,
-                                                       err);
+    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4), pts4, kps, k, radius, max_nn, normals, err);
     return hipGetLastError();
 }
 

@@ -17,9 +17,21 @@ namespace bsk {
 #define HM_THREADS 256
 #define HM_TILE 1024
 
-__global__ void __launch_bounds__(HM_THREADS) k_ham_min(const unsigned int* __restrict__ q, int nq,
-                                                        const unsigned int* __restrict__ r, int nr, int tile,
-                                                        unsigned long long* __restrict__ best) {
+// both directions in one launch: blockIdx.z == 0 -> A vs B (left), 1 -> B vs A (right)
+struct HamDir {
+    const unsigned int* q;
+    const unsigned int* r;
+    unsigned long long* best;
+    int nq, nr, tile, qb, splits;
+};
+
+__global__ void __launch_bounds__(HM_THREADS) k_ham_min(HamDir d0, HamDir d1) {
+    const HamDir& D = blockIdx.z == 0 ? d0 : d1;
+    if ((int)blockIdx.x >= D.qb || (int)blockIdx.y >= D.splits) return;
+    const unsigned int* __restrict__ q = D.q;
+    const unsigned int* __restrict__ r = D.r;
+    unsigned long long* __restrict__ best = D.best;
+    const int nq = D.nq, nr = D.nr, tile = D.tile;
     __shared__ uint4 rt[HM_TILE * 3];
     const int t = threadIdx.x;
     const int qi = blockIdx.x * HM_THREADS + t;
@@ -57,11 +69,6 @@ __global__ void __launch_bounds__(HM_THREADS) k_ham_min(const unsigned int* __re
     if (qi < nq) atomicMin(&best[qi], m);
 }
 
-__global__ void k_fill_u64(unsigned long long* p, int n, unsigned long long v) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = v;
-}
-
 __global__ void k_mutual(const unsigned long long* __restrict__ lbest, int na, const unsigned long long* __restrict__ rbest,
                          int* __restrict__ left, int* __restrict__ right, int nb, int* __restrict__ flag) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -77,26 +84,31 @@ __global__ void k_mutual(const unsigned long long* __restrict__ lbest, int na, c
 
 namespace bsh {
 
-static void ham_dir(const unsigned int* q, int nq, const unsigned int* r, int nr, unsigned long long* best,
-                    hipStream_t s) {
-    bsk::k_fill_u64<<<(nq + 255) / 256, 256, 0, s>>>(best, nq, ~0ull);
+static bsk::HamDir ham_dir(const unsigned int* q, int nq, const unsigned int* r, int nr, unsigned long long* best) {
     // split the reference set so the launch has >= ~1024 workgroups when nq is small
-    const int qb = (nq + HM_THREADS - 1) / HM_THREADS;
-    int splits = (1024 + qb - 1) / qb;
+    bsk::HamDir d;
+    d.q = q; d.r = r; d.best = best; d.nq = nq; d.nr = nr;
+    d.qb = (nq + HM_THREADS - 1) / HM_THREADS;
+    int splits = (1024 + d.qb - 1) / d.qb;
     int tile = (nr + splits - 1) / splits;
     if (tile < 256) tile = 256;
-    splits = (nr + tile - 1) / tile;
-    dim3 grid(qb, splits);
-    bsk::k_ham_min<<<grid, HM_THREADS, 0, s>>>(q, nq, r, nr, tile, best);
+    d.tile = tile;
+    d.splits = (nr + tile - 1) / tile;
+    return d;
 }
 
-hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* lbest,
-                        unsigned long long* rbest, int* left, int* right, int* flag, hipStream_t s) {
+// a: na x 11 words, b: nb x 11 words; best: na + nb packed keys (left then right), reset here;
+// out: left[na] | right[nb] | flag[na]
+hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
+                        int* out, hipStream_t s) {
     if (na <= 0 || nb <= 0) return hipSuccess;
-    ham_dir(a, na, b, nb, lbest, s);
-    ham_dir(b, nb, a, na, rbest, s);
+    hipError_t e = hipMemsetAsync(best, 0xFF, sizeof(unsigned long long) * ((size_t)na + nb), s);
+    if (e != hipSuccess) return e;
+    const bsk::HamDir d0 = ham_dir(a, na, b, nb, best), d1 = ham_dir(b, nb, a, na, best + na);
+    dim3 grid(d0.qb > d1.qb ? d0.qb : d1.qb, d0.splits > d1.splits ? d0.splits : d1.splits, 2);
+    bsk::k_ham_min<<<grid, HM_THREADS, 0, s>>>(d0, d1);
     const int m = na > nb ? na : nb;
-    bsk::k_mutual<<<(m + 255) / 256, 256, 0, s>>>(lbest, na, rbest, left, right, nb, flag);
+    bsk::k_mutual<<<(m + 255) / 256, 256, 0, s>>>(best, na, best + na, out, out + na, nb, out + na + nb);
     return hipGetLastError();
 }
 

@@ -68,6 +68,10 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
     check(bshot_set_cloud_device(ctx_, d_xyz, n), "setSrcFrameDevice");
 }
 
+void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
+    check(bshot_prefetch_cloud_device(ctx_, d_xyz, n), "prefetchFrameDevice");
+}
+
 void LidarOdometry::passSrc2Ref() {
     ref_ = src_;
     ref_pc_ = src_pc_;
@@ -78,10 +82,7 @@ void LidarOdometry::passSrc2Ref() {
 static PointCloudXYZ gather_points(bshot_ctx* c, const std::vector<int32_t>& idx, DBuf<float>& dst) {
     PointCloudXYZ out(idx.size());
     if (idx.empty()) return out;
-    if (bsh::ctx_gather(c, idx.data(), (int)idx.size(), dst) != BSHOT_OK ||
-        hipMemcpyAsync(&out[0][0], dst.p, sizeof(float) * 3 * idx.size(), hipMemcpyDeviceToHost, c->stream) !=
-            hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    if (bsh::ctx_gather_host(c, idx.data(), (int)idx.size(), dst, &out[0][0]) != BSHOT_OK)
         throw std::runtime_error(std::string("gather: ") + c->err);
     return out;
 }
@@ -95,6 +96,8 @@ void LidarOdometry::extractKeypoints() {
     std::vector<int32_t> idx(n > 0 ? n : 1), kidx(prm_.num_keypoints > 0 ? prm_.num_keypoints : 1);
     std::vector<float> ratio(n > 0 ? n : 1), kr(kidx.size());
     int nv = 0, k = 0;
+    // ISS is independent of SR: it runs on the side stream while SR, top-K and the gather proceed
+    if (prm_.run_iss) check(bsh::ctx_iss_launch(ctx_), "iss launch");
     check(bshot_seg_ratio(ctx_, idx.data(), ratio.data(), &nv), "seg_ratio");
     check(bshot_select_topk(idx.data(), ratio.data(), nv, prm_.num_keypoints, kidx.data(), kr.data(), &k), "topk");
     kidx.resize(k);
@@ -129,16 +132,19 @@ void LidarOdometry::computeDescriptors() {
     TicToc t_d;
     const int k = (int)cloud1_kps_.size();
     check(bsh::ctx_describe_dev(ctx_, k), "describe");
-    std::vector<uint32_t> words(11 * (size_t)(k > 0 ? k : 1));
+    check(ctx_->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned bits");
+    check(ctx_->p_err.ensure(1) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned err");
+    const uint32_t* words = ctx_->p_bits.p;
     if (k > 0) {
-        if (hipMemcpyAsync(words.data(), ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
-                           ctx_->stream) != hipSuccess)
+        if (hipMemcpyAsync(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
+                           ctx_->stream) != hipSuccess ||
+            hipMemcpyAsync(ctx_->p_err.p, ctx_->errw.p, sizeof(int), hipMemcpyDeviceToHost, ctx_->stream) !=
+                hipSuccess)
             check(BSHOT_EHIP, "D2H bits");
     }
-    check(bshot_sync(ctx_), "describe sync");
-    int herr = 0;
-    if (ctx_->errw.p && hipMemcpy(&herr, ctx_->errw.p, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && (herr & 2))
-        check(BSHOT_ECAP, "normals neighbourhood overflow");
+    check(bsh::ctx_sync_main(ctx_), "describe sync");
+    ctx_->resolve_events();
+    if (k > 0 && (ctx_->p_err.p[0] & 2)) check(BSHOT_ECAP, "normals neighbourhood overflow");
     cloud1_bshot_.resize(k);
     auto desc = std::make_shared<std::vector<std::bitset<352>>>();
     desc->reserve(k);

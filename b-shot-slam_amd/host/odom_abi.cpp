@@ -16,6 +16,8 @@ struct bshot_odom {
     std::string err;
     std::vector<float> delta;  // last frame's map delta, 15 floats per keypoint
     std::vector<myslam::Map> replicas;
+    const float* next_d = nullptr;  // lookahead cloud (bshot_odom_set_next_device)
+    int next_n = 0;
 };
 
 static int guard(bshot_odom* o, const std::function<void()>& f);
@@ -37,6 +39,12 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     else lo.setSrcFrameDevice(f, d_xyz, n);
     lo.extractKeypoints();
     lo.computeDescriptors();
+    if (o->next_d) {
+        // the next sweep's grids, SR and ISS run on the side stream while the host matches,
+        // runs RANSAC/ICP and updates the map for this one
+        lo.prefetchFrameDevice(o->next_d, o->next_n);
+        o->next_d = nullptr;
+    }
     lo.featureMatching();
     lo.evaluateEstimation();
     lo.poseEstimation();
@@ -104,6 +112,13 @@ int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p) {
 void bshot_odom_destroy(bshot_odom* o) { delete o; }
 
 const char* bshot_odom_last_error(const bshot_odom* o) { return o ? o->err.c_str() : "null"; }
+
+int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next) {
+    if (!o || n_next < 0 || (n_next > 0 && !d_next)) return BSHOT_EINVAL;
+    o->next_d = n_next > 0 ? d_next : nullptr;
+    o->next_n = n_next;
+    return BSHOT_OK;
+}
 
 int bshot_odom_process(bshot_odom* o, const float* xyz, int n, bshot_frame_stats* st) {
     if (!o || n < 0 || (n > 0 && !xyz)) return BSHOT_EINVAL;

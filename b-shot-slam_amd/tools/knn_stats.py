@@ -7,4 +7,4 @@ c.set_cloud(pc)
 c.seg_ratio()
 s = c.knn_stats()
 q = s[0]
-print(json.dumps({"queries": q, "steps": s[1:5], "chunks_per_q": s[5]/q, "refine": s[7], "avgP": s[8]/q, "avg_need": s[9]/q, "avg_total": s[10]/q}))
+print(json.dumps({"queries": q, "steps": s[1:5], "chunks_per_q": s[5]/q, "refine": s[7], "avgP": s[8]/q, "avg_need": s[9]/q, "avg_total": s[10]/q, "streamed": s[11]}))

@@ -1,0 +1,37 @@
+"""Diagnostic: SR kernel time and kNN work counters per tuning-knob setting (same results required)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np  # noqa: E402
+
+import bshot_py  # noqa: E402
+
+pc, _ = bshot_py.synth_sweep(3)
+ref = None
+for ladder in (2, 4):
+    for hint in (0, 1):
+        c = bshot_py.Context(0)
+        c.set_option("ladder_grids", ladder)
+        c.set_option("sr_hint", hint)
+        c.set_cloud(pc)
+        c.seg_ratio()
+        c.set_timing(True)
+        c.stage_reset()
+        for _ in range(10):
+            c.set_cloud(pc)
+            idx, rat = c.seg_ratio()
+        st = c.stage_times()
+        c.set_timing(False)
+        s = c.knn_stats()
+        q = s[0]
+        same = ref is None or (np.array_equal(idx, ref[0]) and np.array_equal(rat.view(np.uint32), ref[1].view(np.uint32)))
+        if ref is None:
+            ref = (idx, rat)
+        print(json.dumps({"ladder": ladder, "hint": hint, "sr_ms": st["seg_ratio"][0] / 10, "grid_ms": st["grid"][0] / 10,
+                          "steps": s[1:5], "chunks_per_q": s[5] / q, "avg_total": s[10] / q, "streamed": s[11],
+                          "refine": s[7], "identical": bool(same),
+                          "cyc_ladder": s[12] / q, "cyc_fastsel": s[13] / q, "cyc_streamsel": s[14] / q,
+                          "cyc_math": s[15] / q}))
+        c.close()

@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="process sweeps strictly one after another (no lookahead of the next sweep's SR/ISS)")
+    ap.add_argument("--ladder-grids", type=int, default=None, help="tuning knob: 2 or 4 kNN ladder grids")
+    ap.add_argument("--sr-hint", type=int, default=None, help="tuning knob: SR ladder start hint 0/1")
+    ap.add_argument("--side-cu-reserve", type=int, default=None, help="tuning knob: CUs kept from the side stream")
     return ap.parse_args()
 
 
@@ -92,9 +97,17 @@ def main():
     npts = [int(x.shape[0]) for x in frames]
 
     odo = bshot_py.Odometry(device=local, params=params)
+    for name, val in (("ladder_grids", a.ladder_grids), ("sr_hint", a.sr_hint),
+                      ("side_cu_reserve", a.side_cu_reserve)):
+        if val is not None:
+            odo.set_option(name, val)
     tot_pts = 0
 
     def step(i):
+        # lookahead inside each region only: the last warm-up sweep does not start the first timed
+        # sweep, so the timed region holds exactly K sweeps' work
+        if not a.no_prefetch and i + 1 < nframes and i + 1 != a.warmup:
+            odo.set_next_device(frames[i + 1].data_ptr(), npts[i + 1])
         st = odo.process_device(frames[i].data_ptr(), npts[i])
         if a.map_bcast and world > 1:
             for r, rec in exchange_map_delta(odo.map_delta(), dist, dev):
@@ -179,6 +192,9 @@ def main():
     if rank == 0:
         if a.profile_stages:
             print(json.dumps({k: [round(v[0], 3), v[1]] for k, v in stages.items()}), file=sys.stderr)
+            hm = np.mean([list(s.host_ms) for s in stats], axis=0)
+            print(json.dumps({"host_ms_per_sweep": dict(zip(bshot_py.FrameStats.HOST_PHASES, np.round(hm, 3).tolist()))}),
+                  file=sys.stderr)
         line = {
             "metric": "Velodyne-64 sweeps/sec (extract+match+ICP)",
             "value": round(value, 3),

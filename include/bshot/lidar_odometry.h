@@ -32,6 +32,8 @@ class LidarOdometry {
     void setSrcFrame(Frame::Ptr src);
     // device-resident cloud (n x 3 floats already in HBM); the Frame keeps a host copy lazily
     void setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n);
+    // extension: start grids + SR + ISS of the next device-resident sweep on the side stream
+    void prefetchFrameDevice(const float* d_xyz, int n);
     void extractKeypoints();
     void computeDescriptors();
     void featureMatching();

@@ -65,6 +65,11 @@ void* bshot_stream(bshot_ctx* c);
 int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n);         /* host pointer (H2D copy) */
 int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n); /* device-resident input */
 
+/* ---- lookahead (throughput mode): build the grids of a FUTURE device-resident cloud and run its SR
+ *      and ISS on the context's side stream now; the next bshot_set_cloud_device with the same
+ *      pointer and size adopts the results instead of recomputing them. d_xyz must stay valid. */
+int bshot_prefetch_cloud_device(bshot_ctx* c, const float* d_xyz, int n);
+
 /* ---- A1: segmentation ratio for every point, index order, origin / NaN skipped
  *      (replaces the loop at src/lidar_odometry.cpp:53-126). idx/ratio caller-sized >= n. --- */
 int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out);
@@ -119,6 +124,9 @@ const char* bshot_odom_last_error(const bshot_odom* o);
 /* one sweep through extract + describe + match + RANSAC + gate + ICP + map update */
 int bshot_odom_process(bshot_odom* o, const float* xyz, int n, bshot_frame_stats* st);
 int bshot_odom_process_device(bshot_odom* o, const float* d_xyz, int n, bshot_frame_stats* st);
+/* lookahead: the device cloud the NEXT bshot_odom_process_device call will receive; its grids,
+ * SR and ISS start on the side stream during the current frame's host phases (must stay valid) */
+int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next);
 int bshot_odom_get_keypoints(bshot_odom* o, float* xyz, int cap);
 int bshot_odom_get_ratios(bshot_odom* o, float* r, int cap);
 int bshot_odom_get_bits(bshot_odom* o, uint32_t* bits, int cap);
@@ -144,6 +152,12 @@ int bshot_map_add(bshot_map* m, const float* xyz, float ratio, const uint32_t* b
 int bshot_map_query(bshot_map* m, const float* pos, float range, float* xyz, uint32_t* bits, int cap);
 int bshot_map_size(bshot_map* m);
 uint64_t bshot_map_block_id(const float* pos);
+
+/* ---- tuning knobs (results never depend on them): "ladder_grids" 2 (default) or 4 grids for the
+ *      exact-kNN radius ladder; "sr_hint" 0 (default) / 1: SR queries start the ladder at the
+ *      step that served the wave's previous query. Takes effect at the next bshot_set_cloud.
+ *      "side_cu_reserve" N (default 32): CUs the side stream (ISS, lookahead) leaves to the main one. */
+int bshot_set_option(bshot_ctx* c, const char* name, int value);
 
 /* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's
  *      stream since the last reset. Stage ids below. */
