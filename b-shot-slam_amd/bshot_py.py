@@ -60,6 +60,7 @@ ABI_SYMBOLS = [
     "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
+    "bshot_odom_set_option",
 ]
 
 _lib = None
@@ -357,7 +358,7 @@ class Odometry:
         return {STAGE_NAMES[i]: (ms[i], nl[i]) for i in range(NSTAGES)}
 
     def set_option(self, name, value):
-        if self.L.bshot_set_option(P(self.context()), name.encode(), int(value)) < 0:
+        if self.L.bshot_odom_set_option(self.h, name.encode(), int(value)) < 0:
             raise BshotError(f"set_option {name}")
 
     def set_timing(self, on):
