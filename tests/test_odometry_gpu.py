@@ -68,3 +68,27 @@ def test_odometry_vlp128_cvsn():
 
 def test_odometry_no_icp_no_iss():
     _run_pair(range(3), run_icp=0, run_iss=0)
+
+
+def test_odometry_lookahead_device_frames():
+    """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
+    stream during the current one (bshot_odom_set_next_device) -- results must not change."""
+    import torch
+
+    frames = [bshot_py.synth_sweep(f)[0] for f in range(20, 24)]
+    dev = [torch.from_numpy(x).to("cuda:0") for x in frames]
+    torch.cuda.synchronize()
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=1024))
+    oo = orc.Odometry(orc.params(num_keypoints=1024))
+    try:
+        for f, (xyz, d) in enumerate(zip(frames, dev)):
+            if f + 1 < len(dev):
+                od.set_next_device(dev[f + 1].data_ptr(), len(frames[f + 1]))
+            st = od.process_device(d.data_ptr(), len(xyz))
+            so = oo.process(xyz)
+            assert st.n_keypoints == so.n_keypoints and st.n_iss == so.n_iss and st.n_inliers == so.n_inliers, f
+            assert np.array_equal(od.bits(), oo.bits()), f
+            assert np.array_equal(od.iss(), oo.iss()), f
+            assert np.array_equal(_u(np.array(st.pose, np.float32)), _u(np.array(so.pose, np.float32))), f
+    finally:
+        od.close()
