@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -55,6 +56,8 @@ struct PinBuf {
 struct StageEv {
     int stage;
     hipEvent_t a, b;
+    int id;
+    bool ended;
 };
 
 // Everything that belongs to one input cloud: float4 copy, radius-ladder and ISS grids, SR ratios,
@@ -120,6 +123,15 @@ struct bshot_ctx {
     DBuf<float> rf, shot;
     DBuf<int> ok;
     DBuf<unsigned int> bits;
+    // load-balanced SHOT (describe2.hip)
+    DBuf<int4> plan;
+    DBuf<int> cb, owner, okf, signs, perm;
+    DBuf<double> csum, eig;
+    DBuf<uint4> recA;
+    DBuf<float4> recB;
+    PinBuf<long long> p_offs;
+    PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
+    int opt_describe2 = 1;  // tuning knob "describe2": 1 load-balanced SHOT, 0 wave/WG per keypoint
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag
     DBuf<unsigned int> ma;
@@ -144,6 +156,8 @@ struct bshot_ctx {
     PinBuf<long long> p_i64;
 
     // instrumentation
+    std::mutex evmu;  // guards pending / evpool / stage_seq (the lookahead task records from its thread)
+    int stage_seq = 0;
     std::vector<StageEv> pending;
     std::vector<hipEvent_t> evpool;
     double stage_ms[BSHOT_NSTAGES] = {0};
@@ -152,8 +166,9 @@ struct bshot_ctx {
 
     int fail(const char* what, hipError_t e);
     int fail(const std::string& what, int code);
-    void stage_begin(int st, hipStream_t s = nullptr);
-    void stage_end(hipStream_t s = nullptr);
+    // stage timing: begin returns a token for the matching end (thread-safe; -1 when timing is off)
+    int stage_begin(int st, hipStream_t s = nullptr);
+    void stage_end(int token, hipStream_t s = nullptr);
     void resolve_events(bool wait = false);
     hipEvent_t get_ev();
 };
@@ -165,11 +180,18 @@ int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n);  // adopts a mat
 int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n);   // grids + SR + ISS on the side stream
 int ctx_sr_launch(bshot_ctx* c);   // SR of the current cloud (main stream) unless already launched
 int ctx_iss_launch(bshot_ctx* c);  // ISS of the current cloud (side stream) unless already launched
-int ctx_describe_dev(bshot_ctx* c, int k);              // keypoints in c->kps; bits in c->bits
+// keypoints in c->kps; bits in c->bits. force_v1: the one-workgroup-per-keypoint SHOT path
+// (fallback when a describe2 sort piece overflows, errw bit 8)
+int ctx_describe_dev(bshot_ctx* c, int k, bool force_v1 = false);              // keypoints in c->kps; bits in c->bits
 int ctx_match_dev(bshot_ctx* c, int na, int nb);        // descriptors in c->ma / c->mb
 // H2D indices, gather xyz of pts4[idx] into dst (device, k x 3); async
 int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst);
 int ctx_sync_main(bshot_ctx* c);
+// explicit-cloud / explicit-stream variants (the lookahead task runs them on the side stream)
+int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1 = false);
+int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst);
+int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst,
+                       float* out);
 // device gather of cloud points -> host (pinned staging), synchronous
 int ctx_gather_host(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst, float* out);
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters);

@@ -33,15 +33,23 @@ hipEvent_t bshot_ctx::get_ev() {
     (void)hipEventCreate(&e);
     return e;
 }
-void bshot_ctx::stage_begin(int st, hipStream_t s) {
-    if (!timing) return;
-    StageEv e{st, get_ev(), get_ev()};
+int bshot_ctx::stage_begin(int st, hipStream_t s) {
+    if (!timing) return -1;
+    std::lock_guard<std::mutex> lk(evmu);
+    StageEv e{st, get_ev(), get_ev(), ++stage_seq, false};
     (void)hipEventRecord(e.a, s ? s : stream);
     pending.push_back(e);
+    return e.id;
 }
-void bshot_ctx::stage_end(hipStream_t s) {
-    if (!timing || pending.empty()) return;
-    (void)hipEventRecord(pending.back().b, s ? s : stream);
+void bshot_ctx::stage_end(int token, hipStream_t s) {
+    if (!timing || token < 0) return;
+    std::lock_guard<std::mutex> lk(evmu);
+    for (auto it = pending.rbegin(); it != pending.rend(); ++it)
+        if (it->id == token) {
+            (void)hipEventRecord(it->b, s ? s : stream);
+            it->ended = true;
+            return;
+        }
 }
 
 void CloudState::release() {
@@ -59,9 +67,10 @@ void CloudState::release() {
 // Without wait, pairs still in flight (e.g. the side stream's lookahead) stay pending, so
 // instrumentation never serialises the two streams.
 void bshot_ctx::resolve_events(bool wait) {
+    std::lock_guard<std::mutex> lk(evmu);
     std::vector<StageEv> keep;
     for (auto& s : pending) {
-        if (!wait && hipEventQuery(s.b) != hipSuccess) {
+        if (!s.ended || (!wait && hipEventQuery(s.b) != hipSuccess)) {
             keep.push_back(s);
             continue;
         }
@@ -120,14 +129,14 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
     HIPCHK(s.pts4.ensure(n > 0 ? n : 1), "alloc pts4");
     HIPCHK(s.errw.ensure(2), "alloc err");
     if (n > 0) {
-        c->stage_begin(BSHOT_STAGE_GRID, st);
+        const int sg1 = c->stage_begin(BSHOT_STAGE_GRID, st);
         HIPCHK(grid_build(s.grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, s.pts4.p, st), "grid build (r/8)");
         HIPCHK(grid_build(s.grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, s.pts4.p, st), "grid build (r/2)");
         if (c->opt_ladder4) {
             HIPCHK(grid_build(s.grid_l16, d_xyz, n, c->prm.seg_radius * 0.0625f, s.pts4.p, st), "grid build (r/16)");
             HIPCHK(grid_build(s.grid_l4, d_xyz, n, c->prm.seg_radius * 0.25f, s.pts4.p, st), "grid build (r/4)");
         }
-        c->stage_end(st);
+        c->stage_end(sg1, st);
     }
     s.fix_ladder(c->opt_ladder4 != 0);
     HIPCHK(hipEventRecord(s.ev_loaded, st), "record loaded");
@@ -144,11 +153,11 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
     HIPCHK(hipMemsetAsync(s.errw.p, 0, sizeof(int), st), "memset err");
     if (n > 0) {
-        c->stage_begin(BSHOT_STAGE_SR, st);
+        const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
                                 c->opt_sr_hint, s.ratio.p, s.errw.p, st),
                "seg_ratio launch");
-        c->stage_end(st);
+        c->stage_end(sg2, st);
         HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
     }
     HIPCHK(hipMemcpyAsync(s.h_err.p, s.errw.p, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
@@ -167,12 +176,12 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
     HIPCHK(hipMemsetAsync(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
-        c->stage_begin(BSHOT_STAGE_ISS, st);
+        const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
         HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient, s.pts4.p, st), "grid build (ISS)");
         HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.errw.p + 1, st),
                "iss launch");
-        c->stage_end(st);
+        c->stage_end(sg3, st);
         HIPCHK(hipMemcpyAsync(s.h_flag.p, s.issflag.p, n, hipMemcpyDeviceToHost, st), "D2H iss");
     }
     HIPCHK(hipMemcpyAsync(s.h_err.p + 1, s.errw.p + 1, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
@@ -199,10 +208,17 @@ int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n) {
 int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
     if (n <= 0) return BSHOT_OK;
     // the prefetch slot holds an older cloud; let work already queued on the main stream finish first
-    hipEvent_t e = c->get_ev();
+    hipEvent_t e;
+    {
+        std::lock_guard<std::mutex> lk(c->evmu);
+        e = c->get_ev();
+    }
     HIPCHK(hipEventRecord(e, c->stream), "record");
     HIPCHK(hipStreamWaitEvent(c->side, e, 0), "wait main");
-    c->evpool.push_back(e);
+    {
+        std::lock_guard<std::mutex> lk(c->evmu);
+        c->evpool.push_back(e);
+    }
     int rc = cloud_load(c, c->pf, d_xyz, n, c->side);
     if (rc) return rc;
     rc = cloud_sr(c, c->pf, c->side);
@@ -229,87 +245,159 @@ int ctx_iss_launch(bshot_ctx* c) {
 }
 
 // keypoints already in c->kps (device, k x 3)
-int ctx_describe_dev(bshot_ctx* c, int k) {
+int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1) {
     if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > 512)
         return c->fail("normal_max_nn must be in [1, 512]", BSHOT_EINVAL);
-    const int n = c->cs.n;
+    const int n = S.n;
     // persistent normals array: resize(n) keeps [0, min) and value-initialises new slots
     HIPCHK(c->normals.ensure(std::max(n, std::max(k, 1))), "alloc normals");
     if (n > c->normals_size)
-        HIPCHK(hipMemsetAsync(c->normals.p + c->normals_size, 0, sizeof(float4) * (n - c->normals_size), c->stream),
+        HIPCHK(hipMemsetAsync(c->normals.p + c->normals_size, 0, sizeof(float4) * (n - c->normals_size), st),
                "zero normals");
     c->normals_size = n;
     if (k <= 0) return BSHOT_OK;
     HIPCHK(c->errw.ensure(1), "alloc err");
-    HIPCHK(hipMemsetAsync(c->errw.p, 0, sizeof(int), c->stream), "memset err");
+    HIPCHK(hipMemsetAsync(c->errw.p, 0, sizeof(int), st), "memset err");
     HIPCHK(c->counts.ensure(k), "alloc counts");
     HIPCHK(c->offs.ensure(k + 1), "alloc offs");
     HIPCHK(c->rf.ensure(9 * (size_t)k), "alloc rf");
     HIPCHK(c->ok.ensure(k), "alloc ok");
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
-    c->stage_begin(BSHOT_STAGE_NORMALS);
-    HIPCHK(launch_normals(c->cs.ladder, c->cs.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
-                          c->normals.p, c->errw.p, c->stream),
+    const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
+    HIPCHK(launch_normals(S.ladder, S.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
+                          c->normals.p, c->errw.p, st),
            "normals launch");
-    c->stage_end();
+    c->stage_end(sg4, st);
     const float R = c->prm.shot_radius;
-    c->stage_begin(BSHOT_STAGE_SHOT_GATHER);
-    HIPCHK(launch_shot_count(c->cs.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, c->stream), "shot count");
-    c->stage_end();
-    HIPCHK(c->p_i64.ensure(1), "alloc pinned");
-    HIPCHK(hipMemcpyAsync(c->p_i64.p, c->offs.p + k, sizeof(long long), hipMemcpyDeviceToHost, c->stream), "D2H total");
-    HIPCHK(hipStreamSynchronize(c->stream), "sync total");
-    const long long total = c->p_i64.p[0];
+    const int sg5 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
+    HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st), "shot count");
+    c->stage_end(sg5, st);
+    HIPCHK(c->p_offs.ensure((size_t)k + 1), "alloc pinned offs");
+    HIPCHK(hipMemcpyAsync(c->p_offs.p, c->offs.p, sizeof(long long) * ((size_t)k + 1), hipMemcpyDeviceToHost,
+                          st),
+           "D2H offs");
+    HIPCHK(hipStreamSynchronize(st), "sync offs");
+    const long long total = c->p_offs.p[k];
     c->work[0] = total;
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
-    c->stage_begin(BSHOT_STAGE_SHOT_GATHER);
-    HIPCHK(launch_shot_gather(c->cs.grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, c->stream), "shot gather");
-    c->stage_end();
-    c->stage_begin(BSHOT_STAGE_SHOT_SORT);
-    HIPCHK(launch_shot_sort(c->offs.p, k, R, c->seg.p, c->segtmp.p, c->stream), "shot sort");
-    c->stage_end();
-    c->stage_begin(BSHOT_STAGE_LRF);
-    HIPCHK(launch_lrf(c->cs.pts4.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, c->stream), "lrf");
-    c->stage_end();
-    c->stage_begin(BSHOT_STAGE_HIST);
-    HIPCHK(launch_shot_hist(c->cs.pts4.p, c->normals.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, c->shot.p,
-                            c->bits.p, c->stream),
-           "shot hist");
-    c->stage_end();
+    const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
+    HIPCHK(launch_shot_gather(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, st), "shot gather");
+    c->stage_end(sg6, st);
+    if (!c->opt_describe2 || force_v1) {
+        const int sg7 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
+        HIPCHK(launch_shot_sort(c->offs.p, k, R, c->seg.p, c->segtmp.p, st), "shot sort");
+        c->stage_end(sg7, st);
+        const int sg8 = c->stage_begin(BSHOT_STAGE_LRF, st);
+        HIPCHK(launch_lrf(S.pts4.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, st), "lrf");
+        c->stage_end(sg8, st);
+        const int sg9 = c->stage_begin(BSHOT_STAGE_HIST, st);
+        HIPCHK(launch_shot_hist(S.pts4.p, c->normals.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p,
+                                c->shot.p, c->bits.p, st),
+               "shot hist");
+        c->stage_end(sg9, st);
+        return BSHOT_OK;
+    }
+    // plan: sort pieces of <= ~3072 keys per keypoint; 64-rank chunks
+    const int piece = 3072;
+    int n_plan = 0;
+    long long nch = 0;
+    for (int q = 0; q < k; ++q) {
+        const long long nq = c->p_offs.p[q + 1] - c->p_offs.p[q];
+        if (nq > 0) n_plan += (int)((nq + piece - 1) / piece);
+        nch += (nq + 63) / 64;
+    }
+    if (nch > 0x7FFFFFFF) return c->fail("describe: too many neighbourhood chunks", BSHOT_ECAP);
+    HIPCHK(c->p_plan.ensure(4 * (size_t)n_plan + 2 * (size_t)k + 1), "alloc pinned plan");
+    int* hp = c->p_plan.p;
+    int* hcb = hp + 4 * (size_t)n_plan;
+    int* hperm = hcb + k + 1;
+    for (int q = 0; q < k; ++q) hperm[q] = q;
+    std::stable_sort(hperm, hperm + k, [&](int x, int y) {
+        return c->p_offs.p[x + 1] - c->p_offs.p[x] > c->p_offs.p[y + 1] - c->p_offs.p[y];
+    });
+    int w = 0, cbr = 0;
+    for (int q = 0; q < k; ++q) {
+        const long long nq = c->p_offs.p[q + 1] - c->p_offs.p[q];
+        hcb[q] = cbr;
+        cbr += (int)((nq + 63) / 64);
+        if (nq <= 0) continue;
+        const int J = (int)((nq + piece - 1) / piece);
+        for (int j = 0; j < J; ++j, ++w) { hp[4 * w] = q; hp[4 * w + 1] = j; hp[4 * w + 2] = J; hp[4 * w + 3] = 0; }
+    }
+    hcb[k] = cbr;
+    HIPCHK(c->plan.ensure(n_plan > 0 ? n_plan : 1), "alloc plan");
+    HIPCHK(c->cb.ensure((size_t)k + 1), "alloc cb");
+    HIPCHK(c->owner.ensure(cbr > 0 ? (size_t)cbr : 1), "alloc owner");
+    HIPCHK(c->csum.ensure(8 * (size_t)(cbr > 0 ? cbr : 1)), "alloc csum");
+    HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
+    HIPCHK(c->okf.ensure(k), "alloc okf");
+    HIPCHK(c->signs.ensure(2 * (size_t)k), "alloc signs");
+    HIPCHK(c->recA.ensure(total > 0 ? (size_t)total : 1), "alloc records");
+    HIPCHK(c->recB.ensure(total > 0 ? (size_t)total : 1), "alloc records");
+    if (n_plan > 0)
+        HIPCHK(hipMemcpyAsync(c->plan.p, hp, sizeof(int4) * n_plan, hipMemcpyHostToDevice, st), "H2D plan");
+    HIPCHK(c->perm.ensure(k), "alloc perm");
+    HIPCHK(hipMemcpyAsync(c->cb.p, hcb, sizeof(int) * ((size_t)k + 1), hipMemcpyHostToDevice, st), "H2D cb");
+    HIPCHK(hipMemcpyAsync(c->perm.p, hperm, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D perm");
+    Describe2Args A;
+    A.k = k; A.n_plan = n_plan; A.n_chunks = cbr; A.R = R;
+    A.plan = c->plan.p; A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p; A.pts4 = S.pts4.p; A.normals = c->normals.p;
+    A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
+    A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recA = c->recA.p; A.recB = c->recB.p;
+    A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
+    const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
+    HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
+    c->stage_end(sg10, st);
+    const int sg11 = c->stage_begin(BSHOT_STAGE_LRF, st);
+    HIPCHK(launch_describe2(A, 1, st), "describe2 lrf");
+    c->stage_end(sg11, st);
+    const int sg12 = c->stage_begin(BSHOT_STAGE_HIST, st);
+    HIPCHK(launch_describe2(A, 2, st), "describe2 hist");
+    c->stage_end(sg12, st);
     return BSHOT_OK;
 }
 
-// descriptors in c->ma (a rows then b rows); results in c->left (left | right | flag)
+int ctx_describe_dev(bshot_ctx* c, int k, bool force_v1) { return ctx_describe_on(c, c->cs, c->stream, k, force_v1); }
+
 int ctx_match_dev(bshot_ctx* c, int na, int nb) {
     HIPCHK(c->lbest.ensure((size_t)na + nb + 1), "alloc best");
     HIPCHK(c->left.ensure(2 * (size_t)na + nb + 1), "alloc match out");
-    c->stage_begin(BSHOT_STAGE_MATCH);
+    const int sg13 = c->stage_begin(BSHOT_STAGE_MATCH);
     HIPCHK(launch_match(c->ma.p, na, c->ma.p + 11 * (size_t)na, nb, c->lbest.p, c->left.p, c->stream), "match launch");
-    c->stage_end();
+    c->stage_end(sg13);
     return BSHOT_OK;
 }
 
-int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst) {
+int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst) {
     HIPCHK(c->gidx.ensure(k > 0 ? k : 1), "alloc gidx");
     HIPCHK(dst.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc gather out");
     if (k <= 0) return BSHOT_OK;
     HIPCHK(c->p_gidx.ensure(k), "alloc pinned idx");
     std::memcpy(c->p_gidx.p, h_idx, sizeof(int) * k);
-    HIPCHK(hipMemcpyAsync(c->gidx.p, c->p_gidx.p, sizeof(int) * k, hipMemcpyHostToDevice, c->stream), "H2D idx");
-    HIPCHK(launch_gather(c->cs.pts4.p, c->gidx.p, k, dst.p, c->stream), "gather");
+    HIPCHK(hipMemcpyAsync(c->gidx.p, c->p_gidx.p, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D idx");
+    HIPCHK(launch_gather(S.pts4.p, c->gidx.p, k, dst.p, st), "gather");
+    return BSHOT_OK;
+}
+
+int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst) {
+    return ctx_gather_on(c, c->cs, c->stream, h_idx, k, dst);
+}
+
+int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst,
+                       float* out) {
+    int rc = ctx_gather_on(c, S, st, h_idx, k, dst);
+    if (rc || k <= 0) return rc;
+    HIPCHK(c->p_g3.ensure(3 * (size_t)k), "alloc pinned gather");
+    HIPCHK(hipMemcpyAsync(c->p_g3.p, dst.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, st), "D2H gather");
+    HIPCHK(hipStreamSynchronize(st), "sync gather");
+    std::memcpy(out, c->p_g3.p, sizeof(float) * 3 * k);
     return BSHOT_OK;
 }
 
 int ctx_gather_host(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst, float* out) {
-    int rc = ctx_gather(c, h_idx, k, dst);
-    if (rc || k <= 0) return rc;
-    HIPCHK(c->p_g3.ensure(3 * (size_t)k), "alloc pinned gather");
-    HIPCHK(hipMemcpyAsync(c->p_g3.p, dst.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, c->stream), "D2H gather");
-    HIPCHK(hipStreamSynchronize(c->stream), "sync gather");
-    std::memcpy(out, c->p_g3.p, sizeof(float) * 3 * k);
-    return BSHOT_OK;
+    return ctx_gather_host_on(c, c->cs, c->stream, h_idx, k, dst, out);
 }
 
 int ctx_sync_main(bshot_ctx* c) {
@@ -343,12 +431,12 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         bg::Mat4f Ts = bg::Mat4f::identity();
         while (true) {
             const int b = it & 1;
-            c->stage_begin(BSHOT_STAGE_ICP);
+            const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
             HIPCHK(launch_icp_iter(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1), Ts.m, it > 0,
                                    ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b, c->ibest.p + (size_t)ns * (b ^ 1),
                                    c->stream),
                    "icp iteration");
-            c->stage_end();
+            c->stage_end(sg14);
             HIPCHK(hipMemcpyAsync(c->p_best.p, c->ibest.p + (size_t)ns * b, sizeof(unsigned long long) * ns,
                                   hipMemcpyDeviceToHost, c->stream),
                    "D2H nn");
@@ -527,6 +615,19 @@ int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf
     }
     HIPCHK(hipStreamSynchronize(c->stream), "sync describe");
     c->resolve_events();
+    if (herr & 8) {
+        // a describe2 sort piece overflowed its LDS buffer (pathological duplicate d2): rerun the
+        // SHOT stages one workgroup per keypoint
+        rc = ctx_describe_dev(c, k, true);
+        if (rc) return rc;
+        if (k > 0) {
+            HIPCHK(hipMemcpyAsync(bits, c->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost, c->stream), "D2H bits");
+            if (shot) HIPCHK(hipMemcpyAsync(shot, c->shot.p, sizeof(float) * 352 * k, hipMemcpyDeviceToHost, c->stream), "D2H shot");
+            if (rf) HIPCHK(hipMemcpyAsync(rf, c->rf.p, sizeof(float) * 9 * k, hipMemcpyDeviceToHost, c->stream), "D2H rf");
+            HIPCHK(hipMemcpyAsync(&herr, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H err");
+        }
+        HIPCHK(hipStreamSynchronize(c->stream), "sync describe");
+    }
     if (herr & 2) return c->fail("normals: neighbourhood with > 1024 exactly tied boundary keys", BSHOT_ECAP);
     return BSHOT_OK;
 }
@@ -639,6 +740,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     const std::string k(name);
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
     else if (k == "sr_hint") c->opt_sr_hint = value ? 1 : 0;
+    else if (k == "describe2") c->opt_describe2 = value ? 1 : 0;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

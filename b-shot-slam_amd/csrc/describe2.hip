@@ -1,0 +1,615 @@
+// describe2.hip -- A5/A6/A7 on gfx950, load-balanced: the SHOT stages split every keypoint's
+// neighbourhood (up to ~22k points for keypoints near the sensor, ~3x the mean) into fixed-size
+// pieces so no single keypoint bounds a launch. Same arithmetic, same order as describe.hip.
+//
+//   k_sort2       (keypoint, piece) workgroups: each piece owns the d2 buckets whose prefix start
+//                 falls in its share of the segment; bucket-scatter into LDS, exact rank inside the
+//                 bucket, write the sorted (d2, idx) keys
+//   k_lrf_chunks  wave per 64-rank chunk: 7 weighted-covariance terms by the xor-butterfly tree
+//   k_lrf_eig     thread per keypoint: chunk sums in chunk order, Jacobi eigenvectors
+//   k_lrf_sign    wave per chunk: sign counts for the x/z disambiguation (integer, order-free)
+//   k_lrf_fin     thread per keypoint: PCL's count + median-5 rule, float LRF rows
+//   k_hist_contrib wave per chunk: the <= 5 (bin, value) interpolation records of every neighbour
+//   k_hist_apply  wave per keypoint: records applied in rank order to the LDS histogram (in-order
+//                 ds_add_f32), L2 normalisation, B-SHOT bits
+// Chunk c of keypoint q covers ranks [64 (c - cb[q]), ...) where cb is the exclusive scan of
+// ceil(n_q / 64) (host-computed after the count pass).
+#include <hip/hip_runtime.h>
+
+#include "bshot_math.h"
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace bsk {
+
+#define S2_BUCKETS 1024
+#define S2_CAP 6144
+
+__device__ __forceinline__ int s2_bucket(unsigned long long key, float sc) {
+    const float d2 = __uint_as_float((unsigned)(key >> 32));
+    int bk = (int)(d2 * sc);
+    return bk < 0 ? 0 : (bk > S2_BUCKETS - 1 ? S2_BUCKETS - 1 : bk);
+}
+
+// plan[w] = {q, piece j, pieces J, 0}
+__global__ void __launch_bounds__(256) k_sort2(const int4* __restrict__ plan, const long long* __restrict__ offs,
+                                               float R, const unsigned long long* __restrict__ seg,
+                                               unsigned long long* __restrict__ out, int* __restrict__ err) {
+    __shared__ unsigned int hist[S2_BUCKETS];
+    __shared__ unsigned int pre[S2_BUCKETS];
+    __shared__ unsigned int cur[S2_BUCKETS];
+    __shared__ unsigned int wsum[4];
+    __shared__ int blo, bhi;
+    __shared__ unsigned long long buf[S2_CAP];
+    const int t = threadIdx.x;
+    const int4 pl = plan[blockIdx.x];
+    const int q = pl.x, j = pl.y, J = pl.z;
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    if (n <= 0) return;
+    const unsigned long long* a = seg + o;
+    unsigned long long* dst = out + o;
+    const float R2 = (float)((double)R * (double)R);
+    const float sc = (float)S2_BUCKETS / R2;
+    for (int i = t; i < S2_BUCKETS; i += 256) hist[i] = 0;
+    if (t == 0) { blo = S2_BUCKETS; bhi = -1; }
+    __syncthreads();
+    // 8 loads in flight per thread (the segment lives in L2/HBM)
+    for (int i0 = t; i0 < n; i0 += 256 * 8) {
+        unsigned long long kk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kk[u] = i0 + 256 * u < n ? a[i0 + 256 * u] : ~0ull;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (kk[u] != ~0ull) atomicAdd(&hist[s2_bucket(kk[u], sc)], 1u);
+    }
+    __syncthreads();
+    // exclusive scan: 4 buckets per thread
+    const unsigned int s4 = hist[4 * t] + hist[4 * t + 1] + hist[4 * t + 2] + hist[4 * t + 3];
+    int tot;
+    const int ex = wave_excl_scan((int)s4, tot);
+    if (lane_id() == 63) wsum[t >> 6] = (unsigned)tot;
+    __syncthreads();
+    unsigned int run = (unsigned)ex;
+    for (int w = 0; w < (t >> 6); ++w) run += wsum[w];
+    const unsigned int lo_cnt = (unsigned)(((long long)j * n) / J), hi_cnt = (unsigned)(((long long)(j + 1) * n) / J);
+    for (int u = 0; u < 4; ++u) {
+        const int b = 4 * t + u;
+        pre[b] = run;
+        if (hist[b] > 0 && run >= lo_cnt && run < hi_cnt) {
+            atomicMin(&blo, b);
+            atomicMax(&bhi, b);
+        }
+        run += hist[b];
+    }
+    __syncthreads();
+    if (bhi < 0) return;  // no bucket starts in this piece (uniform)
+    const unsigned int base = pre[blo], end = pre[bhi] + hist[bhi];
+    if (end - base > S2_CAP) {
+        if (t == 0) atomicOr(err, 8);
+        return;
+    }
+    for (int b = blo + t; b <= bhi; b += 256) cur[b] = pre[b] - base;
+    __syncthreads();
+    for (int i0 = t; i0 < n; i0 += 256 * 8) {
+        unsigned long long kk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kk[u] = i0 + 256 * u < n ? a[i0 + 256 * u] : ~0ull;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (kk[u] == ~0ull) continue;
+            const int b = s2_bucket(kk[u], sc);
+            if (b >= blo && b <= bhi) buf[atomicAdd(&cur[b], 1u)] = kk[u];
+        }
+    }
+    __syncthreads();
+    const int m = (int)(end - base);
+    for (int i = t; i < m; i += 256) {
+        const unsigned long long key = buf[i];
+        const int b = s2_bucket(key, sc);
+        const unsigned int s0 = pre[b] - base, c = hist[b];
+        unsigned int rank = 0;
+        for (unsigned int u = 0; u < c; ++u) rank += buf[s0 + u] < key ? 1u : 0u;
+        dst[base + s0 + rank] = key;
+    }
+}
+
+// owner[c] = keypoint of chunk c (block per keypoint)
+__global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restrict__ cb, int* __restrict__ owner) {
+    const int q = blockIdx.x;
+    if (q >= k) return;
+    for (int c = cb[q] + threadIdx.x; c < cb[q + 1]; c += 256) owner[c] = q;
+}
+
+// csum[8 c + 0..5]: weighted covariance terms, [6]: weight sum, [7]: valid count
+__global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ pts4, const float* __restrict__ kps,
+                                                    int k, float R, const long long* __restrict__ offs,
+                                                    const int* __restrict__ cb, const int* __restrict__ owner,
+                                                    const unsigned long long* __restrict__ seg,
+                                                    double* __restrict__ csum) {
+    const int lane = lane_id();
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= cb[k]) return;
+    const int q = owner[c];
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    const int i = (c - cb[q]) * 64 + lane;
+    double v[7] = {0, 0, 0, 0, 0, 0, 0};
+    int isv = 0;
+    if (i < n) {
+        const unsigned long long key = seg[o + i];
+        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+        if (!(p.x == kx && p.y == ky && p.z == kz)) {
+            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+            const double w = (double)R - sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+            v[0] = w * (vx * vx); v[1] = w * (vx * vy); v[2] = w * (vx * vz);
+            v[3] = w * (vy * vy); v[4] = w * (vy * vz); v[5] = w * (vz * vz);
+            v[6] = w;
+            isv = 1;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j) v[j] = wave_tree_sum_d(v[j]);
+    const int nv = __popcll(__ballot(isv != 0));
+    if (lane < 8) {
+        double x = (double)nv;
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+            if (lane == j) x = v[j];
+        csum[8 * (size_t)c + lane] = x;
+    }
+}
+
+// eig[8 q + 0..2] = x axis (largest), [3..5] = z axis (smallest), [6] = valid count; okf[q]
+__global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ cb, const double* __restrict__ csum,
+                                                double* __restrict__ eig, int* __restrict__ okf) {
+    const int q = blockIdx.x * 64 + threadIdx.x;
+    if (q >= k) return;
+    double tot[7] = {0, 0, 0, 0, 0, 0, 0};
+    long long valid = 0;
+    const int c0 = cb[q], c1 = cb[q + 1];
+    for (int cc = c0; cc < c1; cc += 4) {
+        double4 blk[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (cc + u < c1) {
+                const double4* s4 = reinterpret_cast<const double4*>(csum + 8 * (size_t)(cc + u));
+                blk[u][0] = s4[0];
+                blk[u][1] = s4[1];
+            }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (cc + u < c1) {
+                tot[0] = tot[0] + blk[u][0].x; tot[1] = tot[1] + blk[u][0].y; tot[2] = tot[2] + blk[u][0].z;
+                tot[3] = tot[3] + blk[u][0].w; tot[4] = tot[4] + blk[u][1].x; tot[5] = tot[5] + blk[u][1].y;
+                tot[6] = tot[6] + blk[u][1].z;
+                valid += (long long)blk[u][1].w;
+            }
+    }
+    int ok = 0;
+    if (valid >= 5) {
+        const double sum = tot[6];
+        double cov[9];
+        cov[0] = tot[0] / sum; cov[1] = tot[1] / sum; cov[2] = tot[2] / sum;
+        cov[4] = tot[3] / sum; cov[5] = tot[4] / sum; cov[8] = tot[5] / sum;
+        cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+        double w[3], ev[9];
+        bm::jacobi3(cov, w, ev);
+        if (bm::isfin(w[0]) && bm::isfin(w[1]) && bm::isfin(w[2])) {
+            ok = 1;
+            double* e = eig + 8 * (size_t)q;
+            e[0] = ev[2]; e[1] = ev[5]; e[2] = ev[8];
+            e[3] = ev[0]; e[4] = ev[3]; e[5] = ev[6];
+        }
+    }
+    eig[8 * (size_t)q + 6] = (double)valid;
+    okf[q] = ok;
+}
+
+// signs[2 q] += #(v . x >= 0), signs[2 q + 1] += #(v . z >= 0) over valid neighbours
+__global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
+                                                  const long long* __restrict__ offs, const int* __restrict__ cb,
+                                                  const int* __restrict__ owner,
+                                                  const unsigned long long* __restrict__ seg,
+                                                  const double* __restrict__ eig, const int* __restrict__ okf,
+                                                  int* __restrict__ signs) {
+    const int lane = lane_id();
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= cb[k]) return;
+    const int q = owner[c];
+    if (!okf[q]) return;
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    const int i = (c - cb[q]) * 64 + lane;
+    const double* e = eig + 8 * (size_t)q;
+    int pt = 0, pn = 0;
+    if (i < n) {
+        const unsigned long long key = seg[o + i];
+        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+        if (!(p.x == kx && p.y == ky && p.z == kz)) {
+            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+            if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
+            if (((vx * e[3] + vy * e[4]) + vz * e[5]) >= 0) pn = 1;
+        }
+    }
+    pt = __popcll(__ballot(pt != 0));
+    pn = __popcll(__ballot(pn != 0));
+    if (lane == 0) {
+        if (pt) atomicAdd(&signs[2 * q], pt);
+        if (pn) atomicAdd(&signs[2 * q + 1], pn);
+    }
+}
+
+__global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
+                                                const long long* __restrict__ offs,
+                                                const unsigned long long* __restrict__ seg,
+                                                const double* __restrict__ eig, const int* __restrict__ okf,
+                                                const int* __restrict__ signs, float* __restrict__ rf_out,
+                                                int* __restrict__ ok_out) {
+    const int q = blockIdx.x * 64 + threadIdx.x;
+    if (q >= k) return;
+    float* r9 = rf_out + 9 * (size_t)q;
+    if (!okf[q]) {
+        for (int j = 0; j < 9; ++j) r9[j] = __builtin_nanf("");
+        ok_out[q] = 0;
+        return;
+    }
+    const double* e = eig + 8 * (size_t)q;
+    const int valid_total = (int)e[6];
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    double x[3] = {e[0], e[1], e[2]}, z[3] = {e[3], e[4], e[5]};
+    int PT = 2 * signs[2 * q] - valid_total;
+    int PN = 2 * signs[2 * q + 1] - valid_total;
+    if (PT == 0 || PN == 0) {
+        // median-5 rule over valid neighbours by rank. Excluded neighbours (exact duplicates of the
+        // keypoint) have d2 == 0, so they sit in the leading d2 == 0 run: scan that run, then the
+        // valid rank r lives at index r + (excluded count).
+        const long long o = offs[q];
+        const int n = (int)(offs[q + 1] - o);
+        const int med = valid_total / 2;
+        int addT = 0, addN = 0;
+        int z0n = 0, excl = 0;
+        while (z0n < n && (unsigned)(seg[o + z0n] >> 32) == 0u) {
+            const float4 p = pts4[(unsigned)(seg[o + z0n] & 0xFFFFFFFFu)];
+            if (p.x == kx && p.y == ky && p.z == kz) ++excl;
+            ++z0n;
+        }
+        for (int r = med - 2; r <= med + 2; ++r) {
+            if (r < 0) continue;
+            int i;
+            if (r < z0n - excl) {
+                // rank inside the zero run: walk it (at most a few keys)
+                int rr = 0;
+                i = -1;
+                for (int u = 0; u < z0n; ++u) {
+                    const float4 p = pts4[(unsigned)(seg[o + u] & 0xFFFFFFFFu)];
+                    if (p.x == kx && p.y == ky && p.z == kz) continue;
+                    if (rr == r) { i = u; break; }
+                    ++rr;
+                }
+            } else {
+                i = r + excl;
+            }
+            if (i < 0 || i >= n) continue;
+            const float4 p = pts4[(unsigned)(seg[o + i] & 0xFFFFFFFFu)];
+            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+            if (((vx * x[0] + vy * x[1]) + vz * x[2]) > 0) addT++;
+            if (((vx * z[0] + vy * z[1]) + vz * z[2]) > 0) addN++;
+        }
+        if (PT == 0 && addT < 3) { x[0] = -x[0]; x[1] = -x[1]; x[2] = -x[2]; }
+        if (PN == 0 && addN < 3) { z[0] = -z[0]; z[1] = -z[1]; z[2] = -z[2]; }
+    }
+    if (PT < 0) { x[0] = -x[0]; x[1] = -x[1]; x[2] = -x[2]; }
+    if (PN < 0) { z[0] = -z[0]; z[1] = -z[1]; z[2] = -z[2]; }
+    const float x0 = (float)x[0], x1 = (float)x[1], x2 = (float)x[2];
+    const float z0 = (float)z[0], z1 = (float)z[1], z2 = (float)z[2];
+    r9[0] = x0; r9[1] = x1; r9[2] = x2;
+    r9[3] = z1 * x2 - z2 * x1; r9[4] = z2 * x0 - z0 * x2; r9[5] = z0 * x1 - z1 * x0;
+    r9[6] = z0; r9[7] = z1; r9[8] = z2;
+    ok_out[q] = 1;
+}
+
+__device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0, float b1, float b2) {
+    return (a0 * b0 + a2 * b2) + (a1 * b1 + 0.0f);
+}
+
+#define PST2_RAD_45 0.78539816339744830961566084581988
+#define PST2_RAD_90 1.5707963267948966192313216916398
+#define PST2_RAD_135 2.3561944901923449288469825374596
+#define PST2_RAD_PI_7_8 2.7488935718910690836548129603691
+
+// record of neighbour r: A = {b0 | b1 << 16, b2 | b3 << 16, b4 | sector mask << 16, bits(v4)},
+// B = {v0, v1, v2, v3};
+// unused slots -> bin 360 (padding) with value +0
+__global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__ pts4,
+                                                      const float4* __restrict__ normals,
+                                                      const float* __restrict__ kps, int k, float R,
+                                                      const long long* __restrict__ offs, const int* __restrict__ cb,
+                                                      const int* __restrict__ owner,
+                                                      const unsigned long long* __restrict__ seg,
+                                                      const float* __restrict__ rf_in, const int* __restrict__ ok_in,
+                                                      uint4* __restrict__ recA, float4* __restrict__ recB) {
+    const int lane = lane_id();
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= cb[k]) return;
+    const int q = owner[c];
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
+    if (!(fin && ok_in[q] && n >= 5)) return;
+    const int i = (c - cb[q]) * 64 + lane;
+    if (i >= n) return;
+    const double Rd = (double)R;
+    const double r12 = Rd / 2, r34 = (Rd * 3) / 4, r14 = Rd / 4;
+    const int nr_bins = 10;
+    float rf[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) rf[j] = rf_in[9 * (size_t)q + j];
+    int bins[5] = {-1, -1, -1, -1, -1};
+    float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    const unsigned long long key = seg[o + i];
+    const unsigned int idx = (unsigned int)(key & 0xFFFFFFFFu);
+    const float4 nv = normals[idx];
+    if (__builtin_isfinite(nv.x) && __builtin_isfinite(nv.y) && __builtin_isfinite(nv.z)) {
+        double cosd = (double)dot4f_2(nv.x, nv.y, nv.z, rf[6], rf[7], rf[8]);
+        if (cosd > 1.0) cosd = 1.0;
+        if (cosd < -1.0) cosd = -1.0;
+        double bd = ((1.0 + cosd) * nr_bins) / 2;
+        const float4 p = pts4[idx];
+        const float dx = p.x - kx, dy = p.y - ky, dz = p.z - kz;
+        const double distance = sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+        if (!(fabs(distance - 0.0) < 1e-15)) {
+            double xr = (double)dot4f_2(dx, dy, dz, rf[0], rf[1], rf[2]);
+            double yr = (double)dot4f_2(dx, dy, dz, rf[3], rf[4], rf[5]);
+            double zr = (double)dot4f_2(dx, dy, dz, rf[6], rf[7], rf[8]);
+            if (fabs(yr) < 1E-30) yr = 0;
+            if (fabs(xr) < 1E-30) xr = 0;
+            if (fabs(zr) < 1E-30) zr = 0;
+            const unsigned bit4 = ((yr > 0) || ((yr == 0.0) && (xr < 0))) ? 1u : 0u;
+            const unsigned bit3 = ((xr > 0) || ((xr == 0.0) && (yr > 0))) ? (bit4 ? 0u : 1u) : bit4;
+            int desc = (int)((bit4 << 3) + (bit3 << 2));
+            desc = desc << 1;
+            if ((xr * yr > 0) || (xr == 0.0)) desc += (fabs(xr) >= fabs(yr)) ? 0 : 4;
+            else desc += (fabs(xr) > fabs(yr)) ? 4 : 0;
+            desc += zr > 0 ? 1 : 0;
+            desc += (distance > r12) ? 2 : 0;
+            const int step = (int)floor(bd + 0.5);
+            const int vol = desc * (nr_bins + 1);
+            bd -= step;
+            double w = (1 - fabs(bd));
+            if (bd > 0) { bins[0] = vol + ((step + 1) % nr_bins); vals[0] = (float)bd; }
+            else { bins[0] = vol + ((step - 1 + nr_bins) % nr_bins); vals[0] = -(float)bd; }
+            if (distance > r12) {
+                const double rd = (distance - r34) / r12;
+                if (distance > r34) w += 1 - rd;
+                else { w += 1 + rd; bins[1] = (desc - 2) * (nr_bins + 1) + step; vals[1] = (float)(-rd); }
+            } else {
+                const double rd = (distance - r14) / r12;
+                if (distance < r14) w += 1 + rd;
+                else { w += 1 - rd; bins[1] = (desc + 2) * (nr_bins + 1) + step; vals[1] = (float)rd; }
+            }
+            double ic = zr / distance;
+            if (ic < -1.0) ic = -1.0;
+            if (ic > 1.0) ic = 1.0;
+            const double incl = bm::acos_(ic);
+            if (incl > PST2_RAD_90 || (fabs(incl - PST2_RAD_90) < 1e-30 && zr <= 0)) {
+                const double id = (incl - PST2_RAD_135) / PST2_RAD_90;
+                if (incl > PST2_RAD_135) w += 1 - id;
+                else { w += 1 + id; bins[2] = (desc + 1) * (nr_bins + 1) + step; vals[2] = -(float)id; }
+            } else {
+                const double id = (incl - PST2_RAD_45) / PST2_RAD_90;
+                if (incl < PST2_RAD_45) w += 1 + id;
+                else { w += 1 - id; bins[2] = (desc - 1) * (nr_bins + 1) + step; vals[2] = (float)id; }
+            }
+            if (yr != 0.0 || xr != 0.0) {
+                const double az = bm::atan2_(yr, xr);
+                const int sel = desc >> 2;
+                double ad = (az - (-PST2_RAD_PI_7_8 + PST2_RAD_45 * sel)) / PST2_RAD_45;
+                ad = fmax(-0.5, fmin(ad, 0.5));
+                if (ad > 0) {
+                    w += 1 - ad;
+                    bins[3] = ((desc + 4) % 32) * (nr_bins + 1) + step; vals[3] = (float)ad;
+                } else {
+                    w += 1 + ad;
+                    bins[3] = ((desc - 4 + 32) % 32) * (nr_bins + 1) + step; vals[3] = -(float)ad;
+                }
+            }
+            bins[4] = vol + step;
+            vals[4] = (float)w;
+        }
+    }
+    unsigned int bb[5];
+    float vv[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        bb[j] = bins[j] < 0 ? 360u : (unsigned)bins[j];
+        vv[j] = bins[j] < 0 ? 0.f : vals[j];
+    }
+    unsigned int smask = 0;  // azimuth sectors (bins [44 s, 44 s + 44)) this neighbour touches
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        if (bb[j] < 352u) smask |= 1u << (bb[j] / 44u);
+    recA[o + i] = make_uint4(bb[0] | (bb[1] << 16), bb[2] | (bb[3] << 16), bb[4] | (smask << 16),
+                             __float_as_uint(vv[4]));
+    recB[o + i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+}
+
+// wave per keypoint: records applied in rank order to the LDS histogram (lanes 0..4 own record
+// slots; one in-order ds_add_f32 per neighbour), then normalisation and binarisation. The LDS
+// float-atomic unit of a CU is the limiter (~3 cycles per lane-op), so blocks are launched in
+// descending neighbourhood size (perm, host-sorted) and the LDS reservation caps residency at
+// 4 keypoints per CU: the largest start first and smaller ones fill in as CUs free up.
+#define HA_LDS_PAD 8192
+__global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps, int k, const int* __restrict__ perm,
+                                                   const long long* __restrict__ offs, const int* __restrict__ ok_in,
+                                                   const uint4* __restrict__ recA, const float4* __restrict__ recB,
+                                                   float* __restrict__ shot_out, unsigned int* __restrict__ bits_out) {
+    __shared__ float hist[384];
+    __shared__ int rbin[64 * 5];
+    __shared__ float rval[64 * 5];
+    __shared__ unsigned int gcode[88];
+    __shared__ float pad_[HA_LDS_PAD];  // residency cap (see above)
+    const int lane = lane_id();
+    const int q = perm[blockIdx.x];
+    if (lane == 0 && q < 0) pad_[0] = 0.f;
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
+    const bool good = fin && ok_in[q] && n >= 5;
+    for (int j = lane; j < 384; j += 64) hist[j] = 0.0f;
+    __builtin_amdgcn_wave_barrier();
+    if (good) {
+        // records of 8 chunks are loaded per batch (one wait per 512 neighbours), then applied
+        // chunk by chunk in rank order
+        for (int c0 = 0; c0 < n; c0 += 64 * 8) {
+            uint4 ra[8];
+            float4 rb[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = c0 + 64 * u + lane;
+                ra[u] = make_uint4(360u | (360u << 16), 360u | (360u << 16), 360u, 0u);
+                rb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (i < n) { ra[u] = recA[o + i]; rb[u] = recB[o + i]; }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (c0 + 64 * u >= n) break;
+                rbin[lane * 5 + 0] = (int)(ra[u].x & 0xFFFFu); rval[lane * 5 + 0] = rb[u].x;
+                rbin[lane * 5 + 1] = (int)(ra[u].x >> 16);     rval[lane * 5 + 1] = rb[u].y;
+                rbin[lane * 5 + 2] = (int)(ra[u].y & 0xFFFFu); rval[lane * 5 + 2] = rb[u].z;
+                rbin[lane * 5 + 3] = (int)(ra[u].y >> 16);     rval[lane * 5 + 3] = rb[u].w;
+                rbin[lane * 5 + 4] = (int)(ra[u].z & 0xFFFFu); rval[lane * 5 + 4] = __uint_as_float(ra[u].w);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 5) {
+#pragma unroll
+                    for (int g = 0; g < 64; g += 16) {
+                        int bb[16];
+                        float vv[16];
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            bb[v] = rbin[(g + v) * 5 + lane];
+                            vv[v] = rval[(g + v) * 5 + lane];
+                        }
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) atomicAdd(&hist[bb[v]], vv[v]);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();
+    // normalizeHistogram: double accumulation of float squares in bin order
+    float sv[6];
+    if (good) {
+        double acc = 0.0;
+        if (lane == 0)
+            for (int j = 0; j < 352; j += 8) {
+                float h[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) h[u] = hist[j + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = acc + (double)(h[u] * h[u]);
+            }
+        acc = __shfl(acc, 0, 64);
+        const float fa = (float)sqrt(acc);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int b = lane + 64 * j;
+            sv[j] = b < 352 ? hist[b] / fa : 0.f;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) sv[j] = __builtin_nanf("");
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int b = lane + 64 * j;
+        if (b < 352) {
+            hist[b] = sv[j];
+            if (shot_out) shot_out[352 * (size_t)q + b] = sv[j];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // B-SHOT: 88 groups of 4 (include/bshot_bits.h:144-278)
+    unsigned int code[2] = {0u, 0u};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int gidx = lane + 64 * h;
+        if (gidx < 88) {
+            const float v0 = hist[4 * gidx], v1 = hist[4 * gidx + 1], v2 = hist[4 * gidx + 2], v3 = hist[4 * gidx + 3];
+            const float sum = ((v0 + v1) + v2) + v3;
+            const double th = 0.9 * (double)sum;
+            unsigned b;
+            if (v0 == 0 && v1 == 0 && v2 == 0 && v3 == 0) b = 0;
+            else if ((double)v0 > th) b = 1;
+            else if ((double)v1 > th) b = 2;
+            else if ((double)v2 > th) b = 4;
+            else if ((double)v3 > th) b = 8;
+            else if ((double)(v0 + v1) > th) b = 3;
+            else if ((double)(v1 + v2) > th) b = 6;
+            else if ((double)(v2 + v3) > th) b = 12;
+            else if ((double)(v0 + v3) > th) b = 9;
+            else if ((double)(v1 + v3) > th) b = 10;
+            else if ((double)(v0 + v2) > th) b = 5;
+            else if ((double)((v0 + v1) + v2) > th) b = 7;
+            else if ((double)((v1 + v2) + v3) > th) b = 14;
+            else if ((double)((v0 + v2) + v3) > th) b = 13;
+            else if ((double)((v0 + v1) + v3) > th) b = 11;
+            else b = 15;
+            code[h] = b;
+        }
+    }
+    if (lane < 88) gcode[lane] = code[0];
+    if (lane + 64 < 88) gcode[lane + 64] = code[1];
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 11) {
+        unsigned int w = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w |= gcode[8 * lane + j] << (4 * j);
+        bits_out[11 * (size_t)q + lane] = w;
+    }
+}
+
+}  // namespace bsk
+
+namespace bsh {
+
+// part 0: sort pieces; 1: LRF; 2: histogram records + ordered apply
+hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
+    if (A.k <= 0) return hipSuccess;
+    hipError_t e;
+    const int cblocks = (A.n_chunks + 3) / 4;
+    if (part == 0) {
+        if (A.n_plan > 0) bsk::k_sort2<<<A.n_plan, 256, 0, s>>>(A.plan, A.offs, A.R, A.seg, A.sorted, A.err);
+        return hipGetLastError();
+    }
+    if (part == 1) {
+        if (A.n_chunks > 0) {
+            bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
+            bsk::k_lrf_chunks<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.R, A.offs, A.cb, A.owner, A.sorted,
+                                                       A.csum);
+        }
+        bsk::k_lrf_eig<<<(A.k + 63) / 64, 64, 0, s>>>(A.k, A.cb, A.csum, A.eig, A.okf);
+        if ((e = hipMemsetAsync(A.signs, 0, sizeof(int) * 2 * (size_t)A.k, s)) != hipSuccess) return e;
+        if (A.n_chunks > 0)
+            bsk::k_lrf_sign<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.owner, A.sorted, A.eig,
+                                                     A.okf, A.signs);
+        bsk::k_lrf_fin<<<(A.k + 63) / 64, 64, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.sorted, A.eig, A.okf, A.signs,
+                                                      A.rf, A.ok);
+        return hipGetLastError();
+    }
+    if (A.n_chunks > 0)
+        bsk::k_hist_contrib<<<cblocks, 256, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.offs, A.cb, A.owner,
+                                                     A.sorted, A.rf, A.ok, A.recA, A.recB);
+    bsk::k_hist_apply<<<A.k, 64, 0, s>>>(A.kps, A.k, A.perm, A.offs, A.ok, A.recA, A.recB, A.shot, A.bits);
+    return hipGetLastError();
+}
+
+}  // namespace bsh

@@ -32,4 +32,32 @@ hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16
                            int nt, unsigned long long* best, unsigned long long* best_next, hipStream_t s);
 hipError_t launch_icp_nn(const float* src, int ns, const float4* tgt, int nt, unsigned long long* best, hipStream_t s);
 
+// load-balanced SHOT (describe2.hip): sort pieces, LRF over 64-rank chunks, records + ordered apply
+struct Describe2Args {
+    int k = 0, n_plan = 0, n_chunks = 0;
+    float R = 0.f;
+    const int4* plan = nullptr;            // {q, piece, pieces, 0}
+    const int* cb = nullptr;               // k + 1 chunk offsets
+    int* owner = nullptr;                  // keypoint of every chunk
+    const int* perm = nullptr;             // keypoints by descending neighbourhood size
+    const long long* offs = nullptr;       // k + 1 segment offsets
+    const float4* pts4 = nullptr;
+    const float4* normals = nullptr;
+    const float* kps = nullptr;
+    const unsigned long long* seg = nullptr;  // unsorted keys (gather)
+    unsigned long long* sorted = nullptr;     // sorted keys (output of k_sort2)
+    double* csum = nullptr;                   // 8 per chunk
+    double* eig = nullptr;                    // 8 per keypoint
+    int* okf = nullptr;                       // eigen ok per keypoint
+    int* signs = nullptr;                     // 2 per keypoint
+    float* rf = nullptr;
+    int* ok = nullptr;
+    uint4* recA = nullptr;
+    float4* recB = nullptr;
+    float* shot = nullptr;
+    unsigned int* bits = nullptr;
+    int* err = nullptr;  // |= 8 when a sort piece overflows its LDS buffer
+};
+hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
+
 }  // namespace bsh

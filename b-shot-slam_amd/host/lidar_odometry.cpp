@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 #include "../csrc/ctx.h"
 #include "geom.h"
@@ -15,6 +16,20 @@
 namespace myslam {
 
 static void zero_stats(bshot_frame_stats& s) { std::memset(&s, 0, sizeof(s)); }
+
+// features of one sweep computed ahead of time on a worker thread (prefetchFrameDevice)
+struct LidarOdometry::Lookahead {
+    const float* d_xyz = nullptr;
+    int n = 0;
+    std::thread th;
+    std::string err;
+    int nv = 0;
+    std::vector<int32_t> kidx;
+    std::vector<float> kr;
+    PointCloudXYZ kps, iss;
+    std::vector<uint32_t> words;
+    float ms[3] = {0.f, 0.f, 0.f};  // extract, iss, describe (worker-thread wall time)
+};
 
 LidarOdometry::LidarOdometry()
     : status_(INITIAL), shouldUpdateMap(true), sr_type_("CV"), evaluate_icp_(true), evaluate_corr_(false),
@@ -33,7 +48,22 @@ LidarOdometry::LidarOdometry(const bshot_params& p, int device)
     zero_stats(stats_);
 }
 
-LidarOdometry::~LidarOdometry() { bshot_destroy(ctx_); }
+LidarOdometry::~LidarOdometry() {
+    if (ahead_ && ahead_->th.joinable()) ahead_->th.join();
+    bshot_destroy(ctx_);
+}
+
+void LidarOdometry::joinAhead() {
+    if (!ahead_) return;
+    if (ahead_->th.joinable()) ahead_->th.join();
+    auto la = ahead_;
+    ahead_.reset();
+    if (!la->err.empty()) {
+        err_ = la->err;
+        throw std::runtime_error(err_);
+    }
+    ready_ = la;
+}
 
 void LidarOdometry::check(int rc, const char* where) {
     if (rc >= 0) return;
@@ -53,6 +83,8 @@ void LidarOdometry::setRefFrame(Frame::Ptr ref) {
 }
 
 void LidarOdometry::setSrcFrame(Frame::Ptr src) {
+    joinAhead();
+    ready_.reset();
     src_ = src;
     src_pc_ = *src_->getPointCloud();
     src_dev_ = nullptr;
@@ -61,6 +93,8 @@ void LidarOdometry::setSrcFrame(Frame::Ptr src) {
 }
 
 void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n) {
+    joinAhead();
+    if (ready_ && !(ready_->d_xyz == d_xyz && ready_->n == n)) ready_.reset();
     src_ = src;
     src_pc_.clear();
     src_dev_ = d_xyz;
@@ -69,7 +103,88 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
 }
 
 void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
+    joinAhead();
+    ready_.reset();
+    // grids + SR + ISS on the side stream (after everything already queued on the main stream,
+    // i.e. after this sweep's describe, whose normals the next describe continues from)
     check(bshot_prefetch_cloud_device(ctx_, d_xyz, n), "prefetchFrameDevice");
+    auto la = std::make_shared<Lookahead>();
+    la->d_xyz = d_xyz;
+    la->n = n;
+    Lookahead* p = la.get();
+    la->th = std::thread([this, p]() {
+        try {
+            runAhead(*p);
+        } catch (const std::exception& e) {
+            p->err = e.what();
+        }
+    });
+    ahead_ = la;
+}
+
+// worker thread: the extract + describe half of the frame for the prefetched cloud (ctx->pf) on
+// the side stream. Same steps as extractKeypoints()/computeDescriptors(), so same results.
+void LidarOdometry::runAhead(Lookahead& la) {
+    bshot_ctx* c = ctx_;
+    (void)hipSetDevice(c->device);
+    CloudState& S = c->pf;
+    auto fail = [&](const char* what) { throw std::runtime_error(std::string(what) + ": " + c->err); };
+    TicToc t_ex;
+    if (hipEventSynchronize(S.ev_sr) != hipSuccess) fail("lookahead sr");
+    if (S.h_err.p[0]) throw std::runtime_error("seg_ratio: neighbourhood with > 1024 exactly tied boundary keys");
+    const int n = S.n;
+    std::vector<int32_t> idx(n > 0 ? n : 1);
+    std::vector<float> ratio(n > 0 ? n : 1);
+    int nv = 0;
+    for (int i = 0; i < n; ++i) {
+        const float r = S.h_ratio.p[i];
+        if (r != r) continue;
+        idx[nv] = i;
+        ratio[nv] = r;
+        ++nv;
+    }
+    la.nv = nv;
+    la.kidx.resize(prm_.num_keypoints > 0 ? prm_.num_keypoints : 1);
+    la.kr.resize(la.kidx.size());
+    int k = 0;
+    if (bshot_select_topk(idx.data(), ratio.data(), nv, prm_.num_keypoints, la.kidx.data(), la.kr.data(), &k) < 0)
+        fail("topk");
+    la.kidx.resize(k);
+    la.kr.resize(k);
+    la.kps.resize(k);
+    if (k > 0 && bsh::ctx_gather_host_on(c, S, c->side, la.kidx.data(), k, c->kps, &la.kps[0][0]) != BSHOT_OK)
+        fail("lookahead gather");
+    la.ms[0] = (float)t_ex.toc();
+    TicToc t_d;
+    if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
+    if (c->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) != hipSuccess || c->p_err.ensure(1) != hipSuccess)
+        fail("alloc pinned");
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        c->p_err.p[0] = 0;
+        if (k > 0 && (hipMemcpyAsync(c->p_bits.p, c->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
+                                     c->side) != hipSuccess ||
+                      hipMemcpyAsync(c->p_err.p, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->side) != hipSuccess))
+            fail("D2H bits");
+        if (hipStreamSynchronize(c->side) != hipSuccess) fail("lookahead sync");
+        if (!(c->p_err.p[0] & 8)) break;
+        if (bsh::ctx_describe_on(c, S, c->side, k, true) != BSHOT_OK) fail("lookahead describe (fallback)");
+    }
+    if (k > 0 && (c->p_err.p[0] & 2)) throw std::runtime_error("normals neighbourhood overflow");
+    la.words.assign(c->p_bits.p, c->p_bits.p + 11 * (size_t)k);
+    la.ms[2] = (float)t_d.toc();
+    TicToc t_iss;
+    if (prm_.run_iss) {
+        if (S.iss_state != 1 || hipEventSynchronize(S.ev_iss) != hipSuccess) fail("lookahead iss");
+        if (S.h_err.p[1] & 4) throw std::runtime_error("iss: more than 512 neighbours inside the salient radius");
+        std::vector<int32_t> ii;
+        for (int i = 0; i < n; ++i)
+            if (S.h_flag.p[i]) ii.push_back(i);
+        la.iss.resize(ii.size());
+        if (!ii.empty() &&
+            bsh::ctx_gather_host_on(c, S, c->side, ii.data(), (int)ii.size(), c->gout, &la.iss[0][0]) != BSHOT_OK)
+            fail("lookahead iss gather");
+    }
+    la.ms[1] = (float)t_iss.toc();
 }
 
 void LidarOdometry::passSrc2Ref() {
@@ -92,6 +207,25 @@ void LidarOdometry::extractKeypoints() {
     TicToc t_ex;
     const int n = src_n_;
     stats_.n_points = n;
+    if (ready_ && ready_->d_xyz == src_dev_ && ready_->n == n) {
+        // computed ahead by the worker thread (prefetchFrameDevice)
+        const Lookahead& la = *ready_;
+        stats_.n_valid_ratios = la.nv;
+        stats_.n_keypoints = (int)la.kidx.size();
+        seg_ratios_ = la.kr;
+        src_->setKeypoints(std::make_shared<std::vector<Vector3f>>(la.kps));
+        if (isInitial()) {
+            passSrc2Ref();
+            ref_->setKeypoints(src_->getKeypoints());
+        }
+        cloud1_kps_ = *src_->getKeypoints();
+        cloud2_kps_ = *ref_->getKeypoints();
+        isskps_src = la.iss;
+        stats_.n_iss = (int)isskps_src.size();
+        if (isInitial()) isskps_ref = isskps_src;
+        stats_.host_ms[0] = (float)t_ex.toc();
+        return;
+    }
     // A1 + A2 (src/lidar_odometry.cpp:51-153)
     std::vector<int32_t> idx(n > 0 ? n : 1), kidx(prm_.num_keypoints > 0 ? prm_.num_keypoints : 1);
     std::vector<float> ratio(n > 0 ? n : 1), kr(kidx.size());
@@ -131,19 +265,39 @@ void LidarOdometry::computeDescriptors() {
     // A4-A7 (src/lidar_odometry.cpp:173-184); keypoints are already on the device (ctx->kps)
     TicToc t_d;
     const int k = (int)cloud1_kps_.size();
+    if (ready_ && ready_->d_xyz == src_dev_ && ready_->n == src_n_) {
+        const std::vector<uint32_t>& w = ready_->words;
+        cloud1_bshot_.resize(k);
+        auto desc = std::make_shared<std::vector<std::bitset<352>>>();
+        desc->reserve(k);
+        for (int i = 0; i < k; ++i) {
+            cloud1_bshot_[i].bits = words_to_bits(&w[11 * (size_t)i]);
+            desc->push_back(cloud1_bshot_[i].bits);
+        }
+        src_->setDescriptors(desc);
+        ready_.reset();
+        stats_.host_ms[2] = (float)t_d.toc();
+        return;
+    }
     check(bsh::ctx_describe_dev(ctx_, k), "describe");
     check(ctx_->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned bits");
     check(ctx_->p_err.ensure(1) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned err");
     const uint32_t* words = ctx_->p_bits.p;
-    if (k > 0) {
-        if (hipMemcpyAsync(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
-                           ctx_->stream) != hipSuccess ||
-            hipMemcpyAsync(ctx_->p_err.p, ctx_->errw.p, sizeof(int), hipMemcpyDeviceToHost, ctx_->stream) !=
-                hipSuccess)
-            check(BSHOT_EHIP, "D2H bits");
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        ctx_->p_err.p[0] = 0;
+        if (k > 0) {
+            if (hipMemcpyAsync(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
+                               ctx_->stream) != hipSuccess ||
+                hipMemcpyAsync(ctx_->p_err.p, ctx_->errw.p, sizeof(int), hipMemcpyDeviceToHost, ctx_->stream) !=
+                    hipSuccess)
+                check(BSHOT_EHIP, "D2H bits");
+        }
+        check(bsh::ctx_sync_main(ctx_), "describe sync");
+        ctx_->resolve_events();
+        if (!(ctx_->p_err.p[0] & 8)) break;
+        // a load-balanced sort piece overflowed (pathological duplicate d2): one workgroup per keypoint
+        check(bsh::ctx_describe_dev(ctx_, k, true), "describe (fallback)");
     }
-    check(bsh::ctx_sync_main(ctx_), "describe sync");
-    ctx_->resolve_events();
     if (k > 0 && (ctx_->p_err.p[0] & 2)) check(BSHOT_ECAP, "normals neighbourhood overflow");
     cloud1_bshot_.resize(k);
     auto desc = std::make_shared<std::vector<std::bitset<352>>>();

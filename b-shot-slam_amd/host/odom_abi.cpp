@@ -18,7 +18,6 @@ struct bshot_odom {
     std::vector<myslam::Map> replicas;
     const float* next_d = nullptr;  // lookahead cloud (bshot_odom_set_next_device)
     int next_n = 0;
-    int prefetch_early = 1;  // 1: start the lookahead before describe (default), 0: after it
 };
 
 static int guard(bshot_odom* o, const std::function<void()>& f);
@@ -39,14 +38,10 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     if (xyz) lo.setSrcFrame(f);
     else lo.setSrcFrameDevice(f, d_xyz, n);
     lo.extractKeypoints();
-    if (o->next_d && o->prefetch_early) {
-        lo.prefetchFrameDevice(o->next_d, o->next_n);
-        o->next_d = nullptr;
-    }
     lo.computeDescriptors();
     if (o->next_d) {
-        // the next sweep's grids, SR and ISS run on the side stream while the host matches,
-        // runs RANSAC/ICP and updates the map for this one
+        // the next sweep's grids/SR/ISS (side stream) and top-K/describe (worker thread) run while
+        // this one is matched, RANSAC-gated, ICP-refined and merged into the map
         lo.prefetchFrameDevice(o->next_d, o->next_n);
         o->next_d = nullptr;
     }
@@ -120,10 +115,6 @@ const char* bshot_odom_last_error(const bshot_odom* o) { return o ? o->err.c_str
 
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value) {
     if (!o || !name) return BSHOT_EINVAL;
-    if (std::string(name) == "prefetch_early") {
-        o->prefetch_early = value ? 1 : 0;
-        return BSHOT_OK;
-    }
     return bshot_set_option(o->lo->context(), name, value);
 }
 

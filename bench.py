@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--ladder-grids", type=int, default=None, help="tuning knob: 2 or 4 kNN ladder grids")
     ap.add_argument("--sr-hint", type=int, default=None, help="tuning knob: SR ladder start hint 0/1")
     ap.add_argument("--side-cu-reserve", type=int, default=None, help="tuning knob: CUs kept from the side stream")
-    ap.add_argument("--prefetch-early", type=int, default=None, help="tuning knob: lookahead before describe 0/1")
+    ap.add_argument("--opt", action="append", default=[], help="tuning knob name=value (bshot_odom_set_option)")
     return ap.parse_args()
 
 
@@ -99,9 +99,12 @@ def main():
 
     odo = bshot_py.Odometry(device=local, params=params)
     for name, val in (("ladder_grids", a.ladder_grids), ("sr_hint", a.sr_hint),
-                      ("side_cu_reserve", a.side_cu_reserve), ("prefetch_early", a.prefetch_early)):
+                      ("side_cu_reserve", a.side_cu_reserve)):
         if val is not None:
             odo.set_option(name, val)
+    for kv in a.opt:
+        name, val = kv.split("=")
+        odo.set_option(name, int(val))
     tot_pts = 0
 
     def step(i):

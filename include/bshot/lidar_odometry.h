@@ -32,7 +32,11 @@ class LidarOdometry {
     void setSrcFrame(Frame::Ptr src);
     // device-resident cloud (n x 3 floats already in HBM); the Frame keeps a host copy lazily
     void setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n);
-    // extension: start grids + SR + ISS of the next device-resident sweep on the side stream
+    // extension (throughput mode): start the NEXT device-resident sweep now -- grids, SR and ISS on
+    // the side stream, then top-K, keypoint gather and describe on a host worker thread -- while
+    // this sweep's matching, RANSAC, ICP and map update run. Call after computeDescriptors(); the
+    // next setSrcFrameDevice() with the same pointer adopts the results (identical to computing
+    // them in order).
     void prefetchFrameDevice(const float* d_xyz, int n);
     void extractKeypoints();
     void computeDescriptors();
@@ -75,6 +79,11 @@ class LidarOdometry {
 
   private:
     void check(int rc, const char* where);
+    struct Lookahead;
+    void runAhead(Lookahead& la);
+    void joinAhead();
+    std::shared_ptr<Lookahead> ahead_;  // next sweep, in flight on the worker thread
+    std::shared_ptr<Lookahead> ready_;  // adopted for the current sweep
 
     bshot_params prm_;
     bshot_ctx* ctx_ = nullptr;

@@ -124,11 +124,11 @@ const char* bshot_odom_last_error(const bshot_odom* o);
 /* one sweep through extract + describe + match + RANSAC + gate + ICP + map update */
 int bshot_odom_process(bshot_odom* o, const float* xyz, int n, bshot_frame_stats* st);
 int bshot_odom_process_device(bshot_odom* o, const float* d_xyz, int n, bshot_frame_stats* st);
-/* lookahead: the device cloud the NEXT bshot_odom_process_device call will receive; its grids,
- * SR and ISS start on the side stream during the current frame's host phases (must stay valid) */
+/* lookahead: the device cloud the NEXT bshot_odom_process_device call will receive. Its grids, SR
+ * and ISS (side stream) and its top-K + describe (worker thread) run during the current frame's
+ * matching / RANSAC / ICP / map update. Results are identical; the pointer must stay valid. */
 int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next);
-/* odometry knobs: "prefetch_early" 1 (default: lookahead starts before describe) / 0 (after it);
- * any other name is forwarded to bshot_set_option on the odometry's context */
+/* odometry knobs: forwarded to bshot_set_option on the odometry's context */
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value);
 int bshot_odom_get_keypoints(bshot_odom* o, float* xyz, int cap);
 int bshot_odom_get_ratios(bshot_odom* o, float* r, int cap);

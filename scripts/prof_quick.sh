@@ -4,7 +4,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pq}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$TAG -o t --output-format csv -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 10 --warmup 2 > $R/gpurun_out/$TAG.log 2>&1 || exit $?
+    python3 $R/bench.py --no-cpu-baseline --steps 10 --warmup 2 $2 $3 $4 > $R/gpurun_out/$TAG.log 2>&1 || exit $?
 python3 - "$R/gpurun_out/$TAG/t_kernel_stats.csv" <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
