@@ -219,8 +219,8 @@ class Context:
         self._chk(self.L.bshot_sync(self.h), "sync")
 
     def knn_stats(self):
-        w = (ctypes.c_int64 * 16)()
-        self._chk(self.L.bshot_debug_knn_stats(self.h, w, 16), "knn_stats")
+        w = (ctypes.c_int64 * 32)()
+        self._chk(self.L.bshot_debug_knn_stats(self.h, w, 32), "knn_stats")
         return list(w)
 
     def radius_pairs(self, R):

@@ -84,7 +84,9 @@ struct CloudState {
     PinBuf<unsigned char> h_flag;
     PinBuf<int> h_err;  // [0] SR, [1] ISS
     hipEvent_t ev_loaded = nullptr, ev_sr = nullptr, ev_iss = nullptr;
+    bool fine_ladder = false;  // 4 grids + 7-step sqrt(2) radius ladder (opt_ladder4)
     void fix_ladder(bool four) {
+        fine_ladder = four;
         ladder[0] = four ? &grid_l16 : &grid_fine;
         ladder[1] = &grid_fine;
         ladder[2] = four ? &grid_l4 : &grid_coarse;
@@ -105,9 +107,9 @@ struct bshot_ctx {
     CloudState pf;  // prefetch slot
 
     // tuning knobs (bshot_set_option): results never depend on them
-    int opt_ladder4 = 0;  // 1: one grid per ladder step (cell = step radius / 2); 0: two grids
-    int opt_sr_hint = 0;  // 1: SR waves start the ladder at the previous query step
-    int opt_side_reserve = 32;  // CUs the side stream may not use (kept for the main stream)
+    int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
+    int opt_side_reserve = 0;  // CUs the side stream may not use (0: plain low-priority stream; a CU-masked
+                               // stream's hipStreamDestroy was seen to hang intermittently on ROCm 7.2)
 
     DBuf<int> errw;  // describe-stage error bits (normals)
 

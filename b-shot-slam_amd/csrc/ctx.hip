@@ -2,12 +2,29 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
 #include "../host/geom.h"
 #include "ctx.h"
 #include "kernels.h"
+
+// BSHOT_TRACE=1: entry/exit trace of the C ABI calls on stderr (diagnostics only)
+static bool trace_on() {
+    static const bool on = std::getenv("BSHOT_TRACE") != nullptr;
+    return on;
+}
+struct TraceScope {
+    const char* name;
+    explicit TraceScope(const char* n) : name(n) {
+        if (trace_on()) std::fprintf(stderr, "> %s\n", name);
+    }
+    ~TraceScope() {
+        if (trace_on()) std::fprintf(stderr, "< %s\n", name);
+    }
+};
 
 #define HIPCHK(call, what)                          \
     do {                                            \
@@ -104,7 +121,9 @@ int ctx_make_side_stream(bshot_ctx* c) {
         if (hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data()) == hipSuccess)
             return BSHOT_OK;
     }
-    return hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess ? BSHOT_OK : BSHOT_EHIP;
+    int lo_prio = 0, hi_prio = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    return hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo_prio) == hipSuccess ? BSHOT_OK : BSHOT_EHIP;
 }
 
 static hipError_t ensure_events(CloudState& s) {
@@ -130,11 +149,12 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
     HIPCHK(s.errw.ensure(2), "alloc err");
     if (n > 0) {
         const int sg1 = c->stage_begin(BSHOT_STAGE_GRID, st);
-        HIPCHK(grid_build(s.grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, s.pts4.p, st), "grid build (r/8)");
-        HIPCHK(grid_build(s.grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, s.pts4.p, st), "grid build (r/2)");
         if (c->opt_ladder4) {
-            HIPCHK(grid_build(s.grid_l16, d_xyz, n, c->prm.seg_radius * 0.0625f, s.pts4.p, st), "grid build (r/16)");
-            HIPCHK(grid_build(s.grid_l4, d_xyz, n, c->prm.seg_radius * 0.25f, s.pts4.p, st), "grid build (r/4)");
+            bsh::DevGrid* const lad[4] = {&s.grid_l16, &s.grid_fine, &s.grid_l4, &s.grid_coarse};
+            HIPCHK(grid_build_ladder(lad, d_xyz, n, c->prm.seg_radius * 0.0625f, s.pts4.p, st), "grid build (ladder)");
+        } else {
+            HIPCHK(grid_build(s.grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, s.pts4.p, st), "grid build (r/8)");
+            HIPCHK(grid_build(s.grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, s.pts4.p, st), "grid build (r/2)");
         }
         c->stage_end(sg1, st);
     }
@@ -154,8 +174,8 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(hipMemsetAsync(s.errw.p, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
-        HIPCHK(launch_seg_ratio(s.ladder, s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                c->opt_sr_hint, s.ratio.p, s.errw.p, st),
+        HIPCHK(launch_seg_ratio(s.ladder, s.fine_ladder, s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+                                0, s.ratio.p, s.errw.p, st),
                "seg_ratio launch");
         c->stage_end(sg2, st);
         HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
@@ -265,7 +285,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
     const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
-    HIPCHK(launch_normals(S.ladder, S.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
+    HIPCHK(launch_normals(S.ladder, S.fine_ladder, S.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
                           c->normals.p, c->errw.p, st),
            "normals launch");
     c->stage_end(sg4, st);
@@ -480,6 +500,7 @@ void bshot_default_params(bshot_params* p) {
 }
 
 int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
+    TraceScope trace_scope_("bshot_create");
     if (!out) return BSHOT_EINVAL;
     *out = nullptr;
     int ndev = 0;
@@ -505,13 +526,20 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
 
 void bshot_destroy(bshot_ctx* c) {
     if (!c) return;
+    const bool trace = std::getenv("BSHOT_TRACE") != nullptr;
+    if (trace) std::fprintf(stderr, "destroy enter\n");
     (void)hipSetDevice(c->device);
+    if (trace) std::fprintf(stderr, "destroy step 0\n");
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->side);
+    if (trace) std::fprintf(stderr, "destroy step 1\n");
     c->resolve_events(true);
+    if (trace) std::fprintf(stderr, "destroy step 2\n");
     for (auto e : c->evpool) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->side);
+    if (trace) std::fprintf(stderr, "destroy step 3\n");
     c->cs.release();
+    if (trace) std::fprintf(stderr, "destroy step 4\n");
     c->pf.release();
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
     c->seg.release(); c->segtmp.release(); c->rf.release(); c->shot.release(); c->ok.release(); c->bits.release();
@@ -519,7 +547,9 @@ void bshot_destroy(bshot_ctx* c) {
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
     c->gidx.release(); c->gout.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
+    if (trace) std::fprintf(stderr, "destroy step 6\n");
     (void)hipStreamDestroy(c->side);
     delete c;
 }
@@ -527,6 +557,7 @@ void bshot_destroy(bshot_ctx* c) {
 const char* bshot_last_error(const bshot_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int bshot_sync(bshot_ctx* c) {
+    TraceScope trace_scope_("bshot_sync");
     if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess)
         return c->fail("sync", hipGetLastError());
     c->resolve_events();
@@ -536,6 +567,7 @@ int bshot_sync(bshot_ctx* c) {
 void* bshot_stream(bshot_ctx* c) { return (void*)c->stream; }
 
 int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n) {
+    TraceScope trace_scope_("bshot_set_cloud");
     if (!c || (n > 0 && !xyz)) return BSHOT_EINVAL;
     (void)hipSetDevice(c->device);
     // the current cloud's buffers may still be read by the side stream (its ISS)
@@ -547,18 +579,21 @@ int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n) {
 }
 
 int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
+    TraceScope trace_scope_("bshot_set_cloud_device");
     if (!c || (n > 0 && !d_xyz)) return BSHOT_EINVAL;
     (void)hipSetDevice(c->device);
     return ctx_set_cloud_dev(c, d_xyz, n);
 }
 
 int bshot_prefetch_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
+    TraceScope trace_scope_("bshot_prefetch_cloud_device");
     if (!c || n < 0 || (n > 0 && !d_xyz)) return BSHOT_EINVAL;
     (void)hipSetDevice(c->device);
     return ctx_prefetch_dev(c, d_xyz, n);
 }
 
 int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
+    TraceScope trace_scope_("bshot_seg_ratio");
     if (!c || !n_out) return BSHOT_EINVAL;
     int rc = ctx_sr_launch(c);
     if (rc) return rc;
@@ -581,6 +616,7 @@ int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
 }
 
 int bshot_iss(bshot_ctx* c, int32_t* kp_idx, int cap, int* n_out) {
+    TraceScope trace_scope_("bshot_iss");
     if (!c || !n_out) return BSHOT_EINVAL;
     int rc = ctx_iss_launch(c);
     if (rc) return rc;
@@ -600,6 +636,7 @@ int bshot_iss(bshot_ctx* c, int32_t* kp_idx, int cap, int* n_out) {
 }
 
 int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf, uint32_t* bits) {
+    TraceScope trace_scope_("bshot_describe");
     if (!c || k < 0 || (k > 0 && (!kps || !bits))) return BSHOT_EINVAL;
     if (!c->cs.grids_ok && c->cs.n > 0) return c->fail("bshot_describe: no cloud set", BSHOT_ESTATE);
     HIPCHK(c->kps.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc kps");
@@ -642,6 +679,7 @@ int bshot_get_normals(bshot_ctx* c, float* out, int n) {
 
 int bshot_match(bshot_ctx* c, const uint32_t* a, int na, const uint32_t* b, int nb, int32_t* left_nn,
                 int32_t* right_nn, int32_t* corr_q, int32_t* corr_m, int* n_corr) {
+    TraceScope trace_scope_("bshot_match");
     if (!c || !n_corr || na < 0 || nb < 0) return BSHOT_EINVAL;
     *n_corr = 0;
     if (na == 0 || nb == 0) return BSHOT_OK;
@@ -671,6 +709,7 @@ int bshot_match(bshot_ctx* c, const uint32_t* a, int na, const uint32_t* b, int 
 }
 
 int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T_out, int* iters) {
+    TraceScope trace_scope_("bshot_icp");
     if (!c || !T_out || !iters || ns < 0 || nt < 0) return BSHOT_EINVAL;
     int rc = ctx_icp(c, src, ns, tgt, nt, max_iter, T_out, iters);
     c->resolve_events();
@@ -678,6 +717,7 @@ int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, 
 }
 
 int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n) {
+    TraceScope trace_scope_("bshot_stage_times");
     if (!c) return BSHOT_EINVAL;
     c->resolve_events(true);
     for (int i = 0; i < n && i < BSHOT_NSTAGES; ++i) {
@@ -688,6 +728,7 @@ int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n) {
 }
 
 void bshot_stage_reset(bshot_ctx* c) {
+    TraceScope trace_scope_("bshot_stage_reset");
     if (!c) return;
     c->resolve_events(true);
     for (int i = 0; i < BSHOT_NSTAGES; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
@@ -718,28 +759,29 @@ int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total) {
 }
 
 int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
+    TraceScope trace_scope_("bshot_debug_knn_stats");
     if (!c || !out) return BSHOT_EINVAL;
     if (!c->cs.grids_ok) return c->fail("bshot_debug_knn_stats: no cloud", BSHOT_ESTATE);
     DBuf<unsigned long long> k;
-    HIPCHK(k.ensure(16), "alloc kst");
+    HIPCHK(k.ensure(32), "alloc kst");
     HIPCHK(c->cs.ratio.ensure(c->cs.n), "alloc ratio");
-    HIPCHK(hipMemsetAsync(k.p, 0, 16 * sizeof(unsigned long long), c->stream), "memset");
-    HIPCHK(launch_seg_ratio(c->cs.ladder, c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                            c->opt_sr_hint, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p),
+    HIPCHK(hipMemsetAsync(k.p, 0, 32 * sizeof(unsigned long long), c->stream), "memset");
+    HIPCHK(launch_seg_ratio(c->cs.ladder, c->cs.fine_ladder, c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+                            0, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p),
            "seg_ratio (stats)");
-    unsigned long long h[16];
+    unsigned long long h[32];
     HIPCHK(hipMemcpyAsync(h, k.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
     HIPCHK(hipStreamSynchronize(c->stream), "sync");
     k.release();
-    for (int i = 0; i < n && i < 16; ++i) out[i] = (int64_t)h[i];
-    return 16;
+    for (int i = 0; i < n && i < 32; ++i) out[i] = (int64_t)h[i];
+    return 32;
 }
 
 int bshot_set_option(bshot_ctx* c, const char* name, int value) {
+    TraceScope trace_scope_("bshot_set_option");
     if (!c || !name) return BSHOT_EINVAL;
     const std::string k(name);
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
-    else if (k == "sr_hint") c->opt_sr_hint = value ? 1 : 0;
     else if (k == "describe2") c->opt_describe2 = value ? 1 : 0;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;

@@ -27,9 +27,13 @@ struct GridView {
     float inv_cell;           // 1 / cell (only used for speed-insensitive cell ranges, see cell_of)
 };
 
-// the four grids of the exact-kNN radius ladder: step s searches radius r / 2^(3-s) on g[s]
+// the exact-kNN radius ladder: step s searches radius r * frac[s] on grid g[gi[s]]; the last
+// step is r itself (frac 1). Any radius is exact once it holds >= max_nn points.
 struct LadderGrids {
     GridView g[4];
+    float frac[8];
+    int gi[8];
+    int nsteps;
 };
 
 __device__ __forceinline__ unsigned long long cell_key(int ix, int iy, int iz) {

@@ -17,6 +17,7 @@ struct DevGrid {
     int* ncells = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
+    bool alias = false;  // spts borrowed from another grid (nested ladder build)
 
     GridView view() const {
         GridView v;
@@ -33,5 +34,7 @@ struct DevGrid {
 // points in index order to d_pts4 (N entries).
 hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s);
 void grid_free(DevGrid& g);
+// four nested grids (cells c0, 2c0, 4c0, 8c0) from one sort; g[1..3].spts alias g[0].spts
+hipError_t grid_build_ladder(DevGrid* const* g, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s);
 
 }  // namespace bsh

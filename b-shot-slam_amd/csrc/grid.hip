@@ -65,6 +65,74 @@ __global__ void k_grid_cells(const unsigned long long* __restrict__ keys, const 
     atomicAdd(ncells, 1);
 }
 
+// ---- nested ladder grids (cells c, 2c, 4c, 8c) from ONE sort -------------------------------
+// floor(x / (2^L c)) == floor(x / c) >> L exactly (division by a power of two commutes with the
+// double rounding), so a level-L cell is a prefix of the hierarchical key
+//   (16-bit biased level-3 x, y, z) | level-2 child bits | level-1 child bits | level-0 child bits
+// and points sorted by that key are contiguous per cell at every level.
+__device__ __forceinline__ bool ladder_cells(float x, float y, float z, float c0, int& ix, int& iy, int& iz) {
+    if (!(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z))) return false;
+    ix = cell_of(x, c0);
+    iy = cell_of(y, c0);
+    iz = cell_of(z, c0);
+    const int lim = (1 << 15) << 3;  // level-3 coordinate must fit 16 bits biased
+    return ix > -lim && ix < lim && iy > -lim && iy < lim && iz > -lim && iz < lim;
+}
+
+__global__ void k_ladder_keys(const float* __restrict__ xyz, int n, float c0, unsigned long long* __restrict__ keys,
+                              unsigned int* __restrict__ vals, float4* __restrict__ pts4) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    pts4[i] = make_float4(x, y, z, __uint_as_float((unsigned)i));
+    unsigned long long k = BS_EMPTY_KEY;
+    int ix, iy, iz;
+    if (ladder_cells(x, y, z, c0, ix, iy, iz)) {
+        const unsigned long long x3 = (unsigned)((ix >> 3) + (1 << 15)), y3 = (unsigned)((iy >> 3) + (1 << 15)),
+                                 z3 = (unsigned)((iz >> 3) + (1 << 15));
+        k = (x3 << 41) | (y3 << 25) | (z3 << 9);
+#pragma unroll
+        for (int L = 2; L >= 0; --L) {
+            const unsigned cbits = (unsigned)((((ix >> L) & 1) << 2) | (((iy >> L) & 1) << 1) | ((iz >> L) & 1));
+            k |= (unsigned long long)cbits << (3 * L);
+        }
+    }
+    keys[i] = k;
+    vals[i] = (unsigned)i;
+}
+
+// level-L cells: runs of equal key >> 3L; table entries keyed by the level's own cell_key
+__global__ void k_ladder_cells(const unsigned long long* __restrict__ keys, const unsigned int* __restrict__ vals,
+                               const float4* __restrict__ pts4, int n, int L, float c0,
+                               CellEntry* __restrict__ table, unsigned int mask, float4* __restrict__ spts,
+                               int write_spts) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const float4 p = pts4[vals[j]];
+    if (write_spts) spts[j] = p;
+    const unsigned long long k = keys[j];
+    if (k == BS_EMPTY_KEY) return;
+    const unsigned long long pk = k >> (3 * L);
+    if (j > 0 && (keys[j - 1] >> (3 * L)) == pk) return;
+    int lo = j + 1, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((keys[mid] >> (3 * L)) == pk) lo = mid + 1;
+        else hi = mid;
+    }
+    int ix, iy, iz;
+    ladder_cells(p.x, p.y, p.z, c0, ix, iy, iz);
+    const unsigned long long ck = cell_key(ix >> L, iy >> L, iz >> L);
+    unsigned int h = hash_key(ck) & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&table[h].key, BS_EMPTY_KEY, ck);
+        if (prev == BS_EMPTY_KEY) break;
+        h = (h + 1) & mask;
+    }
+    table[h].start = (unsigned)j;
+    table[h].count = (unsigned)(lo - j);
+}
+
 }  // namespace bsk
 
 // host side --------------------------------------------------------------------------------
@@ -76,9 +144,57 @@ static unsigned int pow2_at_least(unsigned int x) {
     return p;
 }
 
+// g[0..3]: grids of cell c0, 2 c0, 4 c0, 8 c0 built from one 57-bit radix sort; g[0] owns the
+// sort buffers and the cell-sorted points, g[1..3] own only their hash tables and alias g[0].spts
+hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s) {
+    hipError_t e;
+    DevGrid& g0 = *gp[0];
+    bool fresh = n > g0.cap || !g0.keys || g0.alias;
+    for (int L = 1; L < 4; ++L) fresh = fresh || !gp[L]->alias || gp[L]->spts != g0.spts || !gp[L]->table;
+    if (fresh) {
+        for (int L = 0; L < 4; ++L) grid_free(*gp[L]);
+        g0.cap = n + n / 4 + 1024;
+        if ((e = hipMalloc(&g0.keys, sizeof(unsigned long long) * g0.cap))) return e;
+        if ((e = hipMalloc(&g0.keys2, sizeof(unsigned long long) * g0.cap))) return e;
+        if ((e = hipMalloc(&g0.vals, sizeof(unsigned int) * g0.cap))) return e;
+        if ((e = hipMalloc(&g0.vals2, sizeof(unsigned int) * g0.cap))) return e;
+        if ((e = hipMalloc(&g0.spts, sizeof(float4) * g0.cap))) return e;
+        size_t tb = 0;
+        if ((e = rocprim::radix_sort_pairs(nullptr, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)g0.cap, 0, 57,
+                                           s)))
+            return e;
+        g0.tmp_bytes = tb;
+        if ((e = hipMalloc(&g0.tmp, tb))) return e;
+        for (int L = 0; L < 4; ++L) {
+            DevGrid& gl = *gp[L];
+            gl.cap = g0.cap;
+            gl.H = pow2_at_least(2u * (unsigned)g0.cap);
+            if ((e = hipMalloc(&gl.table, sizeof(CellEntry) * gl.H))) return e;
+            if (L > 0) {
+                gl.spts = g0.spts;
+                gl.alias = true;
+            }
+        }
+    }
+    const int B = 256;
+    bsk::k_ladder_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, c0, g0.keys, g0.vals, d_pts4);
+    size_t tb = g0.tmp_bytes;
+    if ((e = rocprim::radix_sort_pairs(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 57, s)))
+        return e;
+    for (int L = 0; L < 4; ++L) {
+        DevGrid& gl = *gp[L];
+        gl.n = n;
+        gl.cell = c0 * (float)(1 << L);
+        bsk::k_grid_clear<<<(gl.H + B - 1) / B, B, 0, s>>>(gl.table, gl.H);
+        bsk::k_ladder_cells<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, L, c0, gl.table, gl.H - 1,
+                                                          g0.spts, L == 0);
+    }
+    return hipGetLastError();
+}
+
 hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s) {
     hipError_t e;
-    if (n > g.cap) {
+    if (n > g.cap || g.alias || !g.keys) {
         grid_free(g);
         g.cap = n + n / 4 + 1024;
         if ((e = hipMalloc(&g.keys, sizeof(unsigned long long) * g.cap))) return e;
@@ -107,6 +223,7 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
 }
 
 void grid_free(DevGrid& g) {
+    if (g.alias) g.spts = nullptr;  // owned by the ladder's level-0 grid
     if (g.keys) (void)hipFree(g.keys);
     if (g.keys2) (void)hipFree(g.keys2);
     if (g.vals) (void)hipFree(g.vals);

@@ -139,13 +139,15 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
     float rs = r, rs2 = r2;
     int total = 0;
     int step = start_step;
-    for (; step < 4; ++step) {
-        rs = step == 0 ? r * 0.125f : (step == 1 ? r * 0.25f : (step == 2 ? r * 0.5f : r));
-        rs2 = step == 3 ? r2 : (float)((double)rs * (double)rs);
+    const int last = lg.nsteps - 1;
+    if (step > last) step = last;
+    for (; step <= last; ++step) {
+        rs = step == last ? r : r * lg.frac[step];
+        rs2 = step == last ? r2 : (float)((double)rs * (double)rs);
         hist_clear(L);
         const float sc = (float)KNN_NB / rs2;
         int cnt = 0;
-        for_candidates(lg.g[step], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             ++chunks;
             if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
             const unsigned long long m = __ballot(v);
@@ -160,8 +162,8 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
         total = cnt;
         if (total >= max_nn) break;
     }
-    if (step > 3) step = 3;
-    const GridView& g = lg.g[step];
+    if (step > last) step = last;
+    const GridView& g = lg.g[lg.gi[step]];
     const int need = total < max_nn ? total : max_nn;
     *need_out = need;
     *step_out = step;
@@ -172,7 +174,7 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
     if (kst && lane == 0) {
         atomicAdd(&kst[12], ts1 - ts0);
         atomicAdd(&kst[0], 1ull);
-        atomicAdd(&kst[1 + step], 1ull);
+        atomicAdd(&kst[16 + step], 1ull);
         atomicAdd(&kst[9], (unsigned long long)need);
         atomicAdd(&kst[10], (unsigned long long)total);
     }
@@ -360,9 +362,6 @@ __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, con
 
 // ------------------------------------------------------------------------------------------
 // A1: segmentation ratio of every point. max_nn <= 512 (host-checked).
-// hint != 0: a wave starts each query's ladder at the step that served its previous query (one
-// step lower when that step held >= 4 x max_nn points). Consecutive queries of a wave are the same
-// beam a few azimuth columns apart, so their k-NN radii are close; results do not depend on it.
 __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
                                                               float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
@@ -377,7 +376,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, co
     const int per = (n + 7) >> 3;
     const int q_begin = xg * per, q_end = min(n, q_begin + per);
     float* fl = reinterpret_cast<float*>(L->list);
-    int start = 0;
+    const int start = 0;
     for (int q = q_begin + gi * KNN_WAVES + wave; q < q_end; q += ng * KNN_WAVES) {
         const float4 sp = pts4[q];
         float out = __builtin_nanf("");
@@ -388,7 +387,6 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, co
             const unsigned long long* sorted = nullptr;
             const bool ok = knn_select(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
             const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
-            if (hint) start = (tot >= 4 * max_nn && used > 0) ? used - 1 : used;
             if (!ok) {
                 if (lane == 0) atomicOr(err, 1);
             } else if (need > 0) {
@@ -515,29 +513,44 @@ size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES; }
 
 namespace bsh {
 
-static LadderGrids ladder(const DevGrid* const* g4) {
+// g4[0..3]: grids of cell r/16, r/8, r/4, r/2 when fine_ladder, else {r/8, r/8, r/2, r/2}
+static LadderGrids ladder(const DevGrid* const* g4, bool fine_ladder) {
     LadderGrids lg;
     for (int i = 0; i < 4; ++i) lg.g[i] = g4[i]->view();
+    if (fine_ladder) {
+        // radii r * 2^(-k/2), k = 6..0; each step on the grid whose cell is rs/2 or rs/sqrt(2)
+        const float f[7] = {0.125f, 0.17677669f, 0.25f, 0.35355339f, 0.5f, 0.70710678f, 1.0f};
+        const int gi[7] = {0, 1, 1, 2, 2, 3, 3};
+        lg.nsteps = 7;
+        for (int i = 0; i < 7; ++i) { lg.frac[i] = f[i]; lg.gi[i] = gi[i]; }
+    } else {
+        const float f[4] = {0.125f, 0.25f, 0.5f, 1.0f};
+        lg.nsteps = 4;
+        for (int i = 0; i < 4; ++i) { lg.frac[i] = f[i]; lg.gi[i] = i; }
+    }
+    lg.frac[7] = 1.0f;
+    lg.gi[7] = 3;
     return lg;
 }
 
-hipError_t launch_seg_ratio(const DevGrid* const* g4, const float4* pts4, int n, float radius, int max_nn, int sr_type,
-                            int hint, float* ratio, int* err, hipStream_t s, unsigned long long* kst) {
+hipError_t launch_seg_ratio(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, int n, float radius,
+                            int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
+                            unsigned long long* kst) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     if (blocks > 8 * 256 * 4) blocks = 8 * 256 * 4;
     blocks = (blocks + 7) & ~7;
-    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4), pts4, n, radius, max_nn, sr_type, hint, ratio,
+    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, fine_ladder), pts4, n, radius, max_nn, sr_type, hint, ratio,
                                                          err, kst);
     return hipGetLastError();
 }
 
-hipError_t launch_normals(const DevGrid* const* g4, const float4* pts4, const float* kps, int k, float radius,
-                          int max_nn, float4* normals, int* err, hipStream_t s) {
+hipError_t launch_normals(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, const float* kps, int k,
+                          float radius, int max_nn, float4* normals, int* err, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (k + KNN_WAVES - 1) / KNN_WAVES;
-    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4), pts4, kps, k, radius, max_nn, normals, err);
+    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, fine_ladder), pts4, kps, k, radius, max_nn, normals, err);
     return hipGetLastError();
 }
 

@@ -1,4 +1,5 @@
 """Diagnostic: SR kernel time and kNN work counters per tuning-knob setting (same results required)."""
+import faulthandler
 import json
 import os
 import sys
@@ -8,13 +9,14 @@ import numpy as np  # noqa: E402
 
 import bshot_py  # noqa: E402
 
+faulthandler.dump_traceback_later(int(os.environ.get("HT_TIMEOUT", "100")), exit=True)
 pc, _ = bshot_py.synth_sweep(3)
 ref = None
-for ladder in (2, 4):
-    for hint in (0, 1):
+variants = [tuple(int(x) for x in v.split(",")) for v in sys.argv[1:]] or [(2, 0), (2, 1), (4, 0), (4, 1)]
+for ladder, hint in variants:
+    if True:
         c = bshot_py.Context(0)
         c.set_option("ladder_grids", ladder)
-        c.set_option("sr_hint", hint)
         c.set_cloud(pc)
         c.seg_ratio()
         c.set_timing(True)
@@ -30,7 +32,7 @@ for ladder in (2, 4):
         if ref is None:
             ref = (idx, rat)
         print(json.dumps({"ladder": ladder, "hint": hint, "sr_ms": st["seg_ratio"][0] / 10, "grid_ms": st["grid"][0] / 10,
-                          "steps": s[1:5], "chunks_per_q": s[5] / q, "avg_total": s[10] / q, "streamed": s[11],
+                          "steps": s[16:23], "chunks_per_q": s[5] / q, "avg_total": s[10] / q, "streamed": s[11],
                           "refine": s[7], "identical": bool(same),
                           "cyc_ladder": s[12] / q, "cyc_fastsel": s[13] / q, "cyc_streamsel": s[14] / q,
                           "cyc_math": s[15] / q}))

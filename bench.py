@@ -64,7 +64,6 @@ def parse():
     ap.add_argument("--no-prefetch", action="store_true",
                     help="process sweeps strictly one after another (no lookahead of the next sweep's SR/ISS)")
     ap.add_argument("--ladder-grids", type=int, default=None, help="tuning knob: 2 or 4 kNN ladder grids")
-    ap.add_argument("--sr-hint", type=int, default=None, help="tuning knob: SR ladder start hint 0/1")
     ap.add_argument("--side-cu-reserve", type=int, default=None, help="tuning knob: CUs kept from the side stream")
     ap.add_argument("--opt", action="append", default=[], help="tuning knob name=value (bshot_odom_set_option)")
     return ap.parse_args()
@@ -98,8 +97,7 @@ def main():
     npts = [int(x.shape[0]) for x in frames]
 
     odo = bshot_py.Odometry(device=local, params=params)
-    for name, val in (("ladder_grids", a.ladder_grids), ("sr_hint", a.sr_hint),
-                      ("side_cu_reserve", a.side_cu_reserve)):
+    for name, val in (("ladder_grids", a.ladder_grids), ("side_cu_reserve", a.side_cu_reserve)):
         if val is not None:
             odo.set_option(name, val)
     for kv in a.opt:

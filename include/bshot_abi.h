@@ -156,10 +156,10 @@ int bshot_map_query(bshot_map* m, const float* pos, float range, float* xyz, uin
 int bshot_map_size(bshot_map* m);
 uint64_t bshot_map_block_id(const float* pos);
 
-/* ---- tuning knobs (results never depend on them): "ladder_grids" 2 (default) or 4 grids for the
- *      exact-kNN radius ladder; "sr_hint" 0 (default) / 1: SR queries start the ladder at the
- *      step that served the wave's previous query. Takes effect at the next bshot_set_cloud.
- *      "side_cu_reserve" N (default 32): CUs the side stream (ISS, lookahead) leaves to the main one. */
+/* ---- tuning knobs (results never depend on them): "ladder_grids" 4 (default) or 2 grids for the
+ *      exact-kNN radius ladder (4: seven radii r 2^(-k/2)); "describe2" 1 (default) load-balanced
+ *      SHOT / 0 one workgroup per keypoint; "side_cu_reserve" N (default 0): CUs the side stream
+ *      (ISS, lookahead) leaves to the main one (0: plain low-priority stream). Grid options take effect at the next set_cloud. */
 int bshot_set_option(bshot_ctx* c, const char* name, int value);
 
 /* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's
