@@ -108,8 +108,8 @@ struct bshot_ctx {
 
     // tuning knobs (bshot_set_option): results never depend on them
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
-    int opt_side_reserve = 0;  // CUs the side stream may not use (0: plain low-priority stream; a CU-masked
-                               // stream's hipStreamDestroy was seen to hang intermittently on ROCm 7.2)
+    int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)
+    bool side_shared = false;   // side stream from the process-wide CU-masked pool (never destroyed)
 
     DBuf<int> errw;  // describe-stage error bits (normals)
 

@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "../host/geom.h"
@@ -104,22 +106,39 @@ void bshot_ctx::resolve_events(bool wait) {
 
 namespace bsh {
 
-// side stream restricted to all but opt_side_reserve CUs, which stay free for the main stream
+// side stream restricted to all but opt_side_reserve CUs, which stay free for the main stream.
+// CU-masked streams are created once per (device, reserve) and shared for the process lifetime:
+// destroying one was seen to hang intermittently (ROCm 7.2), so they are never destroyed.
 int ctx_make_side_stream(bshot_ctx* c) {
-    if (c->side) {
+    if (c->side && !c->side_shared) {
         (void)hipStreamSynchronize(c->side);
         (void)hipStreamDestroy(c->side);
-        c->side = nullptr;
     }
+    c->side = nullptr;
+    c->side_shared = false;
     hipDeviceProp_t prop;
     int ncu = 0;
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) ncu = prop.multiProcessorCount;
     const int keep = ncu - c->opt_side_reserve;
     if (c->opt_side_reserve > 0 && ncu > 0 && keep >= 8) {
+        static std::mutex mu;
+        static std::map<std::pair<int, int>, hipStream_t> pool;
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = pool.find({c->device, c->opt_side_reserve});
+        if (it != pool.end()) {
+            c->side = it->second;
+            c->side_shared = true;
+            return BSHOT_OK;
+        }
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int i = 0; i < keep; ++i) mask[i / 32] |= 1u << (i % 32);
-        if (hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data()) == hipSuccess)
+        hipStream_t st = nullptr;
+        if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+            pool[{c->device, c->opt_side_reserve}] = st;
+            c->side = st;
+            c->side_shared = true;
             return BSHOT_OK;
+        }
     }
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
@@ -550,7 +569,7 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
-    (void)hipStreamDestroy(c->side);
+    if (!c->side_shared) (void)hipStreamDestroy(c->side);
     delete c;
 }
 
