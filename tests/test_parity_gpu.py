@@ -32,13 +32,16 @@ def sr_ref(cloud):
     return orc.seg_ratio(cloud)
 
 
-def test_seg_ratio_bit_exact(ctx, cloud, sr_ref):
+@pytest.mark.parametrize("ladder", [4, 2])
+def test_seg_ratio_bit_exact(ctx, cloud, sr_ref, ladder):
+    ctx.set_option("ladder_grids", ladder)  # 4 nested grids / 7 radii (default) and 2 grids / 4 radii
     ctx.set_cloud(cloud)
     idx, rat = ctx.seg_ratio()
     ridx, rrat = sr_ref
     assert len(idx) == len(ridx)
     np.testing.assert_array_equal(idx, ridx)
     np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32))
+    ctx.set_option("ladder_grids", 4)
 
 
 def test_topk_keypoints_exact(sr_ref):
@@ -56,8 +59,10 @@ def test_iss_exact(ctx, cloud):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("k", [600, 2048])
-def test_describe_parity(ctx, cloud, sr_ref, k):
+@pytest.mark.parametrize("k,d2", [(600, 1), (2048, 1), (2048, 0)])
+def test_describe_parity(ctx, cloud, sr_ref, k, d2):
+    """d2 = 1: load-balanced SHOT (describe2.hip, default); 0: one workgroup per keypoint."""
+    ctx.set_option("describe2", d2)
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, k)
     kps = cloud[kidx]
@@ -78,6 +83,7 @@ def test_describe_parity(ctx, cloud, sr_ref, k):
     np.testing.assert_array_equal(rf.view(np.uint32)[~np.isnan(rf)], rrf.view(np.uint32)[~np.isnan(rrf)])
     np.testing.assert_array_equal(shot.view(np.uint32)[~np.isnan(shot)], rs.view(np.uint32)[~np.isnan(rs)])
     np.testing.assert_array_equal(bits, rb)
+    ctx.set_option("describe2", 1)
 
 
 def test_match_exact_random_and_ties(ctx):
