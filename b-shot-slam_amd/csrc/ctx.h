@@ -98,7 +98,8 @@ struct CloudState {
 struct bshot_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // main: describe, match, ICP, and everything synchronous
-    hipStream_t side = nullptr;    // side: ISS and prefetched clouds
+    hipStream_t side = nullptr;    // side: prefetched clouds (grids, SR) and the lookahead describe
+    hipStream_t iss = nullptr;     // ISS (needed only at the end of a sweep), low priority
     bshot_params prm;
     std::string err;
     bool timing = false;

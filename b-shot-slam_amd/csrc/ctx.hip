@@ -216,7 +216,7 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(hipMemsetAsync(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
-        HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient, s.pts4.p, st), "grid build (ISS)");
+        HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient, s.pts4.p, st, false), "grid build (ISS)");
         HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.errw.p + 1, st),
                "iss launch");
@@ -258,12 +258,15 @@ int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
         std::lock_guard<std::mutex> lk(c->evmu);
         c->evpool.push_back(e);
     }
+    if (c->pf.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->side, c->pf.ev_iss, 0), "wait old iss");
     int rc = cloud_load(c, c->pf, d_xyz, n, c->side);
     if (rc) return rc;
     rc = cloud_sr(c, c->pf, c->side);
     if (rc) return rc;
     if (c->prm.run_iss) {
-        rc = cloud_iss(c, c->pf, c->side);
+        // ISS is only needed at the end of the sweep: its own stream, overlapping SR and describe
+        HIPCHK(hipStreamWaitEvent(c->iss, c->pf.ev_loaded, 0), "wait cloud");
+        rc = cloud_iss(c, c->pf, c->iss);
         if (rc) return rc;
     }
     c->pf.prefetched = true;
@@ -279,8 +282,8 @@ int ctx_sr_launch(bshot_ctx* c) {
 int ctx_iss_launch(bshot_ctx* c) {
     if (!c->cs.grids_ok) return c->fail("iss: no cloud set", BSHOT_ESTATE);
     if (c->cs.iss_state == 1) return BSHOT_OK;
-    HIPCHK(hipStreamWaitEvent(c->side, c->cs.ev_loaded, 0), "wait cloud");
-    return cloud_iss(c, c->cs, c->side);
+    HIPCHK(hipStreamWaitEvent(c->iss, c->cs.ev_loaded, 0), "wait cloud");
+    return cloud_iss(c, c->cs, c->iss);
 }
 
 // keypoints already in c->kps (device, k x 3)
@@ -535,6 +538,7 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
     if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->iss, hipStreamNonBlocking, lo_prio) != hipSuccess ||
         bsh::ctx_make_side_stream(c) != BSHOT_OK) {
         delete c;
         return BSHOT_EHIP;
@@ -570,6 +574,7 @@ void bshot_destroy(bshot_ctx* c) {
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
     if (!c->side_shared) (void)hipStreamDestroy(c->side);
+    (void)hipStreamDestroy(c->iss);
     delete c;
 }
 
@@ -577,7 +582,8 @@ const char* bshot_last_error(const bshot_ctx* c) { return c ? c->err.c_str() : "
 
 int bshot_sync(bshot_ctx* c) {
     TraceScope trace_scope_("bshot_sync");
-    if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess)
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess ||
+        hipStreamSynchronize(c->iss) != hipSuccess)
         return c->fail("sync", hipGetLastError());
     c->resolve_events();
     return BSHOT_OK;

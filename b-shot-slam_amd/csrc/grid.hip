@@ -18,7 +18,7 @@ __global__ void k_grid_keys(const float* __restrict__ xyz, int n, float cell, un
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-    pts4[i] = make_float4(x, y, z, __uint_as_float((unsigned)i));
+    if (pts4) pts4[i] = make_float4(x, y, z, __uint_as_float((unsigned)i));
     unsigned long long k = BS_EMPTY_KEY;
     if (__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z)) {
         const int ix = cell_of(x, cell), iy = cell_of(y, cell), iz = cell_of(z, cell);
@@ -192,7 +192,8 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
     return hipGetLastError();
 }
 
-hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s) {
+hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s,
+                      bool write_pts4) {
     hipError_t e;
     if (n > g.cap || g.alias || !g.keys) {
         grid_free(g);
@@ -213,7 +214,7 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
     g.n = n;
     g.cell = cell;
     const int B = 256;
-    bsk::k_grid_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, cell, g.keys, g.vals, d_pts4);
+    bsk::k_grid_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, cell, g.keys, g.vals, write_pts4 ? d_pts4 : nullptr);
     size_t tb = g.tmp_bytes;
     if ((e = rocprim::radix_sort_pairs(g.tmp, tb, g.keys, g.keys2, g.vals, g.vals2, (unsigned)n, 0, 64, s))) return e;
     bsk::k_grid_clear<<<(g.H + B - 1) / B, B, 0, s>>>(g.table, g.H);

@@ -156,7 +156,23 @@ void LidarOdometry::runAhead(Lookahead& la) {
         fail("lookahead gather");
     la.ms[0] = (float)t_ex.toc();
     TicToc t_d;
+    // describe is queued on the side stream; while it runs, ISS (own stream) is collected
     if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
+    TicToc t_iss;
+    if (prm_.run_iss) {
+        if (S.iss_state != 1 || hipEventSynchronize(S.ev_iss) != hipSuccess) fail("lookahead iss");
+        if (S.h_err.p[1] & 4) throw std::runtime_error("iss: more than 512 neighbours inside the salient radius");
+        std::vector<int32_t> ii;
+        ii.reserve(1024);
+        const unsigned char* fl = S.h_flag.p;
+        for (int i = 0; i < n; ++i)
+            if (fl[i]) ii.push_back(i);
+        la.iss.resize(ii.size());
+        if (!ii.empty() &&
+            bsh::ctx_gather_host_on(c, S, c->iss, ii.data(), (int)ii.size(), c->gout, &la.iss[0][0]) != BSHOT_OK)
+            fail("lookahead iss gather");
+    }
+    la.ms[1] = (float)t_iss.toc();
     if (c->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) != hipSuccess || c->p_err.ensure(1) != hipSuccess)
         fail("alloc pinned");
     for (int attempt = 0; attempt < 2; ++attempt) {
@@ -172,19 +188,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
     if (k > 0 && (c->p_err.p[0] & 2)) throw std::runtime_error("normals neighbourhood overflow");
     la.words.assign(c->p_bits.p, c->p_bits.p + 11 * (size_t)k);
     la.ms[2] = (float)t_d.toc();
-    TicToc t_iss;
-    if (prm_.run_iss) {
-        if (S.iss_state != 1 || hipEventSynchronize(S.ev_iss) != hipSuccess) fail("lookahead iss");
-        if (S.h_err.p[1] & 4) throw std::runtime_error("iss: more than 512 neighbours inside the salient radius");
-        std::vector<int32_t> ii;
-        for (int i = 0; i < n; ++i)
-            if (S.h_flag.p[i]) ii.push_back(i);
-        la.iss.resize(ii.size());
-        if (!ii.empty() &&
-            bsh::ctx_gather_host_on(c, S, c->side, ii.data(), (int)ii.size(), c->gout, &la.iss[0][0]) != BSHOT_OK)
-            fail("lookahead iss gather");
-    }
-    la.ms[1] = (float)t_iss.toc();
+
 }
 
 void LidarOdometry::passSrc2Ref() {
