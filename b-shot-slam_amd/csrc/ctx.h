@@ -79,6 +79,8 @@ struct CloudState {
     DBuf<double> third;
     DBuf<unsigned char> issflag;
     DBuf<int> issovf;  // ISS overflow list: [0] = count, [1..] = point indices
+    DBuf<unsigned int> issnml;  // ISS non-max neighbour lists, [32][n]
+    DBuf<int> issnmc;           // their lengths (-1: overflow point)
     DBuf<int> errw;    // [0] SR error bits, [1] ISS error bits
     PinBuf<float> h_ratio;
     PinBuf<unsigned char> h_flag;
@@ -109,6 +111,7 @@ struct bshot_ctx {
 
     // tuning knobs (bshot_set_option): results never depend on them
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
+    int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
     int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)
     bool side_shared = false;   // side stream from the process-wide CU-masked pool (never destroyed)
 

@@ -77,7 +77,7 @@ void CloudState::release() {
     bsh::grid_free(grid_fine);
     bsh::grid_free(grid_coarse);
     bsh::grid_free(grid_iss);
-    xyz.release(); pts4.release(); ratio.release(); third.release(); issflag.release(); issovf.release();
+    xyz.release(); pts4.release(); ratio.release(); third.release(); issflag.release(); issovf.release(); issnml.release(); issnmc.release();
     errw.release(); h_ratio.release(); h_flag.release(); h_err.release();
     for (hipEvent_t* e : {&ev_loaded, &ev_sr, &ev_iss})
         if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
@@ -211,14 +211,18 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.third.ensure(n > 0 ? n : 1), "alloc third");
     HIPCHK(s.issflag.ensure(n > 0 ? n : 1), "alloc issflag");
     HIPCHK(s.issovf.ensure((size_t)n + 1), "alloc iss overflow");
+    HIPCHK(s.issnml.ensure((size_t)32 * (n > 0 ? n : 1)), "alloc iss nms lists");
+    HIPCHK(s.issnmc.ensure(n > 0 ? n : 1), "alloc iss nms counts");
     HIPCHK(s.h_flag.ensure(n > 0 ? n : 1), "alloc pinned flags");
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
     HIPCHK(hipMemsetAsync(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
-        HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient, s.pts4.p, st, false), "grid build (ISS)");
+        HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient * (float)c->opt_iss_cell, s.pts4.p, st, false),
+               "grid build (ISS)");
         HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
-                          c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.errw.p + 1, st),
+                          c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
+                          s.issnmc.p, s.errw.p + 1, st),
                "iss launch");
         c->stage_end(sg3, st);
         HIPCHK(hipMemcpyAsync(s.h_flag.p, s.issflag.p, n, hipMemcpyDeviceToHost, st), "D2H iss");
@@ -808,6 +812,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     const std::string k(name);
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
     else if (k == "describe2") c->opt_describe2 = value ? 1 : 0;
+    else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

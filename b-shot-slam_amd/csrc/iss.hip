@@ -100,103 +100,230 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
     }
 }
 
-// lane/point: every lane owns one point. Neighbours within the salient radius are insertion-sorted
-// by (d2, idx) into a private LDS list of ISS_LCAP keys while the 27 cells are scanned; the double
-// scatter matrix is summed sequentially in rank order and the Jacobi eigensolve runs per lane.
-// Points with more than ISS_LCAP neighbours go to the overflow list (wave kernel above).
+// lane/point: every lane owns one point. Neighbours within the salient radius are appended to a
+// private LDS column (no ordering work while the cells stream by); a lane stops scanning as soon
+// as it holds more than ISS_LCAP neighbours and hands the point to the overflow list (wave kernel
+// above). The kept keys are then sorted by (d2, idx) in registers with a bitonic network sized to
+// the wave's longest list, and the double scatter matrix is summed in that rank order.
 #define ISS_LCAP 32
 #define ISS_LBLOCK 64
 
+template <int N>
+__device__ __forceinline__ void sort_net(unsigned long long* k) {
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const unsigned long long a = k[i], b = k[j];
+                    const bool sw = up ? (a > b) : (a < b);
+                    k[i] = sw ? b : a;
+                    k[j] = sw ? a : b;
+                }
+            }
+}
+
+// sorts the lane's kept keys, sums the scatter matrix in rank order and writes the neighbours
+// inside the non-max radius (a prefix of the sorted list, nonmax <= salient) to nml[slot * n + q];
+// returns their count
+template <int N>
+__device__ __forceinline__ int iss_sum_sorted(const unsigned long long (*keys)[ISS_LBLOCK], int t, int cnt,
+                                              const float4* __restrict__ pts4, double cx, double cy, double cz,
+                                              double* sm, unsigned int r2nm_bits, unsigned int* __restrict__ nml,
+                                              int n, int q) {
+    unsigned long long k[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) k[i] = i < cnt ? keys[i][t] : ~0ull;
+    sort_net<N>(k);
+    int cnm = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (i < cnt && (unsigned int)(k[i] >> 32) < r2nm_bits) {  // d2 >= 0: bit order = float order
+            nml[(size_t)i * n + q] = (unsigned int)k[i];
+            cnm = i + 1;
+        }
+#pragma unroll
+    for (int r0 = 0; r0 < N; r0 += 8) {
+        if (r0 >= cnt) break;
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (r0 + u < cnt) pp[u] = pts4[(unsigned)(k[r0 + u] & 0xFFFFFFFFu)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (r0 + u >= cnt) break;
+            const double dx = (double)pp[u].x - cx, dy = (double)pp[u].y - cy, dz = (double)pp[u].z - cz;
+            sm[0] = sm[0] + dx * dx; sm[1] = sm[1] + dx * dy; sm[2] = sm[2] + dx * dz;
+            sm[3] = sm[3] + dy * dy; sm[4] = sm[4] + dy * dz; sm[5] = sm[5] + dz * dz;
+        }
+    }
+    return cnm;
+}
+
 __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float4* __restrict__ pts4, int n,
-                                                        float salient, int min_nn, double g21, double g32,
-                                                        double* __restrict__ third, int* __restrict__ ovf) {
+                                                        float salient, float nonmax, int min_nn, double g21,
+                                                        double g32, double* __restrict__ third, int* __restrict__ ovf,
+                                                        unsigned int* __restrict__ nml, int* __restrict__ nmc) {
     __shared__ unsigned long long keys[ISS_LCAP][ISS_LBLOCK];  // [slot][thread]: conflict-free columns
     const int t = threadIdx.x;
     const int q = blockIdx.x * ISS_LBLOCK + t;
-    if (q >= n) return;
-    const float4 c = pts4[q];
-    double out = 0.0;
-    if (__builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
+    const bool live = q < n;
+    const float4 c = live ? pts4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool fin = live && __builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z);
+    int cnt = 0;
+    if (fin) {
         const float r2 = (float)((double)salient * (double)salient);
         const double cs = (double)g.cell;
         const int x0 = (int)floor(((double)c.x - salient) / cs), x1 = (int)floor(((double)c.x + salient) / cs);
         const int y0 = (int)floor(((double)c.y - salient) / cs), y1 = (int)floor(((double)c.y + salient) / cs);
         const int z0 = (int)floor(((double)c.z - salient) / cs), z1 = (int)floor(((double)c.z + salient) / cs);
-        int cnt = 0;
-        for (int ix = x0; ix <= x1; ++ix)
-            for (int iy = y0; iy <= y1; ++iy)
-                for (int iz = z0; iz <= z1; ++iz) {
-                    unsigned int st, ct;
-                    if (!grid_lookup(g, cell_key(ix, iy, iz), st, ct)) continue;
-                    for (unsigned int j = 0; j < ct; ++j) {
-                        const float4 p = g.spts[st + j];
-                        const float d2 = d2_flann(c.x, c.y, c.z, p.x, p.y, p.z);
-                        if (!(d2 < r2)) continue;
-                        if (cnt < ISS_LCAP) {
-                            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) |
-                                                           __float_as_uint(p.w);
-                            int pos = cnt;
-                            while (pos > 0 && keys[pos - 1][t] > key) {
-                                keys[pos][t] = keys[pos - 1][t];
-                                --pos;
-                            }
-                            keys[pos][t] = key;
-                        }
-                        ++cnt;
-                    }
-                }
-        if (cnt > ISS_LCAP) {
-            ovf[1 + atomicAdd(&ovf[0], 1)] = q;
-            return;  // third[q] written by the overflow pass
-        }
-        if (cnt >= min_nn) {
-            // pcl ISS scatter matrix: double, (neighbour - centre) outer products in rank order
-            const double cx = c.x, cy = c.y, cz = c.z;
-            double sm[6] = {0, 0, 0, 0, 0, 0};
-            for (int r = 0; r < cnt; ++r) {
-                const float4 p = pts4[(unsigned)(keys[r][t] & 0xFFFFFFFFu)];
-                const double dx = (double)p.x - cx, dy = (double)p.y - cy, dz = (double)p.z - cz;
-                sm[0] = sm[0] + dx * dx; sm[1] = sm[1] + dx * dy; sm[2] = sm[2] + dx * dz;
-                sm[3] = sm[3] + dy * dy; sm[4] = sm[4] + dy * dz; sm[5] = sm[5] + dz * dz;
+        auto take = [&](const float4& p) {
+            if (d2_flann(c.x, c.y, c.z, p.x, p.y, p.z) < r2) {
+                if (cnt < ISS_LCAP)
+                    keys[cnt][t] = ((unsigned long long)__float_as_uint(d2_flann(c.x, c.y, c.z, p.x, p.y, p.z))
+                                    << 32) | __float_as_uint(p.w);
+                ++cnt;
             }
-            out = iss_third(sm, g21, g32);
+        };
+        // returns false once the lane overflowed (no need to look further)
+        auto scan_cell = [&](unsigned int st, unsigned int ct) -> bool {
+            unsigned int j = 0;
+            for (; j + 4 <= ct; j += 4) {
+                const float4 p0 = g.spts[st + j], p1 = g.spts[st + j + 1], p2 = g.spts[st + j + 2],
+                             p3 = g.spts[st + j + 3];
+                take(p0); take(p1); take(p2); take(p3);
+                if (cnt > ISS_LCAP) return false;
+            }
+            for (; j < ct; ++j) take(g.spts[st + j]);
+            return cnt <= ISS_LCAP;
+        };
+        if (x1 - x0 <= 1 && y1 - y0 <= 1 && z1 - z0 <= 1) {
+            // cell >= 2 x radius: at most 2 x 2 x 2 cells; first probes of all 8 issued together
+            unsigned long long ck[8];
+            CellEntry e[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int ix = x0 + (u >> 2), iy = y0 + ((u >> 1) & 1), iz = z0 + (u & 1);
+                ck[u] = (ix <= x1 && iy <= y1 && iz <= z1) ? cell_key(ix, iy, iz) : BS_EMPTY_KEY;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (ck[u] != BS_EMPTY_KEY) e[u] = g.table[hash_key(ck[u]) & g.mask];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (ck[u] == BS_EMPTY_KEY) continue;
+                unsigned int st = 0, ct = 0;
+                if (e[u].key == ck[u]) { st = e[u].start; ct = e[u].count; }
+                else if (e[u].key != BS_EMPTY_KEY && !grid_lookup(g, ck[u], st, ct)) ct = 0;
+                if (ct && !scan_cell(st, ct)) break;
+            }
+        } else {
+            bool go = true;
+            for (int ix = x0; go && ix <= x1; ++ix)
+                for (int iy = y0; go && iy <= y1; ++iy)
+                    for (int iz = z0; go && iz <= z1; ++iz) {
+                        unsigned int st, ct;
+                        if (grid_lookup(g, cell_key(ix, iy, iz), st, ct)) go = scan_cell(st, ct);
+                    }
         }
     }
-    third[q] = out;
+    const bool over = cnt > ISS_LCAP;
+    if (over) ovf[1 + atomicAdd(&ovf[0], 1)] = q;  // third[q] written by the overflow pass
+    const bool work = fin && !over && cnt >= min_nn;
+    double out = 0.0;
+    // wave-uniform network size: the longest kept list of the wave
+    int wmax = work ? cnt : 0;
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o, 64));
+    if (work) {
+        double sm[6] = {0, 0, 0, 0, 0, 0};
+        const double cx = c.x, cy = c.y, cz = c.z;
+        const unsigned int r2nm = __float_as_uint((float)((double)nonmax * (double)nonmax));
+        int cnm;
+        if (wmax <= 8) cnm = iss_sum_sorted<8>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+        else if (wmax <= 16) cnm = iss_sum_sorted<16>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+        else cnm = iss_sum_sorted<32>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+        out = iss_third(sm, g21, g32);
+        nmc[q] = cnm;
+    }
+    if (live && over) nmc[q] = -1;
+    if (live && !over) third[q] = out;
 }
 
-__global__ void __launch_bounds__(256) k_iss_nms(GridView g, const float4* __restrict__ pts4, int n, float nonmax,
-                                                 int min_nn, const double* __restrict__ third,
-                                                 unsigned char* __restrict__ flag) {
+// non-maximum suppression from the lane kernel's lists (nonmax <= salient): flag[i] = the point has
+// at least min_nn neighbours inside the non-max radius and none with a strictly larger third
+// eigenvalue. Overflow points (nmc = -1) are left to k_iss_nms_ovf.
+__global__ void __launch_bounds__(256) k_iss_nms_list(int n, int min_nn, const double* __restrict__ third,
+                                                      const unsigned int* __restrict__ nml,
+                                                      const int* __restrict__ nmc, unsigned char* __restrict__ flag) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    unsigned char f = 0;
     const double ti = third[i];
-    const float4 c = pts4[i];
-    if (ti > 0.0 && __builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
-        const float r2 = (float)((double)nonmax * (double)nonmax);
-        const double cs = (double)g.cell;
-        const int x0 = (int)floor(((double)c.x - nonmax) / cs), x1 = (int)floor(((double)c.x + nonmax) / cs);
-        const int y0 = (int)floor(((double)c.y - nonmax) / cs), y1 = (int)floor(((double)c.y + nonmax) / cs);
-        const int z0 = (int)floor(((double)c.z - nonmax) / cs), z1 = (int)floor(((double)c.z + nonmax) / cs);
-        int cnt = 0;
-        bool is_max = true;
-        for (int ix = x0; ix <= x1; ++ix)
-            for (int iy = y0; iy <= y1; ++iy)
-                for (int iz = z0; iz <= z1; ++iz) {
-                    unsigned int st, ct;
-                    if (!grid_lookup(g, cell_key(ix, iy, iz), st, ct)) continue;
-                    for (unsigned int j = 0; j < ct; ++j) {
-                        const float4 p = g.spts[st + j];
-                        if (d2_flann(c.x, c.y, c.z, p.x, p.y, p.z) < r2) {
-                            ++cnt;
-                            if (ti < third[__float_as_uint(p.w)]) is_max = false;
+    if (!(ti > 0.0)) {
+        flag[i] = 0;
+        return;
+    }
+    const int m = nmc[i];
+    if (m < 0) return;
+    bool bigger = false;
+    for (int s0 = 0; s0 < m; s0 += 8) {
+        unsigned int j[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) j[u] = s0 + u < m ? nml[(size_t)(s0 + u) * n + i] : (unsigned int)i;
+        double tj[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tj[u] = third[j[u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bigger = bigger || (ti < tj[u]);
+    }
+    flag[i] = (m >= min_nn && !bigger) ? 1 : 0;
+}
+
+// wave/point non-maximum suppression for the overflow list (and for every point when nonmax > salient,
+// all = true): the wave sweeps the cells around the point with 64 lanes
+__global__ void __launch_bounds__(256) k_iss_nms_wave(GridView g, const float4* __restrict__ pts4, int n,
+                                                      const int* __restrict__ ovf, int all, float nonmax, int min_nn,
+                                                      const double* __restrict__ third,
+                                                      unsigned char* __restrict__ flag) {
+    const int lane = lane_id();
+    const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const int cnt_pts = all ? n : ovf[0];
+    const float r2 = (float)((double)nonmax * (double)nonmax);
+    const double cs = (double)g.cell;
+    for (int oi = wv; oi < cnt_pts; oi += nw) {
+        const int q = all ? oi : ovf[1 + oi];
+        const double tq = third[q];
+        const float4 c = pts4[q];
+        unsigned char f = 0;
+        if (tq > 0.0 && __builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
+            const int x0 = (int)floor(((double)c.x - nonmax) / cs), x1 = (int)floor(((double)c.x + nonmax) / cs);
+            const int y0 = (int)floor(((double)c.y - nonmax) / cs), y1 = (int)floor(((double)c.y + nonmax) / cs);
+            const int z0 = (int)floor(((double)c.z - nonmax) / cs), z1 = (int)floor(((double)c.z + nonmax) / cs);
+            int cnt = 0;
+            bool bigger = false;
+            for (int ix = x0; ix <= x1 && !bigger; ++ix)
+                for (int iy = y0; iy <= y1 && !bigger; ++iy)
+                    for (int iz = z0; iz <= z1 && !bigger; ++iz) {
+                        unsigned int st, ct;
+                        if (!grid_lookup(g, cell_key(ix, iy, iz), st, ct)) continue;
+                        for (unsigned int j0 = 0; j0 < ct; j0 += 64) {
+                            bool in = false, big = false;
+                            if (j0 + lane < ct) {
+                                const float4 p = g.spts[st + j0 + lane];
+                                in = d2_flann(c.x, c.y, c.z, p.x, p.y, p.z) < r2;
+                                big = in && tq < third[__float_as_uint(p.w)];
+                            }
+                            cnt += __popcll(__ballot(in));
+                            if (__ballot(big)) bigger = true;
                         }
                     }
-                }
-        f = (cnt >= min_nn && is_max) ? 1 : 0;
+            f = (cnt >= min_nn && !bigger) ? 1 : 0;
+        }
+        if (lane == 0) flag[q] = f;
     }
-    flag[i] = f;
 }
 
 }  // namespace bsk
@@ -204,16 +331,23 @@ __global__ void __launch_bounds__(256) k_iss_nms(GridView g, const float4* __res
 namespace bsh {
 
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
-                      double g32, double* third, unsigned char* flag, int* ovf, int* err, hipStream_t s) {
+                      double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc, int* err,
+                      hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, min_nn, g21,
-                                                                             g32, third, ovf);
+    bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn,
+                                                                             g21, g32, third, ovf, nml, nmc);
     const size_t lds = sizeof(bsk::IssLds) * ISS_WAVES;
     // the overflow count is device-side: launch a full grid, idle waves exit at once
     bsk::k_iss_scatter<<<4096, 64 * ISS_WAVES, lds, s>>>(g.view(), pts4, ovf, salient, min_nn, g21, g32, third, err);
-    bsk::k_iss_nms<<<(n + 255) / 256, 256, 0, s>>>(g.view(), pts4, n, nonmax, min_nn, third, flag);
+    if (nonmax <= salient) {
+        // the non-max neighbours are a prefix of the lane kernel's sorted salient neighbours
+        bsk::k_iss_nms_list<<<(n + 255) / 256, 256, 0, s>>>(n, min_nn, third, nml, nmc, flag);
+        bsk::k_iss_nms_wave<<<1024, 256, 0, s>>>(g.view(), pts4, n, ovf, 0, nonmax, min_nn, third, flag);
+    } else {
+        bsk::k_iss_nms_wave<<<4096, 256, 0, s>>>(g.view(), pts4, n, ovf, 1, nonmax, min_nn, third, flag);
+    }
     return hipGetLastError();
 }
 

@@ -14,7 +14,8 @@ hipError_t launch_seg_ratio(const DevGrid* const* g4, bool fine_ladder, const fl
 hipError_t launch_normals(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, const float* kps, int k,
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
-                      double g32, double* third, unsigned char* flag, int* ovf, int* err, hipStream_t s);
+                      double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc,
+                      int* err, hipStream_t s);
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s);
 hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R, const long long* offs,

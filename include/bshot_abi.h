@@ -159,7 +159,8 @@ uint64_t bshot_map_block_id(const float* pos);
 /* ---- tuning knobs (results never depend on them): "ladder_grids" 4 (default) or 2 grids for the
  *      exact-kNN radius ladder (4: seven radii r 2^(-k/2)); "describe2" 1 (default) load-balanced
  *      SHOT / 0 one workgroup per keypoint; "side_cu_reserve" N (default 0): CUs the side stream
- *      (ISS, lookahead) leaves to the main one (0: plain low-priority stream). Grid options take effect at the next set_cloud. */
+ *      (ISS, lookahead) leaves to the main one (0: plain low-priority stream);
+ *      "iss_cell" 2 (default) / 1: ISS grid cell in salient radii. Grid options take effect at the next set_cloud. */
 int bshot_set_option(bshot_ctx* c, const char* name, int value);
 
 /* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's
