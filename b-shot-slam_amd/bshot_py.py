@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libbshot_amd.so")
+# BSHOT_LIB: diagnostic override (timing experiments on `make variant` builds)
+LIB_PATH = os.environ.get("BSHOT_LIB") or os.path.join(HERE, "lib", "libbshot_amd.so")
 SYNTH_PATH = os.path.join(HERE, "lib", "libbshot_synth.so")
 P = ctypes.c_void_p
 

@@ -111,6 +111,8 @@ struct bshot_ctx {
 
     // tuning knobs (bshot_set_option): results never depend on them
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
+    int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
+    int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
     int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)
     bool side_shared = false;   // side stream from the process-wide CU-masked pool (never destroyed)
@@ -138,6 +140,7 @@ struct bshot_ctx {
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
     int opt_describe2 = 1;  // tuning knob "describe2": 1 load-balanced SHOT, 0 wave/WG per keypoint
+    int ladder_mode(const CloudState& s) const { return s.fine_ladder ? (opt_ladder_front ? 2 : 1) : 0; }
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag
     DBuf<unsigned int> ma;

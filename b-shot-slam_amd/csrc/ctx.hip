@@ -193,8 +193,8 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(hipMemsetAsync(s.errw.p, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
-        HIPCHK(launch_seg_ratio(s.ladder, s.fine_ladder, s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                0, s.ratio.p, s.errw.p, st),
+        HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+                                c->opt_sr_start, s.ratio.p, s.errw.p, st),
                "seg_ratio launch");
         c->stage_end(sg2, st);
         HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
@@ -311,7 +311,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
     const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
-    HIPCHK(launch_normals(S.ladder, S.fine_ladder, S.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
+    HIPCHK(launch_normals(S.ladder, c->ladder_mode(S), S.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
                           c->normals.p, c->errw.p, st),
            "normals launch");
     c->stage_end(sg4, st);
@@ -795,8 +795,8 @@ int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
     HIPCHK(k.ensure(32), "alloc kst");
     HIPCHK(c->cs.ratio.ensure(c->cs.n), "alloc ratio");
     HIPCHK(hipMemsetAsync(k.p, 0, 32 * sizeof(unsigned long long), c->stream), "memset");
-    HIPCHK(launch_seg_ratio(c->cs.ladder, c->cs.fine_ladder, c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                            0, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p),
+    HIPCHK(launch_seg_ratio(c->cs.ladder, c->ladder_mode(c->cs), c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
+                            c->opt_sr_start, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p),
            "seg_ratio (stats)");
     unsigned long long h[32];
     HIPCHK(hipMemcpyAsync(h, k.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
@@ -813,6 +813,8 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
     else if (k == "describe2") c->opt_describe2 = value ? 1 : 0;
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
+    else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
+    else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

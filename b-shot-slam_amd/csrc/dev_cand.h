@@ -33,9 +33,78 @@ __device__ __forceinline__ void cand_init(CandLds* cs) {
     __builtin_amdgcn_wave_barrier();
 }
 
+// streams the candidates of one 64-cell round (lane = cell: spts run [st, st + cnt), off = its
+// exclusive prefix among the round's runs, total = their sum)
+template <int GROUP, class F>
+__device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs, int& epoch, float qx, float qy,
+                                                  float qz, float rs2, unsigned int st, unsigned int cnt, int off,
+                                                  int total, F& f) {
+    const int lane = lane_id();
+    const int cbase = (int)st - off;  // spts index of flattened candidate t is cbase(cell) + t
+    const unsigned long long nonempty = __ballot(cnt > 0);
+    int carry = (int)__ffsll((long long)nonempty) - 1;
+    for (int t0 = 0; t0 < total; t0 += 64 * GROUP) {
+        ++epoch;
+        const int tag = epoch << 6;
+        if (cnt > 0 && off >= t0 && off < t0 + 64 * GROUP) cs->mark[off - t0] = tag | lane;
+        __builtin_amdgcn_wave_barrier();
+        int owner[GROUP];
+#pragma unroll
+        for (int j = 0; j < GROUP; ++j) {
+            const int v = cs->mark[64 * j + lane];
+            owner[j] = (v & ~63) == tag ? (v & 63) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < GROUP; ++j) {
+            int m = wave_incl_max_i(owner[j]);
+            m = m > carry ? m : carry;
+            carry = readlane_i(m, 63);
+            owner[j] = m;
+        }
+        float4 p[GROUP];
+#pragma unroll
+        for (int j = 0; j < GROUP; ++j) {
+            const int cb = __builtin_amdgcn_ds_bpermute(owner[j] << 2, cbase);
+            const int t = t0 + 64 * j + lane;
+            p[j] = t < total ? g.spts[cb + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < GROUP; ++j) {
+            if (t0 + 64 * j < total) {
+                const int t = t0 + 64 * j + lane;
+                const float d2 = d2_flann(qx, qy, qz, p[j].x, p[j].y, p[j].z);
+                f(t < total && d2 < rs2, d2, __float_as_uint(p[j].w));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// lane's cell of round `base` of the query cube: its spts run (cnt = 0 when pruned or empty)
+__device__ __forceinline__ void cand_lookup(const GridView& g, double c, int x0, int y0, int z0, int ny, int nz,
+                                            int ncell, int cidx, float qx, float qy, float qz, double lim,
+                                            unsigned int& st, unsigned int& cnt) {
+    st = 0;
+    cnt = 0;
+    if (cidx < ncell) {
+        const int iz = cidx % nz, t = cidx / nz, iy = t % ny, ix = t / ny;
+        const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
+        const double bx0 = cx * c, by0 = cy * c, bz0 = cz * c;
+        double dx = 0, dy = 0, dz = 0;
+        if (qx < bx0) dx = bx0 - qx; else if (qx > bx0 + c) dx = qx - (bx0 + c);
+        if (qy < by0) dy = by0 - qy; else if (qy > by0 + c) dy = qy - (by0 + c);
+        if (qz < bz0) dz = bz0 - qz; else if (qz > bz0 + c) dz = qz - (bz0 + c);
+        if (dx * dx + dy * dy + dz * dz <= lim * lim) {
+            if (!grid_lookup(g, cell_key(cx, cy, cz), st, cnt)) cnt = 0;
+        }
+    }
+}
+
+// Returns false (and streams nothing) when the cube holds fewer than min_total candidates -- the
+// ball then holds fewer too. Cubes of <= 128 cells do all their lookups before streaming.
 template <int GROUP = CAND_GROUP, class F>
-__device__ __forceinline__ void for_candidates(const GridView& g, CandLds* cs, float qx, float qy, float qz, float rs,
-                                               float rs2, F&& f) {
+__device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, float qx, float qy, float qz, float rs,
+                                               float rs2, F&& f, int min_total = 0) {
     const int lane = lane_id();
     const double c = (double)g.cell;
     const int x0 = (int)floor(((double)qx - rs) / c), x1 = (int)floor(((double)qx + rs) / c);
@@ -45,65 +114,38 @@ __device__ __forceinline__ void for_candidates(const GridView& g, CandLds* cs, f
     const int ncell = nx * ny * nz;
     const double lim = (double)rs + 1.0;
     int epoch = cs->epoch;
-    for (int base = 0; base < ncell; base += 64) {
-        const int cidx = base + lane;
-        unsigned int st = 0, cnt = 0;
-        if (cidx < ncell) {
-            const int iz = cidx % nz, t = cidx / nz, iy = t % ny, ix = t / ny;
-            const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
-            const double bx0 = cx * c, by0 = cy * c, bz0 = cz * c;
-            double dx = 0, dy = 0, dz = 0;
-            if (qx < bx0) dx = bx0 - qx; else if (qx > bx0 + c) dx = qx - (bx0 + c);
-            if (qy < by0) dy = by0 - qy; else if (qy > by0 + c) dy = qy - (by0 + c);
-            if (qz < bz0) dz = bz0 - qz; else if (qz > bz0 + c) dz = qz - (bz0 + c);
-            if (dx * dx + dy * dy + dz * dz <= lim * lim) {
-                if (!grid_lookup(g, cell_key(cx, cy, cz), st, cnt)) cnt = 0;
+    bool streamed = true;
+    if (ncell <= 128) {
+        unsigned int st0, cnt0, st1 = 0, cnt1 = 0;
+        cand_lookup(g, c, x0, y0, z0, ny, nz, ncell, lane, qx, qy, qz, lim, st0, cnt0);
+        if (ncell > 64) cand_lookup(g, c, x0, y0, z0, ny, nz, ncell, 64 + lane, qx, qy, qz, lim, st1, cnt1);
+        int tot0, tot1 = 0;
+        const int off0 = wave_excl_scan((int)cnt0, tot0);
+        const int off1 = ncell > 64 ? wave_excl_scan((int)cnt1, tot1) : 0;
+        if (tot0 + tot1 < min_total) {
+            streamed = false;
+        } else {
+#pragma unroll 1
+            for (int r = 0; r < 2; ++r) {
+                const int tot = r ? tot1 : tot0;
+                if (tot > 0)
+                    cand_stream_round<GROUP>(g, cs, epoch, qx, qy, qz, rs2, r ? st1 : st0, r ? cnt1 : cnt0,
+                                             r ? off1 : off0, tot, f);
             }
         }
-        int total;
-        const int off = wave_excl_scan((int)cnt, total);
-        if (total == 0) continue;
-        const int cbase = (int)st - off;  // spts index of flattened candidate t is cbase(cell) + t
-        const unsigned long long nonempty = __ballot(cnt > 0);
-        int carry = (int)__ffsll((long long)nonempty) - 1;
-        for (int t0 = 0; t0 < total; t0 += 64 * GROUP) {
-            ++epoch;
-            const int tag = epoch << 6;
-            if (cnt > 0 && off >= t0 && off < t0 + 64 * GROUP) cs->mark[off - t0] = tag | lane;
-            __builtin_amdgcn_wave_barrier();
-            int owner[GROUP];
-#pragma unroll
-            for (int j = 0; j < GROUP; ++j) {
-                const int v = cs->mark[64 * j + lane];
-                owner[j] = (v & ~63) == tag ? (v & 63) : -1;
-            }
-#pragma unroll
-            for (int j = 0; j < GROUP; ++j) {
-                int m = wave_incl_max_i(owner[j]);
-                m = m > carry ? m : carry;
-                carry = readlane_i(m, 63);
-                owner[j] = m;
-            }
-            float4 p[GROUP];
-#pragma unroll
-            for (int j = 0; j < GROUP; ++j) {
-                const int cb = __builtin_amdgcn_ds_bpermute(owner[j] << 2, cbase);
-                const int t = t0 + 64 * j + lane;
-                p[j] = t < total ? g.spts[cb + t] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int j = 0; j < GROUP; ++j) {
-                if (t0 + 64 * j < total) {
-                    const int t = t0 + 64 * j + lane;
-                    const float d2 = d2_flann(qx, qy, qz, p[j].x, p[j].y, p[j].z);
-                    f(t < total && d2 < rs2, d2, __float_as_uint(p[j].w));
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
+    } else {
+        for (int base = 0; base < ncell; base += 64) {
+            unsigned int st, cnt;
+            cand_lookup(g, c, x0, y0, z0, ny, nz, ncell, base + lane, qx, qy, qz, lim, st, cnt);
+            int total;
+            const int off = wave_excl_scan((int)cnt, total);
+            if (total == 0) continue;
+            cand_stream_round<GROUP>(g, cs, epoch, qx, qy, qz, rs2, st, cnt, off, total, f);
         }
     }
     if (lane == 0) cs->epoch = epoch;
     __builtin_amdgcn_wave_barrier();
+    return streamed;
 }
 
 // bitonic sort of a[0, P) ascending, P power of two, one wave

@@ -31,8 +31,8 @@ struct GridView {
 // step is r itself (frac 1). Any radius is exact once it holds >= max_nn points.
 struct LadderGrids {
     GridView g[4];
-    float frac[8];
-    int gi[8];
+    float frac[9];
+    int gi[9];
     int nsteps;
 };
 

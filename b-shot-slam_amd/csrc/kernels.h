@@ -6,12 +6,12 @@
 
 namespace bsh {
 
-// g4: the radius-ladder grids (cells r/16, r/8, r/4, r/2 with fine_ladder: 7 radii r 2^(-k/2);
-// else r/8, r/8, r/2, r/2: 4 radii r 2^-k)
-hipError_t launch_seg_ratio(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, int n, float radius,
+// g4: the radius-ladder grids (cells r/16, r/8, r/4, r/2 for ladder modes 1, 2; r/8, r/8, r/2, r/2
+// for mode 0), see ladder() in knn.hip
+hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
                             unsigned long long* kst = nullptr);
-hipError_t launch_normals(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, const float* kps, int k,
+hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float4* pts4, const float* kps, int k,
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc,

@@ -147,18 +147,23 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
         hist_clear(L);
         const float sc = (float)KNN_NB / rs2;
         int cnt = 0;
-        for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        // a step whose cube holds fewer than max_nn candidates cannot deliver: skipped unstreamed
+        const bool went = for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             ++chunks;
-            if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
+#ifndef SR_EXP
+#define SR_EXP 0
+#endif
+            if (!(SR_EXP & 4) && v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
             const unsigned long long m = __ballot(v);
-            if (v) {
+            if (!(SR_EXP & 8) && v) {
                 const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
                 if (slot < KNN_CAP) L->list[slot] = knn_key(d2, idx);
             }
             cnt += __popcll(m);
-        });
+        }, step == last ? 0 : max_nn);
         __builtin_amdgcn_wave_barrier();
+        if (!went && kst && lane == 0) atomicAdd(&kst[6], 1ull);
         total = cnt;
         if (total >= max_nn) break;
     }
@@ -179,6 +184,7 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
         atomicAdd(&kst[10], (unsigned long long)total);
     }
 
+    if (SR_EXP & 2) { *sorted = L->list; return true; }
     // ---- fast path: every in-radius key is in L->list
     if (total <= KNN_CAP) {
         int Bmax = KNN_NB - 1;
@@ -313,6 +319,33 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
     return true;
 }
 
+// First ladder step worth streaming, from the point counts of the query's own cell in each ladder
+// grid (lanes 0..3 look them up in one round trip): step s is predicted to hold
+// own(g[gi[s]]) * pi * (rs / cell)^2 * 100 / pct points (a surface through the cell). Speed only --
+// any start step is exact, a late one just streams a larger ball.
+__device__ __forceinline__ int ladder_start(const LadderGrids& lg, float qx, float qy, float qz, float r, int max_nn,
+                                            int pct) {
+    const int lane = lane_id();
+    unsigned int st = 0, cnt = 0;
+    if (lane < 4) {
+        const GridView& g = lg.g[lane];
+        const double c = (double)g.cell;
+        if (!grid_lookup(g, cell_key((int)floor((double)qx / c), (int)floor((double)qy / c), (int)floor((double)qz / c)),
+                         st, cnt))
+            cnt = 0;
+    }
+    const float c0 = (float)readlane_i((int)cnt, 0), c1 = (float)readlane_i((int)cnt, 1);
+    const float c2 = (float)readlane_i((int)cnt, 2), c3 = (float)readlane_i((int)cnt, 3);
+    const float k = 3.14159265f * 100.f / (float)pct;
+    for (int s = 0; s < lg.nsteps - 1; ++s) {
+        const int L = lg.gi[s];
+        const float own = L == 0 ? c0 : L == 1 ? c1 : L == 2 ? c2 : c3;
+        const float rc = r * lg.frac[s] / lg.g[L].cell;
+        if (own * k * rc * rc >= (float)max_nn) return s;
+    }
+    return lg.nsteps - 1;
+}
+
 // sequential float sum of a[0, n) in index order (8 loads in flight, dependent adds)
 __device__ __forceinline__ float seq_sum(const float* a, int n) {
     float acc = 0.f;
@@ -376,7 +409,6 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, co
     const int per = (n + 7) >> 3;
     const int q_begin = xg * per, q_end = min(n, q_begin + per);
     float* fl = reinterpret_cast<float*>(L->list);
-    const int start = 0;
     for (int q = q_begin + gi * KNN_WAVES + wave; q < q_end; q += ng * KNN_WAVES) {
         const float4 sp = pts4[q];
         float out = __builtin_nanf("");
@@ -385,10 +417,13 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, co
         if (!origin && fin) {
             int need = 0, used = 0, tot = 0;
             const unsigned long long* sorted = nullptr;
+            const int start = hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
             const bool ok = knn_select(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
             const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
             if (!ok) {
                 if (lane == 0) atomicOr(err, 1);
+            } else if (SR_EXP & 1) {
+                out = (float)need;
             } else if (need > 0) {
                 gather_xyz(sorted, pts4, need, fl);
                 // pcl::computeCentroid: sequential float sums in rank order (lanes 0,1,2)
@@ -514,43 +549,45 @@ size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES; }
 namespace bsh {
 
 // g4[0..3]: grids of cell r/16, r/8, r/4, r/2 when fine_ladder, else {r/8, r/8, r/2, r/2}
-static LadderGrids ladder(const DevGrid* const* g4, bool fine_ladder) {
+// mode 0: grids r/8, r/8, r/2, r/2, radii r 2^-k (4 steps); 1: nested grids r/16 .. r/2, radii
+// r 2^(-k/2) from r/8 (7 steps); 2: as 1 with two more steps r/16, r/(8 sqrt 2) in front (9 steps),
+// so dense neighbourhoods stop at a ball whose keys fit the LDS list
+static LadderGrids ladder(const DevGrid* const* g4, int mode) {
     LadderGrids lg;
     for (int i = 0; i < 4; ++i) lg.g[i] = g4[i]->view();
-    if (fine_ladder) {
-        // radii r * 2^(-k/2), k = 6..0; each step on the grid whose cell is rs/2 or rs/sqrt(2)
-        const float f[7] = {0.125f, 0.17677669f, 0.25f, 0.35355339f, 0.5f, 0.70710678f, 1.0f};
-        const int gi[7] = {0, 1, 1, 2, 2, 3, 3};
-        lg.nsteps = 7;
-        for (int i = 0; i < 7; ++i) { lg.frac[i] = f[i]; lg.gi[i] = gi[i]; }
+    if (mode >= 1) {
+        // each step on the grid whose cell is rs/2 or rs/sqrt(2) (r/16 for the two front steps)
+        const float f[9] = {0.0625f, 0.08838835f, 0.125f, 0.17677669f, 0.25f, 0.35355339f, 0.5f, 0.70710678f, 1.0f};
+        const int gi[9] = {0, 0, 0, 1, 1, 2, 2, 3, 3};
+        const int o = mode == 2 ? 0 : 2;
+        lg.nsteps = 9 - o;
+        for (int i = 0; i < lg.nsteps; ++i) { lg.frac[i] = f[o + i]; lg.gi[i] = gi[o + i]; }
     } else {
         const float f[4] = {0.125f, 0.25f, 0.5f, 1.0f};
         lg.nsteps = 4;
         for (int i = 0; i < 4; ++i) { lg.frac[i] = f[i]; lg.gi[i] = i; }
     }
-    lg.frac[7] = 1.0f;
-    lg.gi[7] = 3;
     return lg;
 }
 
-hipError_t launch_seg_ratio(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, int n, float radius,
+hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
                             unsigned long long* kst) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     if (blocks > 8 * 256 * 4) blocks = 8 * 256 * 4;
     blocks = (blocks + 7) & ~7;
-    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, fine_ladder), pts4, n, radius, max_nn, sr_type, hint, ratio,
+    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type, hint, ratio,
                                                          err, kst);
     return hipGetLastError();
 }
 
-hipError_t launch_normals(const DevGrid* const* g4, bool fine_ladder, const float4* pts4, const float* kps, int k,
+hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float4* pts4, const float* kps, int k,
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (k + KNN_WAVES - 1) / KNN_WAVES;
-    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, fine_ladder), pts4, kps, k, radius, max_nn, normals, err);
+    bsk::k_normals<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, kps, k, radius, max_nn, normals, err);
     return hipGetLastError();
 }
 

@@ -186,9 +186,12 @@ int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
 /* instrumentation (outside timed regions): sum over all points of the current cloud of
  * |B(p, R)| (strict d2 < R^2, self included) -> the P_sr / P_iss work figures of SURVEY.md §8(d). */
 int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total);
-/* diagnostic: re-run the SR kernel with work counters: [0] queries, [1..4] ladder step reached
- * (r/8, r/4, r/2, r), [5] 64-candidate chunks streamed, [7] refinement passes, [8] sum of bitonic
- * sizes, [9] sum of selected neighbours, [10] sum of in-radius candidates at the final step. */
+/* diagnostic: re-run the SR kernel with work counters: [0] queries, [5] 64-candidate chunks
+ * streamed, [6] ladder steps skipped unstreamed (cube holds < max_nn candidates), [7] refinement
+ * passes, [8] sum of bitonic sizes, [9] sum of selected neighbours, [10] sum of in-radius
+ * candidates at the final step, [11] queries on the streaming selection path, [12..15] cycles in
+ * ladder / fast selection / streaming selection / ratio math, [16 + s] queries whose ladder
+ * stopped at step s. */
 int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n);
 
 #ifdef __cplusplus

@@ -1,0 +1,9 @@
+#!/bin/bash
+# SR timing of the `make variant` diagnostic builds (lib/exp/libbshot_<tag>.so) against the default build
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+timeout -k 10 100 python b-shot-slam_amd/tools/sr_variants.py sr_start=0 || exit $?
+for f in b-shot-slam_amd/lib/exp/libbshot_*.so; do
+    echo "== $f"
+    BSHOT_LIB=$R/$f timeout -k 10 100 python b-shot-slam_amd/tools/sr_variants.py sr_start=0 || exit $?
+done
