@@ -61,7 +61,7 @@ ABI_SYMBOLS = [
     "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
-    "bshot_odom_set_option",
+    "bshot_odom_set_option", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
 ]
 
 _lib = None
@@ -73,6 +73,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libbshot_amd.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (soname
+        # libamdhip64.so.7, loaded by torch under the name libamdhip64.so). Loaded after ours, it
+        # would bring a second HIP/HSA runtime that finds no GPU; loaded first, the library binds to
+        # it by soname. So torch, when installed, is imported before the library is opened.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = ctypes.CDLL(LIB_PATH)
         _lib.bshot_last_error.restype = ctypes.c_char_p
         _lib.bshot_odom_last_error.restype = ctypes.c_char_p
@@ -139,6 +147,9 @@ class Context:
 
     def prefetch_cloud_device(self, dptr, n):
         self._chk(self.L.bshot_prefetch_cloud_device(self.h, P(dptr), n), "prefetch_cloud_device")
+
+    def queue_cloud_device(self, dptr, n):
+        self._chk(self.L.bshot_queue_cloud_device(self.h, P(dptr), n), "queue_cloud_device")
 
     def set_cloud_device(self, dptr, n):
         self.n = n
@@ -294,6 +305,10 @@ class Odometry:
     def set_next_device(self, dptr, n):
         """Lookahead: the device cloud the next process_device call will receive."""
         self._chk(self.L.bshot_odom_set_next_device(self.h, P(dptr), n), "odom_set_next_device")
+
+    def set_next2_device(self, dptr, n):
+        """Lookahead depth 2: the device cloud of the process_device call after next."""
+        self._chk(self.L.bshot_odom_set_next2_device(self.h, P(dptr), n), "odom_set_next2_device")
 
     def process_device(self, dptr, n):
         st = FrameStats()

@@ -102,16 +102,19 @@ struct bshot_ctx {
     hipStream_t stream = nullptr;  // main: describe, match, ICP, and everything synchronous
     hipStream_t side = nullptr;    // side: prefetched clouds (grids, SR) and the lookahead describe
     hipStream_t iss = nullptr;     // ISS (needed only at the end of a sweep), low priority
+    hipStream_t pre = nullptr;     // grids + SR of the sweep after next (queue slot pf2), low priority
     bshot_params prm;
     std::string err;
     bool timing = false;
 
     CloudState cs;  // current cloud
-    CloudState pf;  // prefetch slot
+    CloudState pf;  // prefetch slot (next sweep: the lookahead worker describes it)
+    CloudState pf2; // queue slot (the sweep after next: grids + SR + ISS only)
 
     // tuning knobs (bshot_set_option): results never depend on them
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
+    int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
     int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)
@@ -197,6 +200,7 @@ int ctx_match_dev(bshot_ctx* c, int na, int nb);        // descriptors in c->ma 
 int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst);
 int ctx_sync_main(bshot_ctx* c);
 // explicit-cloud / explicit-stream variants (the lookahead task runs them on the side stream)
+int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1 = false);
 int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst);
 int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst,

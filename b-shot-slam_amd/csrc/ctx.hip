@@ -194,7 +194,7 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                c->opt_sr_start, s.ratio.p, s.errw.p, st),
+                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks),
                "seg_ratio launch");
         c->stage_end(sg2, st);
         HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
@@ -233,11 +233,25 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     return BSHOT_OK;
 }
 
+static bool holds(const CloudState& s, const float* d_xyz, int n) {
+    return s.prefetched && s.d_xyz == d_xyz && s.n == n && n > 0;
+}
+
+// slots move by value: their ladder pointers must be re-aimed at their own grids afterwards
+static void swap_slots(bshot_ctx* c, CloudState& a, CloudState& b) {
+    std::swap(a, b);
+    a.fix_ladder(c->opt_ladder4 != 0);
+    b.fix_ladder(c->opt_ladder4 != 0);
+}
+
 int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n) {
-    if (c->pf.prefetched && c->pf.d_xyz == d_xyz && c->pf.n == n && n > 0) {
-        std::swap(c->cs, c->pf);
-        c->cs.fix_ladder(c->opt_ladder4 != 0);
-        c->pf.fix_ladder(c->opt_ladder4 != 0);
+    if (!holds(c->pf, d_xyz, n) && holds(c->pf2, d_xyz, n)) {
+        // queued two ahead and never promoted: adopt it through the prefetch slot
+        swap_slots(c, c->pf, c->pf2);
+        c->pf2.prefetched = false;
+    }
+    if (holds(c->pf, d_xyz, n)) {
+        swap_slots(c, c->cs, c->pf);
         c->cs.prefetched = false;
         c->pf.prefetched = false;
         HIPCHK(hipStreamWaitEvent(c->stream, c->cs.ev_loaded, 0), "wait prefetch");
@@ -250,6 +264,14 @@ int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n) {
 
 int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
     if (n <= 0) return BSHOT_OK;
+    if (holds(c->pf2, d_xyz, n)) {
+        // queued earlier (grids, SR and ISS on the pre/iss streams): promote; the lookahead
+        // describe on the side stream starts after its grids
+        swap_slots(c, c->pf, c->pf2);
+        c->pf2.prefetched = false;
+        HIPCHK(hipStreamWaitEvent(c->side, c->pf.ev_loaded, 0), "wait queued cloud");
+        return BSHOT_OK;
+    }
     // the prefetch slot holds an older cloud; let work already queued on the main stream finish first
     hipEvent_t e;
     {
@@ -274,6 +296,36 @@ int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
         if (rc) return rc;
     }
     c->pf.prefetched = true;
+    return BSHOT_OK;
+}
+
+// the sweep after next: grids + SR on the pre stream, ISS on the iss stream, into the queue slot,
+// running beside the side stream's describe of the next sweep
+int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n) {
+    if (n <= 0 || holds(c->pf, d_xyz, n) || holds(c->pf2, d_xyz, n)) return BSHOT_OK;
+    // the queue slot's buffers may still be read by work queued on the main stream or by ISS
+    hipEvent_t e;
+    {
+        std::lock_guard<std::mutex> lk(c->evmu);
+        e = c->get_ev();
+    }
+    HIPCHK(hipEventRecord(e, c->stream), "record");
+    HIPCHK(hipStreamWaitEvent(c->pre, e, 0), "wait main");
+    {
+        std::lock_guard<std::mutex> lk(c->evmu);
+        c->evpool.push_back(e);
+    }
+    if (c->pf2.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->pre, c->pf2.ev_iss, 0), "wait old iss");
+    int rc = cloud_load(c, c->pf2, d_xyz, n, c->pre);
+    if (rc) return rc;
+    rc = cloud_sr(c, c->pf2, c->pre);
+    if (rc) return rc;
+    if (c->prm.run_iss) {
+        HIPCHK(hipStreamWaitEvent(c->iss, c->pf2.ev_loaded, 0), "wait cloud");
+        rc = cloud_iss(c, c->pf2, c->iss);
+        if (rc) return rc;
+    }
+    c->pf2.prefetched = true;
     return BSHOT_OK;
 }
 
@@ -543,6 +595,7 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
     if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio) != hipSuccess ||
         hipStreamCreateWithPriority(&c->iss, hipStreamNonBlocking, lo_prio) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->pre, hipStreamNonBlocking, lo_prio) != hipSuccess ||
         bsh::ctx_make_side_stream(c) != BSHOT_OK) {
         delete c;
         return BSHOT_EHIP;
@@ -559,6 +612,8 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 0\n");
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->side);
+    (void)hipStreamSynchronize(c->pre);
+    (void)hipStreamSynchronize(c->iss);
     if (trace) std::fprintf(stderr, "destroy step 1\n");
     c->resolve_events(true);
     if (trace) std::fprintf(stderr, "destroy step 2\n");
@@ -568,6 +623,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->cs.release();
     if (trace) std::fprintf(stderr, "destroy step 4\n");
     c->pf.release();
+    c->pf2.release();
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
     c->seg.release(); c->segtmp.release(); c->rf.release(); c->shot.release(); c->ok.release(); c->bits.release();
     c->ma.release(); c->lbest.release(); c->left.release();
@@ -579,6 +635,7 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 6\n");
     if (!c->side_shared) (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->iss);
+    (void)hipStreamDestroy(c->pre);
     delete c;
 }
 
@@ -587,7 +644,7 @@ const char* bshot_last_error(const bshot_ctx* c) { return c ? c->err.c_str() : "
 int bshot_sync(bshot_ctx* c) {
     TraceScope trace_scope_("bshot_sync");
     if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess ||
-        hipStreamSynchronize(c->iss) != hipSuccess)
+        hipStreamSynchronize(c->iss) != hipSuccess || hipStreamSynchronize(c->pre) != hipSuccess)
         return c->fail("sync", hipGetLastError());
     c->resolve_events();
     return BSHOT_OK;
@@ -619,6 +676,13 @@ int bshot_prefetch_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
     if (!c || n < 0 || (n > 0 && !d_xyz)) return BSHOT_EINVAL;
     (void)hipSetDevice(c->device);
     return ctx_prefetch_dev(c, d_xyz, n);
+}
+
+int bshot_queue_cloud_device(bshot_ctx* c, const float* d_xyz, int n) {
+    TraceScope trace_scope_("bshot_queue_cloud_device");
+    if (!c || n < 0 || (n > 0 && !d_xyz)) return BSHOT_EINVAL;
+    (void)hipSetDevice(c->device);
+    return ctx_queue_dev(c, d_xyz, n);
 }
 
 int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
@@ -815,6 +879,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
+    else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

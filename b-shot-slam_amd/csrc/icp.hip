@@ -11,7 +11,8 @@
 namespace bsk {
 
 #define ICP_THREADS 256
-#define ICP_TILE 2048
+// small LDS tile (4 KB): ICP runs on the main stream beside LDS-heavy side-stream kernels
+#define ICP_TILE 256
 
 __global__ void __launch_bounds__(ICP_THREADS) k_icp_nn(const float* __restrict__ src, int ns,
                                                         const float4* __restrict__ tgt, int nt, int tile,

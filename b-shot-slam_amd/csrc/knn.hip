@@ -572,10 +572,12 @@ static LadderGrids ladder(const DevGrid* const* g4, int mode) {
 
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst) {
+                            unsigned long long* kst, int max_blocks) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
-    if (blocks > 8 * 256 * 4) blocks = 8 * 256 * 4;
+    // fewer, longer-lived waves cost less dispatch; more, short-lived ones let high-priority
+    // kernels of other streams in sooner
+    if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
     blocks = (blocks + 7) & ~7;
     bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type, hint, ratio,
                                                          err, kst);

@@ -15,7 +15,9 @@
 namespace bsk {
 
 #define HM_THREADS 256
-#define HM_TILE 1024
+// a small LDS tile (6 KB): the launch runs on the main stream beside the side stream's LDS-heavy
+// kernels, and a workgroup only starts on a CU with that much LDS free
+#define HM_TILE 128
 
 // both directions in one launch: blockIdx.z == 0 -> A vs B (left), 1 -> B vs A (right)
 struct HamDir {
@@ -91,7 +93,7 @@ static bsk::HamDir ham_dir(const unsigned int* q, int nq, const unsigned int* r,
     d.qb = (nq + HM_THREADS - 1) / HM_THREADS;
     int splits = (1024 + d.qb - 1) / d.qb;
     int tile = (nr + splits - 1) / splits;
-    if (tile < 256) tile = 256;
+    if (tile < HM_TILE) tile = HM_TILE;
     d.tile = tile;
     d.splits = (nr + tile - 1) / tile;
     return d;

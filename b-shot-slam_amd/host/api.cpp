@@ -57,21 +57,52 @@ Keypoint::Ptr Keypoint::createKeypoint(Vector3f& pos, float seg_ratio, bshot_des
 }
 
 // ---------------------------------------------------------------- Map (src/mymap.cpp)
+// 1 m suppression cells: two keypoints closer than 800 mm are in the same or adjacent cells
+static inline int sup_cell(float v) { return (int)std::floor(v / 1000.f); }
+static inline uint64_t sup_key(int x, int y, int z) {
+    return ((uint64_t)(uint32_t)(x + (1 << 20)) << 42) | ((uint64_t)(uint32_t)(y + (1 << 20)) << 21) |
+           (uint64_t)(uint32_t)(z + (1 << 20));
+}
+
 void Map::addKeypoint(Keypoint::Ptr keypoint) {
-    const unsigned long block_id = getBlockID(keypoint->getPosition());
+    const Vector3f p = keypoint->getPosition();
+    const unsigned long block_id = getBlockID(p);
+    const int cx = sup_cell(p[0]), cy = sup_cell(p[1]), cz = sup_cell(p[2]);
     auto it = keypoints_.find(block_id);
+    BlockAux& ax = aux_[block_id];
     if (it == keypoints_.end()) {
         Block kp_block;
-        kp_block.insert(std::make_pair(keypoint->getPosition(), keypoint));
+        kp_block.insert(std::make_pair(p, keypoint));
         keypoints_.insert(std::make_pair(block_id, kp_block));
+        ax.cells[sup_key(cx, cy, cz)].push_back(Cand{p, keypoint.get()});
+        ax.dirty = true;
         return;
     }
-    bool isCandidate = true;
-    const Vector3f p = keypoint->getPosition();
-    for (auto& kp : it->second) {
-        if ((p - kp.first).norm() < 800 && keypoint->getSegRatio() <= kp.second->getSegRatio()) isCandidate = false;
+    // src/mymap.cpp: rejected when any keypoint of the block lies within 800 mm with a segmentation
+    // ratio >= this one's -- the same predicate over the same keypoints, visited by cell
+    const float sr = keypoint->getSegRatio();
+    // cells meeting the ball (801 mm: margin for the float norm's rounding): <= 2 per axis
+    const int x0 = sup_cell(p[0] - 801.f), x1 = sup_cell(p[0] + 801.f);
+    const int y0 = sup_cell(p[1] - 801.f), y1 = sup_cell(p[1] + 801.f);
+    const int z0 = sup_cell(p[2] - 801.f), z1 = sup_cell(p[2] + 801.f);
+    for (int gx = x0; gx <= x1; ++gx)
+        for (int gy = y0; gy <= y1; ++gy)
+            for (int gz = z0; gz <= z1; ++gz) {
+                auto c = ax.cells.find(sup_key(gx, gy, gz));
+                if (c == ax.cells.end()) continue;
+                for (const Cand& e : c->second)
+                    if ((p - e.p).norm() < 800 && sr <= e.kp->getSegRatio()) return;
+            }
+    std::vector<Cand>& mine = ax.cells[sup_key(cx, cy, cz)];
+    const bool existed = it->second.find(p) != it->second.end();
+    it->second[p] = keypoint;
+    if (existed) {
+        for (Cand& e : mine)
+            if (e.p[0] == p[0] && e.p[1] == p[1] && e.p[2] == p[2]) e.kp = keypoint.get();
+    } else {
+        mine.push_back(Cand{p, keypoint.get()});
     }
-    if (isCandidate) it->second[p] = keypoint;
+    ax.dirty = true;
 }
 
 void Map::getKeypoints(Vector3f pos, float range, PointCloudXYZ& kpts_pos, std::vector<bshot_descriptor>& descriptors) {
@@ -86,14 +117,24 @@ void Map::getKeypoints(Vector3f pos, float range, PointCloudXYZ& kpts_pos, std::
     for (int x = x_min; x <= x_max; x += prec)
         for (int y = y_min; y <= y_max; y += prec)
             for (int z = z_min; z <= z_max; z += prec) {
-                auto it = keypoints_.find(getBlockID(Vector3f((float)x, (float)y, (float)z)));
+                const unsigned long id = getBlockID(Vector3f((float)x, (float)y, (float)z));
+                auto it = keypoints_.find(id);
                 if (it == keypoints_.end()) continue;
-                kpts_pos.reserve(kpts_pos.size() + it->second.size());
-                descriptors.reserve(descriptors.size() + it->second.size());
-                for (auto& kp : it->second) {
-                    kpts_pos.push_back(kp.first);
-                    descriptors.push_back(kp.second->getDescriptor());
+                BlockAux& ax = aux_[id];
+                if (ax.dirty) {
+                    // the block's iteration order, as the reference loop visits it
+                    ax.pos.clear();
+                    ax.desc.clear();
+                    ax.pos.reserve(it->second.size());
+                    ax.desc.reserve(it->second.size());
+                    for (auto& kp : it->second) {
+                        ax.pos.push_back(kp.first);
+                        ax.desc.push_back(kp.second->getDescriptor());
+                    }
+                    ax.dirty = false;
                 }
+                kpts_pos.insert(kpts_pos.end(), ax.pos.begin(), ax.pos.end());
+                descriptors.insert(descriptors.end(), ax.desc.begin(), ax.desc.end());
             }
 }
 

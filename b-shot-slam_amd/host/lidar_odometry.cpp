@@ -122,6 +122,10 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
     ahead_ = la;
 }
 
+void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
+    check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
+}
+
 // worker thread: the extract + describe half of the frame for the prefetched cloud (ctx->pf) on
 // the side stream. Same steps as extractKeypoints()/computeDescriptors(), so same results.
 void LidarOdometry::runAhead(Lookahead& la) {

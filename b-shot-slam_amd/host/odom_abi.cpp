@@ -18,6 +18,8 @@ struct bshot_odom {
     std::vector<myslam::Map> replicas;
     const float* next_d = nullptr;  // lookahead cloud (bshot_odom_set_next_device)
     int next_n = 0;
+    const float* next2_d = nullptr;  // the one after (bshot_odom_set_next2_device)
+    int next2_n = 0;
 };
 
 static int guard(bshot_odom* o, const std::function<void()>& f);
@@ -44,7 +46,9 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
         // this one is matched, RANSAC-gated, ICP-refined and merged into the map
         lo.prefetchFrameDevice(o->next_d, o->next_n);
         o->next_d = nullptr;
+        if (o->next2_d) lo.queueFrameDevice(o->next2_d, o->next2_n);
     }
+    o->next2_d = nullptr;
     lo.featureMatching();
     lo.evaluateEstimation();
     lo.poseEstimation();
@@ -122,6 +126,13 @@ int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next) {
     if (!o || n_next < 0 || (n_next > 0 && !d_next)) return BSHOT_EINVAL;
     o->next_d = n_next > 0 ? d_next : nullptr;
     o->next_n = n_next;
+    return BSHOT_OK;
+}
+
+int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2) {
+    if (!o || n_next2 < 0 || (n_next2 > 0 && !d_next2)) return BSHOT_EINVAL;
+    o->next2_d = n_next2 > 0 ? d_next2 : nullptr;
+    o->next2_n = n_next2;
     return BSHOT_OK;
 }
 

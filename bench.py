@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
+    ap.add_argument("--depth", type=int, default=2, help="lookahead depth (1: next sweep only, 2: two sweeps)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="process sweeps strictly one after another (no lookahead of the next sweep's SR/ISS)")
     ap.add_argument("--ladder-grids", type=int, default=None, help="tuning knob: 2 or 4 kNN ladder grids")
@@ -110,6 +111,9 @@ def main():
         # sweep, so the timed region holds exactly K sweeps' work
         if not a.no_prefetch and i + 1 < nframes and i + 1 != a.warmup:
             odo.set_next_device(frames[i + 1].data_ptr(), npts[i + 1])
+            # depth 2: the sweep after next gets its grids/SR/ISS queued beside the next describe
+            if a.depth >= 2 and i + 2 < nframes and i + 2 != a.warmup:
+                odo.set_next2_device(frames[i + 2].data_ptr(), npts[i + 2])
         st = odo.process_device(frames[i].data_ptr(), npts[i])
         if a.map_bcast and world > 1:
             for r, rec in exchange_map_delta(odo.map_delta(), dist, dev):

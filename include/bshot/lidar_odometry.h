@@ -38,6 +38,9 @@ class LidarOdometry {
     // next setSrcFrameDevice() with the same pointer adopts the results (identical to computing
     // them in order).
     void prefetchFrameDevice(const float* d_xyz, int n);
+    // the sweep after the prefetched one: grids, SR and ISS queued now (no worker), promoted by
+    // the next prefetchFrameDevice() with the same pointer
+    void queueFrameDevice(const float* d_xyz, int n);
     void extractKeypoints();
     void computeDescriptors();
     void featureMatching();

@@ -4,6 +4,7 @@
 // pcl::PointCloud<pcl::PointXYZ> in getKeypoints is replaced by PointCloudXYZ.
 #pragma once
 #include <cmath>
+#include <cstdint>
 #include <memory>
 #include <unordered_map>
 #include <vector>
@@ -36,6 +37,21 @@ class Map {
   private:
     BlockMap keypoints_;
     int prec = 10000;  // map grid (mm)
+
+    // acceleration only (contents and iteration order of keypoints_ are untouched): per block, its
+    // keypoints bucketed in 1 m cells for the 800 mm suppression test of addKeypoint, and a flat
+    // copy of the block in iteration order for getKeypoints, rebuilt after the block changes
+    struct Cand {
+        Vector3f p;
+        const Keypoint* kp;
+    };
+    struct BlockAux {
+        std::unordered_map<uint64_t, std::vector<Cand>> cells;
+        bool dirty = true;
+        std::vector<Vector3f> pos;
+        std::vector<bshot_descriptor> desc;
+    };
+    std::unordered_map<unsigned long, BlockAux> aux_;
 };
 
 }  // namespace myslam

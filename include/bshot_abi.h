@@ -69,6 +69,10 @@ int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n); /* device-r
  *      and ISS on the context's side stream now; the next bshot_set_cloud_device with the same
  *      pointer and size adopts the results instead of recomputing them. d_xyz must stay valid. */
 int bshot_prefetch_cloud_device(bshot_ctx* c, const float* d_xyz, int n);
+/* queue a cloud two sweeps ahead: grids + SR on a low-priority stream and ISS now, beside the
+ * describe of the prefetched cloud; a later bshot_prefetch_cloud_device (or set_cloud_device) with
+ * the same pointer promotes it. */
+int bshot_queue_cloud_device(bshot_ctx* c, const float* d_xyz, int n);
 
 /* ---- A1: segmentation ratio for every point, index order, origin / NaN skipped
  *      (replaces the loop at src/lidar_odometry.cpp:53-126). idx/ratio caller-sized >= n. --- */
@@ -128,6 +132,9 @@ int bshot_odom_process_device(bshot_odom* o, const float* d_xyz, int n, bshot_fr
  * and ISS (side stream) and its top-K + describe (worker thread) run during the current frame's
  * matching / RANSAC / ICP / map update. Results are identical; the pointer must stay valid. */
 int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next);
+/* the cloud after that (two calls ahead): its grids, SR and ISS are queued as well, so they run
+ * beside the next sweep's describe. Optional; same validity rule. */
+int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2);
 /* odometry knobs: forwarded to bshot_set_option on the odometry's context */
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value);
 int bshot_odom_get_keypoints(bshot_odom* o, float* xyz, int cap);

@@ -100,3 +100,41 @@ def test_bitset_layout_roundtrip():
     m.add([0, 0, 0], 0.5, words)
     _, b = m.query([0, 0, 0])
     assert np.array_equal(b[0], words)
+
+
+def test_map_suppression_random_model():
+    """Randomised adds against a direct model of src/mymap.cpp addKeypoint (every keypoint of the
+    block within 800 mm and with ratio >= the new one rejects it; same quantised position
+    replaces): the cell-bucketed suppression test must keep exactly the same keypoints."""
+    rng = np.random.default_rng(7)
+    m = bshot_py.KeypointMap()
+    blocks = {}
+    f32 = np.float32
+    for t in range(2500):
+        p = rng.uniform(-14000, 14000, 3).astype(np.float32)
+        if t % 7 == 0 and t:
+            p = prev.copy()  # noqa: F821 -- an earlier position again (replacement path)
+        prev = p
+        r = float(rng.uniform(0, 1))
+        bits = rng.integers(0, 2 ** 32, 11, dtype=np.uint64).astype(np.uint32)
+        m.add(p, r, bits)
+        q = tuple(f32(int(np.trunc(f32(x) / f32(10))) * 10) for x in p)
+        bid = bshot_py.KeypointMap.block_id(np.array(q, np.float32))
+        blk = blocks.get(bid)
+        if blk is None:
+            blocks[bid] = {q: (f32(r), bits)}
+            continue
+        ok = True
+        for k, (rr, _) in blk.items():
+            dx, dy, dz = f32(q[0] - k[0]), f32(q[1] - k[1]), f32(q[2] - k[2])
+            if np.sqrt(f32(f32(f32(dx * dx) + f32(dy * dy)) + f32(dz * dz))) < f32(800) and f32(r) <= rr:
+                ok = False
+                break
+        if ok:
+            blk[q] = (f32(r), bits)
+    assert m.size() == sum(len(b) for b in blocks.values())
+    xyz, b = m.query([0, 0, 0], 40000.0)
+    got = sorted((tuple(x), tuple(w)) for x, w in zip(xyz.tolist(), b.tolist()))
+    want = sorted((tuple(float(v) for v in k), tuple(int(v) for v in w)) for blk in blocks.values()
+                  for k, (_, w) in blk.items())
+    assert got == want

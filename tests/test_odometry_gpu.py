@@ -70,12 +70,14 @@ def test_odometry_no_icp_no_iss():
     _run_pair(range(3), run_icp=0, run_iss=0)
 
 
-def test_odometry_lookahead_device_frames():
+@pytest.mark.parametrize("depth", [1, 2])
+def test_odometry_lookahead_device_frames(depth):
     """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
-    stream during the current one (bshot_odom_set_next_device) -- results must not change."""
+    stream during the current one (bshot_odom_set_next_device; depth 2 also queues the sweep after
+    next, bshot_odom_set_next2_device) -- results must not change."""
     import torch
 
-    frames = [bshot_py.synth_sweep(f)[0] for f in range(20, 24)]
+    frames = [bshot_py.synth_sweep(f)[0] for f in range(20, 25)]
     dev = [torch.from_numpy(x).to("cuda:0") for x in frames]
     torch.cuda.synchronize()
     od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=1024))
@@ -84,6 +86,8 @@ def test_odometry_lookahead_device_frames():
         for f, (xyz, d) in enumerate(zip(frames, dev)):
             if f + 1 < len(dev):
                 od.set_next_device(dev[f + 1].data_ptr(), len(frames[f + 1]))
+                if depth == 2 and f + 2 < len(dev):
+                    od.set_next2_device(dev[f + 2].data_ptr(), len(frames[f + 2]))
             st = od.process_device(d.data_ptr(), len(xyz))
             so = oo.process(xyz)
             assert st.n_keypoints == so.n_keypoints and st.n_iss == so.n_iss and st.n_inliers == so.n_inliers, f
