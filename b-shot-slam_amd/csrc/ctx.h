@@ -9,6 +9,7 @@
 
 #include "../../include/bshot_abi.h"
 #include "grid.h"
+#include "kernels.h"
 
 template <typename T>
 struct DBuf {
@@ -150,7 +151,17 @@ struct bshot_ctx {
     DBuf<unsigned long long> lbest;
     DBuf<int> left;
 
+    // host timeline (diagnostics): BSHOT_HOST_TRACE=<file> records named steady-clock stamps of
+    // both host threads, written as CSV when the context is destroyed
+    bool htrace_on = false;
+    std::mutex htmu;
+    std::vector<std::pair<const char*, long long>> htrace;
+    void hmark(const char* name);
+
     // icp
+    DBuf<bsh::IcpState> istate;
+    PinBuf<bsh::IcpState> p_istate;
+    int opt_icp_dev = 0;  // 1: ICP loop resident on the device (one sync); 0: host Umeyama per iteration (faster under load)
     DBuf<float> isrc, itgt3;
     DBuf<float4> itgt;
     DBuf<unsigned long long> ibest;

@@ -1,6 +1,10 @@
 // ctx.hip -- bshot_ctx lifecycle and the GPU half of the C ABI (include/bshot_abi.h).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -52,6 +56,14 @@ hipEvent_t bshot_ctx::get_ev() {
     (void)hipEventCreate(&e);
     return e;
 }
+void bshot_ctx::hmark(const char* name) {
+    if (!htrace_on) return;
+    const long long t = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::lock_guard<std::mutex> lk(htmu);
+    htrace.emplace_back(name, t);
+}
+
 int bshot_ctx::stage_begin(int st, hipStream_t s) {
     if (!timing) return -1;
     std::lock_guard<std::mutex> lk(evmu);
@@ -523,6 +535,38 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                "H2D src");
         HIPCHK(hipMemsetAsync(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
         HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
+        if (c->opt_icp_dev) {
+            // max_iter (NN, update) pairs queued at once; converged iterations return immediately
+            HIPCHK(c->istate.ensure(1), "alloc icp state");
+            HIPCHK(c->p_istate.ensure(1), "alloc pinned icp state");
+            IcpState& h = *c->p_istate.p;
+            const bg::Mat4f I = bg::Mat4f::identity();
+            std::memcpy(h.T, I.m, sizeof(h.T));
+            std::memcpy(h.fin, I.m, sizeof(h.fin));
+            h.prev_mse = 1.7976931348623157e308;
+            h.it = 0;
+            h.done = 0;
+            h.max_iter = max_iter;
+            h.pad = 0;
+            HIPCHK(hipMemcpyAsync(c->istate.p, c->p_istate.p, sizeof(IcpState), hipMemcpyHostToDevice, c->stream),
+                   "H2D icp state");
+            const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
+            const int n_it = max_iter > 1 ? max_iter : 1;
+            for (int j = 0; j < n_it; ++j) {
+                const int b = j & 1;
+                HIPCHK(launch_icp_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
+                                      c->istate.p, ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b,
+                                      c->ibest.p + (size_t)ns * (b ^ 1), c->stream),
+                       "icp iteration");
+            }
+            c->stage_end(sg14);
+            HIPCHK(hipMemcpyAsync(c->p_istate.p, c->istate.p, sizeof(IcpState), hipMemcpyDeviceToHost, c->stream),
+                   "D2H icp state");
+            HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
+            std::memcpy(T, h.fin, sizeof(float) * 16);
+            *iters = h.it;
+            return BSHOT_OK;
+        }
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
         const unsigned long long* best = c->p_best.p;
         double prev_mse = 1.7976931348623157e308;
@@ -587,6 +631,7 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
     if (hipSetDevice(device) != hipSuccess) return BSHOT_EHIP;
     bshot_ctx* c = new bshot_ctx();
     c->device = device;
+    c->htrace_on = std::getenv("BSHOT_HOST_TRACE") != nullptr;
     if (p) c->prm = *p;
     else bshot_default_params(&c->prm);
     // main stream at the highest priority: its short kernels (match, ICP) run during the host
@@ -620,6 +665,12 @@ void bshot_destroy(bshot_ctx* c) {
     for (auto e : c->evpool) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->side);
     if (trace) std::fprintf(stderr, "destroy step 3\n");
+    if (c->htrace_on) {
+        if (FILE* f = std::fopen(std::getenv("BSHOT_HOST_TRACE"), "w")) {
+            for (auto& e : c->htrace) std::fprintf(f, "%s,%lld\n", e.first, e.second);
+            std::fclose(f);
+        }
+    }
     c->cs.release();
     if (trace) std::fprintf(stderr, "destroy step 4\n");
     c->pf.release();
@@ -629,7 +680,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->ma.release(); c->lbest.release(); c->left.release();
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
-    c->gidx.release(); c->gout.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
@@ -880,6 +931,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
+    else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

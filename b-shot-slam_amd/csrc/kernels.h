@@ -33,6 +33,17 @@ hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t 
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
 hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,
                            int nt, unsigned long long* best, unsigned long long* best_next, hipStream_t s);
+// device-resident ICP loop state (ctx_icp with opt icp_dev): step T, accumulated fin, PCL
+// convergence bookkeeping
+struct IcpState {
+    float T[16];
+    float fin[16];
+    double prev_mse;
+    int it, done, max_iter, pad;
+};
+// one (NN, update) iteration pair; no-ops once st->done
+hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int ns, const float4* tgt, int nt,
+                          unsigned long long* best, unsigned long long* best_next, hipStream_t s);
 hipError_t launch_icp_nn(const float* src, int ns, const float4* tgt, int nt, unsigned long long* best, hipStream_t s);
 
 // load-balanced SHOT (describe2.hip): sort pieces, LRF over 64-rank chunks, records + ordered apply

@@ -28,6 +28,7 @@ struct HamDir {
 };
 
 __global__ void __launch_bounds__(HM_THREADS) k_ham_min(HamDir d0, HamDir d1) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     const HamDir& D = blockIdx.z == 0 ? d0 : d1;
     if ((int)blockIdx.x >= D.qb || (int)blockIdx.y >= D.splits) return;
     const unsigned int* __restrict__ q = D.q;
@@ -73,6 +74,7 @@ __global__ void __launch_bounds__(HM_THREADS) k_ham_min(HamDir d0, HamDir d1) {
 
 __global__ void k_mutual(const unsigned long long* __restrict__ lbest, int na, const unsigned long long* __restrict__ rbest,
                          int* __restrict__ left, int* __restrict__ right, int nb, int* __restrict__ flag) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nb) right[i] = (int)(rbest[i] & 0xFFFFFFFFu);
     if (i < na) {

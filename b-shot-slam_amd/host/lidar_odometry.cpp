@@ -93,7 +93,9 @@ void LidarOdometry::setSrcFrame(Frame::Ptr src) {
 }
 
 void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n) {
+    ctx_->hmark("M_frame");
     joinAhead();
+    ctx_->hmark("M_joined");
     if (ready_ && !(ready_->d_xyz == d_xyz && ready_->n == n)) ready_.reset();
     src_ = src;
     src_pc_.clear();
@@ -107,6 +109,7 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
     ready_.reset();
     // grids + SR + ISS on the side stream (after everything already queued on the main stream,
     // i.e. after this sweep's describe, whose normals the next describe continues from)
+    ctx_->hmark("M_prefetch");
     check(bshot_prefetch_cloud_device(ctx_, d_xyz, n), "prefetchFrameDevice");
     auto la = std::make_shared<Lookahead>();
     la->d_xyz = d_xyz;
@@ -120,10 +123,12 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
         }
     });
     ahead_ = la;
+    ctx_->hmark("M_prefetched");
 }
 
 void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
     check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
+    ctx_->hmark("M_queued");
 }
 
 // worker thread: the extract + describe half of the frame for the prefetched cloud (ctx->pf) on
@@ -134,7 +139,9 @@ void LidarOdometry::runAhead(Lookahead& la) {
     CloudState& S = c->pf;
     auto fail = [&](const char* what) { throw std::runtime_error(std::string(what) + ": " + c->err); };
     TicToc t_ex;
+    c->hmark("W_start");
     if (hipEventSynchronize(S.ev_sr) != hipSuccess) fail("lookahead sr");
+    c->hmark("W_sr_ready");
     if (S.h_err.p[0]) throw std::runtime_error("seg_ratio: neighbourhood with > 1024 exactly tied boundary keys");
     const int n = S.n;
     std::vector<int32_t> idx(n > 0 ? n : 1);
@@ -161,7 +168,9 @@ void LidarOdometry::runAhead(Lookahead& la) {
     la.ms[0] = (float)t_ex.toc();
     TicToc t_d;
     // describe is queued on the side stream; while it runs, ISS (own stream) is collected
+    c->hmark("W_topk_done");
     if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
+    c->hmark("W_describe_queued");
     TicToc t_iss;
     if (prm_.run_iss) {
         if (S.iss_state != 1 || hipEventSynchronize(S.ev_iss) != hipSuccess) fail("lookahead iss");
@@ -177,6 +186,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
             fail("lookahead iss gather");
     }
     la.ms[1] = (float)t_iss.toc();
+    c->hmark("W_iss_done");
     if (c->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) != hipSuccess || c->p_err.ensure(1) != hipSuccess)
         fail("alloc pinned");
     for (int attempt = 0; attempt < 2; ++attempt) {
@@ -191,6 +201,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
     }
     if (k > 0 && (c->p_err.p[0] & 2)) throw std::runtime_error("normals neighbourhood overflow");
     la.words.assign(c->p_bits.p, c->p_bits.p + 11 * (size_t)k);
+    c->hmark("W_done");
     la.ms[2] = (float)t_d.toc();
 
 }
@@ -329,6 +340,7 @@ void LidarOdometry::featureMatching() {
     } else {
         const Matrix4f rp = ref_->getPose();
         globalMap_.getKeypoints(rp.topRightCorner(), prm_.map_range, cloud2_kps_, cloud2_bshot_);
+        ctx_->hmark("M_map_query");
         for (const Vector3f& q : *ref_->getKeypoints()) cloud2_kps_.push_back(rp.transformPoint(q));
         std::vector<bshot_descriptor> rb = eigen2dc(ref_->getDescriptors());
         cloud2_bshot_.insert(cloud2_bshot_.end(), rb.begin(), rb.end());
@@ -340,7 +352,9 @@ void LidarOdometry::featureMatching() {
     for (int i = 0; i < nb; ++i) bits_to_words(cloud2_bshot_[i].bits, &b[11 * (size_t)i]);
     std::vector<int32_t> left(na > 0 ? na : 1), right(nb > 0 ? nb : 1), cq(na > 0 ? na : 1), cm(na > 0 ? na : 1);
     int nc = 0;
+    ctx_->hmark("M_match_prep");
     check(bshot_match(ctx_, a.data(), na, b.data(), nb, left.data(), right.data(), cq.data(), cm.data(), &nc), "match");
+    ctx_->hmark("M_matched");
     stats_.n_mutual = nc;
     stats_.host_ms[3] = (float)t_m.toc();
     TicToc t_r;
@@ -352,6 +366,7 @@ void LidarOdometry::featureMatching() {
                        cm.data(), nc, prm_.ransac_max_iter, prm_.ransac_thresh, T, iq.data(), im.data(), &ni),
           "ransac");
     std::memcpy(T_ransac_.m, T, sizeof(T));
+    ctx_->hmark("M_ransac");
     corr_.resize(ni);
     for (int i = 0; i < ni; ++i) corr_[i] = std::make_pair(iq[i], im[i]);
     stats_.n_inliers = ni;
@@ -389,6 +404,7 @@ void LidarOdometry::evaluateEstimation() {
     int iters = 0;
     check(bshot_icp(ctx_, src.data(), k, m ? &cloud2_kps_[0][0] : nullptr, m, prm_.icp_max_iter, Ticp, &iters), "icp");
     stats_.icp_iters = iters;
+    ctx_->hmark("M_icp");
     stats_.host_ms[5] = (float)t_icp.toc();
     Matrix4f F;
     std::memcpy(F.m, Ticp, sizeof(Ticp));
@@ -420,6 +436,7 @@ void LidarOdometry::updateMap() {
     std::memcpy(stats_.pose, T_best_.m, sizeof(stats_.pose));
     stats_.map_size = globalMap_.size();
     stats_.host_ms[6] = (float)t_map.toc();
+    ctx_->hmark("M_map");
 }
 
 void LidarOdometry::updateCorrespondence() {
