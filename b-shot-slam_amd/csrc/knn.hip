@@ -21,9 +21,26 @@
 namespace bsk {
 
 #define KNN_NB 256
-#define KNN_CAP 1024
-#define KNN_SCAT 512
+// LDS per wave sets k_seg_ratio's occupancy (latency-bound candidate streaming): 640 + 384 keys
+// -> 11.3 KB per wave, 14 waves per CU (1024 + 512 gave 10); measured 1.23 -> 0.96 ms per sweep
+#ifndef KNN_CAP
+#define KNN_CAP 640
+#endif
+#ifndef KNN_SCAT
+#define KNN_SCAT 384
+#endif
 #define KNN_WAVES 2
+// list + scat double as the 4 x 512-float rank-order arrays of the finishing math and as the
+// bitonic buffer (P <= 1024) of the general path
+static_assert(KNN_CAP + KNN_SCAT >= 1024, "list + scat must hold 1024 keys");
+#ifndef SR_WPE
+#define SR_WPE 4  // VGPRs <= 128: 4 waves per SIMD, above the LDS limit
+#endif
+#if SR_WPE > 0
+#define SR_ATTR __attribute__((amdgpu_waves_per_eu(SR_WPE)))
+#else
+#define SR_ATTR
+#endif
 
 struct KnnLds {
     unsigned int hist[KNN_NB];
@@ -375,15 +392,15 @@ __device__ __forceinline__ float seq_dot(const float* a, const float* b, int n) 
 __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, const float4* __restrict__ pts4, int need,
                                            float* fl) {
     const int lane = lane_id();
-    unsigned int myidx[KNN_CAP / 128];
+    unsigned int myidx[512 / 64];
 #pragma unroll
-    for (int j = 0; j < KNN_CAP / 128; ++j) {
+    for (int j = 0; j < 512 / 64; ++j) {
         const int r = lane + 64 * j;
         myidx[j] = r < need ? (unsigned int)(sorted[r] & 0xFFFFFFFFu) : 0u;
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int j = 0; j < KNN_CAP / 128; ++j) {
+    for (int j = 0; j < 512 / 64; ++j) {
         const int r = lane + 64 * j;
         if (r < need) {
             const float4 p = pts4[myidx[j]];
@@ -395,7 +412,7 @@ __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, con
 
 // ------------------------------------------------------------------------------------------
 // A1: segmentation ratio of every point. max_nn <= 512 (host-checked).
-__global__ void __launch_bounds__(64 * KNN_WAVES) k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
+__global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
                                                               float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
                                                               unsigned long long* __restrict__ kst) {

@@ -151,6 +151,7 @@ def main():
     last = frames[-1]
     ctx.set_cloud_device(last.data_ptr(), npts[-1])
     P_sr = ctx.radius_pairs(params.seg_radius)
+    kst = [int(x) for x in ctx.knn_stats()]  # SR work counters of the same sweep (separate launch)
     k_eff = float(np.mean([s.n_keypoints for s in stats]))
     m_eff = float(np.mean([s.n_target for s in stats]))
     icp_it = float(np.mean([s.icp_iters for s in stats]))
@@ -174,6 +175,14 @@ def main():
                 "traffic_source": tsrc, "alg_bytes_per_launch": alg[dname],
                 "ms_per_launch": round(per_launch_ms[dname], 4),
                 "convention": "SURVEY.md 8(d) pair-gather bytes; DESIGN.md section 4"}
+        if dname == "seg_ratio":
+            # the same launch on the candidate-gather convention: the float4 candidates the radius
+            # ladder actually streams (64 per chunk) + query read + ratio write
+            g = 16.0 * 64.0 * kst[5] + 20.0 * n_eff
+            roof["gather_bytes_per_launch"] = g
+            roof["achieved_gather"] = round(g / (per_launch_ms[dname] * 1e-3) / 1e9, 1)
+            roof["frac_gather"] = round(roof["achieved_gather"] / HBM_PEAK_GBPS, 4)
+            roof["candidates_per_query"] = round(64.0 * kst[5] / max(1, kst[0]), 1)
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference algorithm), rank 0 only
     cpu = None
