@@ -21,20 +21,19 @@
 namespace bsk {
 
 #define KNN_NB 256
-// LDS per wave sets k_seg_ratio's occupancy (latency-bound candidate streaming): 640 + 384 keys
-// -> 11.3 KB per wave, 14 waves per CU (1024 + 512 gave 10); measured 1.23 -> 0.96 ms per sweep
+// LDS per wave sets k_seg_ratio's occupancy (its candidate streaming is latency-bound). The list
+// holds every in-radius key of the deciding ladder step; the counting sort of the selected
+// prefix (<= KNN_PRE keys) runs in place through registers, so there is no scatter buffer:
+// 768 keys + hist + offsets + candidate marks = 9.2 KB per wave -> 16 waves per CU, the VGPR
+// limit at <= 128 VGPRs (1024 keys + a 512-key scatter buffer gave 10 waves: 1.23 ms; 640 + 384
+// gave 14: 0.96 ms).
 #ifndef KNN_CAP
-#define KNN_CAP 640
+#define KNN_CAP 768
 #endif
-#ifndef KNN_SCAT
-#define KNN_SCAT 384
-#endif
+#define KNN_PRE 512  // largest prefix the counting sort handles (8 keys per lane)
 #define KNN_WAVES 2
-// list + scat double as the 4 x 512-float rank-order arrays of the finishing math and as the
-// bitonic buffer (P <= 1024) of the general path
-static_assert(KNN_CAP + KNN_SCAT >= 1024, "list + scat must hold 1024 keys");
 #ifndef SR_WPE
-#define SR_WPE 4  // VGPRs <= 128: 4 waves per SIMD, above the LDS limit
+#define SR_WPE 4  // VGPRs <= 128: 4 waves per SIMD
 #endif
 #if SR_WPE > 0
 #define SR_ATTR __attribute__((amdgpu_waves_per_eu(SR_WPE)))
@@ -42,13 +41,18 @@ static_assert(KNN_CAP + KNN_SCAT >= 1024, "list + scat must hold 1024 keys");
 #define SR_ATTR
 #endif
 
+// list, hist and boff are contiguous: after the selection they double as the bitonic buffer of the
+// general path (P <= 1024 keys) and as the rank-order float arrays of the finishing math (3 x 512
+// coordinates, plus 512 CVS terms)
 struct KnnLds {
+    unsigned long long list[KNN_CAP];  // in-radius keys of the last ladder step; then the sorted result
     unsigned int hist[KNN_NB];
     unsigned int boff[KNN_NB + 4];
     CandLds cand;
-    unsigned long long list[KNN_CAP];   // in-radius keys of the last ladder step; then the sorted result
-    unsigned long long scat[KNN_SCAT];  // bucket-grouped prefix (counting-sort scatter target)
 };
+static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 4 * (KNN_NB + 4) >= 8192,
+              "list + hist + boff must hold 1024 keys");
+static_assert(KNN_CAP >= KNN_PRE, "the prefix must fit the list");
 
 __device__ __forceinline__ int bucket_of(float d2, float lo, float sc) {
     const float v = (d2 - lo) * sc;
@@ -108,7 +112,7 @@ __device__ __forceinline__ int prefix_offsets(KnnLds* L, int Bmax) {
     }
     int tot;
     int run = wave_excl_scan(s, tot);
-    if (tot <= KNN_SCAT) {
+    if (tot <= KNN_PRE) {
 #pragma unroll
         for (int j = 0; j < KNN_NB / 64; ++j) {
             const int b = lane * (KNN_NB / 64) + j;
@@ -123,17 +127,31 @@ __device__ __forceinline__ int prefix_offsets(KnnLds* L, int Bmax) {
     return tot;
 }
 
-// keys scattered bucket-grouped in scat[0, tot) -> exact (d2, idx) order in list[0, tot)
-__device__ __forceinline__ void rank_into_list(KnnLds* L, int tot, float sc0) {
+// keys scattered bucket-grouped in list[0, tot) -> exact (d2, idx) order in list[0, tot), in place
+// (every lane ranks its keys against the bucket first, then all write)
+__device__ __forceinline__ void rank_in_place(KnnLds* L, int tot, float sc0) {
     const int lane = lane_id();
-    for (int i = lane; i < tot; i += 64) {
-        const unsigned long long key = L->scat[i];
-        const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
-        const unsigned s0 = L->boff[b], e0 = L->boff[b + 1];
-        unsigned rank = 0;
-        for (unsigned j = s0; j < e0; ++j) rank += L->scat[j] < key ? 1u : 0u;
-        L->list[s0 + rank] = key;
+    unsigned long long kk[KNN_PRE / 64];
+    unsigned int dst[KNN_PRE / 64];
+#pragma unroll
+    for (int j = 0; j < KNN_PRE / 64; ++j) {
+        const int i = lane + 64 * j;
+        kk[j] = 0;
+        dst[j] = 0;
+        if (i < tot) {
+            const unsigned long long key = L->list[i];
+            const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
+            const unsigned s0 = L->boff[b], e0 = L->boff[b + 1];
+            unsigned rank = 0;
+            for (unsigned q = s0; q < e0; ++q) rank += L->list[q] < key ? 1u : 0u;
+            kk[j] = key;
+            dst[j] = s0 + rank;
+        }
     }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < KNN_PRE / 64; ++j)
+        if (lane + 64 * j < tot) L->list[dst[j]] = kk[j];
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -210,14 +228,24 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
             Bmax = hist_cross(L, need, &below);
         }
         const int tot = prefix_offsets(L, Bmax);
-        if (tot <= KNN_SCAT) {
-            for (int i = lane; i < total; i += 64) {
-                const unsigned long long key = L->list[i];
-                const int b = bucket_of(__uint_as_float((unsigned)(key >> 32)), 0.f, sc0);
-                if (b <= Bmax) L->scat[atomicAdd(&L->hist[b], 1u)] = key;
+        if (tot <= KNN_PRE) {
+            // scatter the prefix bucket-grouped into the front of the list, through registers
+            unsigned long long kk[KNN_CAP / 64];
+#pragma unroll
+            for (int j = 0; j < KNN_CAP / 64; ++j) {
+                const int i = lane + 64 * j;
+                kk[j] = i < total ? L->list[i] : ~0ull;
             }
             __builtin_amdgcn_wave_barrier();
-            rank_into_list(L, tot, sc0);
+#pragma unroll
+            for (int j = 0; j < KNN_CAP / 64; ++j) {
+                if (lane + 64 * j < total) {
+                    const int b = bucket_of(__uint_as_float((unsigned)(kk[j] >> 32)), 0.f, sc0);
+                    if (b <= Bmax) L->list[atomicAdd(&L->hist[b], 1u)] = kk[j];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            rank_in_place(L, tot, sc0);
             *sorted = L->list;
             if (kst) {
                 const unsigned long long ts2 = cycle_stamp();
@@ -225,7 +253,7 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
             }
             return true;
         }
-        // a boundary bucket too crowded for the scatter buffer: refine by streaming (rare)
+        // a boundary bucket too crowded for the in-place counting sort: refine by streaming (rare)
     }
     if (kst && lane == 0) atomicAdd(&kst[11], 1ull);
 
@@ -235,7 +263,7 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
     int levels = 0;
     if (total > need) {
         // the level-0 histogram of the final ladder step is intact here: prefix_offsets only
-        // rewrites it when the prefix fits the scatter buffer
+        // rewrites it when the prefix fits the counting sort
         int below_acc = 0;
         float w = rs2;
         for (int lev = 0; lev < 3; ++lev) {
@@ -260,7 +288,7 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
             B[lev] = Bl;
             levels = lev + 1;
             below_acc += below;
-            if (below_acc + (int)L->hist[Bl] <= KNN_SCAT) break;
+            if (below_acc + (int)L->hist[Bl] <= KNN_PRE) break;
             if (lev == 2) {
                 if (below_acc + (int)L->hist[Bl] <= KNN_CAP) break;
                 return false;
@@ -276,16 +304,16 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
         // level-0 histogram is current: counting sort of the prefix, streamed
         const int Bmax = lv >= 1 ? B[0] : KNN_NB - 1;
         const int tot = prefix_offsets(L, Bmax);
-        if (tot <= KNN_SCAT) {
+        if (tot <= KNN_PRE) {
             for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
                 ++chunks;
                 if (v) {
                     const int b = bucket_of(d2, 0.f, sc0);
-                    if (b <= Bmax) L->scat[atomicAdd(&L->hist[b], 1u)] = knn_key(d2, idx);
+                    if (b <= Bmax) L->list[atomicAdd(&L->hist[b], 1u)] = knn_key(d2, idx);
                 }
             });
             __builtin_amdgcn_wave_barrier();
-            rank_into_list(L, tot, sc0);
+            rank_in_place(L, tot, sc0);
             *sorted = L->list;
             if (kst) {
                 const unsigned long long ts2 = cycle_stamp();
@@ -329,9 +357,10 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
             atomicAdd(&kst[14], ts2 - ts1);
         }
     }
-    for (int i = cnt + lane; i < P; i += 64) L->list[i] = ~0ull;
+    unsigned long long* buf = L->list;  // P <= 1024 keys: spans list, hist and boff (dead here)
+    for (int i = cnt + lane; i < P; i += 64) buf[i] = ~0ull;
     __builtin_amdgcn_wave_barrier();
-    wave_bitonic(L->list, P);
+    wave_bitonic(buf, P);
     *sorted = L->list;
     return true;
 }
@@ -468,23 +497,23 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
                 } else {
                     // CVS / CVSN: per-neighbour terms in parallel, sequential float sum in rank order
                     const float ctn = sqrtf((tx * tx + ty * ty) + tz * tz);
+                    // a skipped neighbour stores +0: sum + (+0) == sum, as sum starts at +0 and so
+                    // is never -0 (the only value +0 changes)
                     float* term = fl + 1536;
-                    unsigned int* use = reinterpret_cast<unsigned int*>(L->hist);
                     for (int r0 = 0; r0 < need; r0 += 64) {
                         const int r = r0 + lane;
                         if (r < need) {
                             const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
                             const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
                             const float dot = (tx * vx + ty * vy) + tz * vz;
-                            use[r] = (ctn == 0.f || vn == 0.f) ? 0u : 1u;
-                            term[r] = sr_type == 1 ? dot : dot / (ctn * vn);
+                            const bool use = !(ctn == 0.f || vn == 0.f);
+                            term[r] = !use ? 0.f : (sr_type == 1 ? dot : dot / (ctn * vn));
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
                     float sum = 0.f;
                     if (lane == 0)
-                        for (int r = 0; r < need; ++r)
-                            if (use[r]) sum = sum + term[r];
+                        for (int r = 0; r < need; ++r) sum = sum + term[r];
                     sum = __shfl(sum, 0, 64);
                     out = fabsf(sum) / (float)need;
                 }

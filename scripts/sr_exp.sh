@@ -4,6 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 timeout -k 10 100 python b-shot-slam_amd/tools/sr_variants.py "$@" || exit $?
+shopt -s nullglob
 for f in b-shot-slam_amd/lib/exp/libbshot_*.so; do
     echo "== $f"
     BSHOT_LIB=$R/$f timeout -k 10 100 python b-shot-slam_amd/tools/sr_variants.py "$@" || exit $?
