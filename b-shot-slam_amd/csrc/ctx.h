@@ -119,7 +119,7 @@ struct bshot_ctx {
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
     int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)
-    bool side_shared = false;   // side stream from the process-wide CU-masked pool (never destroyed)
+    bool side_shared = false;   // side/pre/iss streams from the process-wide CU-masked pool (never destroyed)
 
     DBuf<int> errw;  // describe-stage error bits (normals)
 

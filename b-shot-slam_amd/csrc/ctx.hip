@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 
@@ -118,43 +119,58 @@ void bshot_ctx::resolve_events(bool wait) {
 
 namespace bsh {
 
-// side stream restricted to all but opt_side_reserve CUs, which stay free for the main stream.
-// CU-masked streams are created once per (device, reserve) and shared for the process lifetime:
-// destroying one was seen to hang intermittently (ROCm 7.2), so they are never destroyed.
-int ctx_make_side_stream(bshot_ctx* c) {
-    if (c->side && !c->side_shared) {
-        (void)hipStreamSynchronize(c->side);
-        (void)hipStreamDestroy(c->side);
+// The three low-priority streams (side: lookahead describe, pre: queued grids + SR, iss) are
+// restricted to all but opt_side_reserve CUs, which stay free for the main stream's short
+// latency-critical kernels (match, RANSAC, ICP). The reserved CUs are i = 33 m mod ncu,
+// m < reserve: that covers every residue mod 8 and every block of 32, so every XCD keeps some
+// whichever way the CU mask is numbered. CU-masked streams are created once per (device, reserve,
+// role) and shared for the process lifetime: destroying one was seen to hang intermittently
+// (ROCm 7.2), so they are never destroyed.
+static hipStream_t masked_stream(int device, int ncu, int reserve, int role) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int>, hipStream_t> pool;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = pool.find({device, reserve, role});
+    if (it != pool.end()) return it->second;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
+    for (int m = 0; m < reserve; ++m) {
+        const int i = (33 * m) % ncu;
+        mask[i / 32] &= ~(1u << (i % 32));
     }
-    c->side = nullptr;
+    hipStream_t st = nullptr;
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+    pool[{device, reserve, role}] = st;
+    return st;
+}
+
+int ctx_make_side_stream(bshot_ctx* c) {
+    hipStream_t* sts[3] = {&c->side, &c->pre, &c->iss};
+    for (hipStream_t* p : sts) {
+        if (*p && !c->side_shared) {
+            (void)hipStreamSynchronize(*p);
+            (void)hipStreamDestroy(*p);
+        }
+        *p = nullptr;
+    }
     c->side_shared = false;
     hipDeviceProp_t prop;
     int ncu = 0;
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) ncu = prop.multiProcessorCount;
-    const int keep = ncu - c->opt_side_reserve;
-    if (c->opt_side_reserve > 0 && ncu > 0 && keep >= 8) {
-        static std::mutex mu;
-        static std::map<std::pair<int, int>, hipStream_t> pool;
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = pool.find({c->device, c->opt_side_reserve});
-        if (it != pool.end()) {
-            c->side = it->second;
+    if (c->opt_side_reserve > 0 && ncu > 0 && ncu - c->opt_side_reserve >= 8) {
+        bool ok = true;
+        for (int r = 0; r < 3; ++r) ok = ok && (*sts[r] = masked_stream(c->device, ncu, c->opt_side_reserve, r)) != nullptr;
+        if (ok) {
             c->side_shared = true;
             return BSHOT_OK;
         }
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < keep; ++i) mask[i / 32] |= 1u << (i % 32);
-        hipStream_t st = nullptr;
-        if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
-            pool[{c->device, c->opt_side_reserve}] = st;
-            c->side = st;
-            c->side_shared = true;
-            return BSHOT_OK;
-        }
+        for (hipStream_t* p : sts) *p = nullptr;
     }
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
-    return hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo_prio) == hipSuccess ? BSHOT_OK : BSHOT_EHIP;
+    for (hipStream_t* p : sts)
+        if (hipStreamCreateWithPriority(p, hipStreamNonBlocking, lo_prio) != hipSuccess) return BSHOT_EHIP;
+    return BSHOT_OK;
 }
 
 static hipError_t ensure_events(CloudState& s) {
@@ -639,8 +655,6 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
     if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->iss, hipStreamNonBlocking, lo_prio) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->pre, hipStreamNonBlocking, lo_prio) != hipSuccess ||
         bsh::ctx_make_side_stream(c) != BSHOT_OK) {
         delete c;
         return BSHOT_EHIP;
@@ -684,9 +698,11 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
-    if (!c->side_shared) (void)hipStreamDestroy(c->side);
-    (void)hipStreamDestroy(c->iss);
-    (void)hipStreamDestroy(c->pre);
+    if (!c->side_shared) {
+        (void)hipStreamDestroy(c->side);
+        (void)hipStreamDestroy(c->iss);
+        (void)hipStreamDestroy(c->pre);
+    }
     delete c;
 }
 

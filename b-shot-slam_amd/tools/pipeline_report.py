@@ -35,3 +35,28 @@ for fi in range(max(0, len(frames) - 1 - nshow), len(frames) - 1):
             a = span.get(st, (s, e))
             span[st] = (min(a[0], s), max(a[1], e))
     print("   spans:", " ".join(f"s{st}:[{(a - t0) / 1e6:.2f},{(b - t0) / 1e6:.2f}]" for st, (a, b) in sorted(span.items())))
+
+# whole-run summary: union of kernel intervals (any stream busy) vs wall time between the first
+# and the last frame mark, and the busy time per stream
+if len(starts) >= 2:
+    t0, t1 = starts[0], starts[-1]
+    iv = sorted((max(s, t0), min(e, t1)) for s, e, _, _ in ker if e > t0 and s < t1)
+    union, cur_s, cur_e = 0, None, None
+    for s, e in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                union += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        union += cur_e - cur_s
+    per = defaultdict(float)
+    for s, e, st, nm in ker:
+        a, b = max(s, t0), min(e, t1)
+        if b > a:
+            per[st] += (b - a) / 1e6
+    nf = len(starts) - 1
+    print(f"=== {nf} frames, {(t1 - t0) / 1e6 / nf:.3f} ms/frame; GPU busy (any stream) {union / 1e6 / nf:.3f} ms/frame "
+          f"({union / (t1 - t0):.1%}); per stream ms/frame: " +
+          " ".join(f"s{st}:{v / nf:.3f}" for st, v in sorted(per.items())))
