@@ -15,8 +15,9 @@ LIB_PATH = os.environ.get("BSHOT_LIB") or os.path.join(HERE, "lib", "libbshot_am
 SYNTH_PATH = os.path.join(HERE, "lib", "libbshot_synth.so")
 P = ctypes.c_void_p
 
-NSTAGES = 10
-STAGE_NAMES = ["grid", "seg_ratio", "iss", "normals", "shot_gather", "shot_sort", "lrf", "shot_hist", "match", "icp"]
+NSTAGES = 11
+STAGE_NAMES = ["grid", "seg_ratio", "iss", "normals", "shot_gather", "shot_sort", "lrf", "shot_hist", "match", "icp",
+               "ransac"]
 
 
 class Params(ctypes.Structure):
@@ -53,13 +54,14 @@ class FrameStats(ctypes.Structure):
 ABI_SYMBOLS = [
     "bshot_default_params", "bshot_create", "bshot_destroy", "bshot_last_error", "bshot_sync", "bshot_stream",
     "bshot_set_cloud", "bshot_set_cloud_device", "bshot_seg_ratio", "bshot_select_topk", "bshot_iss",
-    "bshot_describe", "bshot_get_normals", "bshot_match", "bshot_ransac", "bshot_icp", "bshot_odom_create",
+    "bshot_describe", "bshot_get_normals", "bshot_match", "bshot_ransac", "bshot_ransac_dev", "bshot_icp", "bshot_odom_create",
     "bshot_odom_destroy", "bshot_odom_last_error", "bshot_odom_process", "bshot_odom_process_device",
     "bshot_odom_get_keypoints", "bshot_odom_get_ratios", "bshot_odom_get_bits", "bshot_odom_get_target",
     "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
     "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
     "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
+    "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
     "bshot_odom_set_option", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
 ]
@@ -206,6 +208,21 @@ class Context:
         self._chk(self.L.bshot_icp(self.h, _ptr(src), len(src), _ptr(tgt), len(tgt), max_iter, _ptr(T),
                                    ctypes.byref(it)), "icp")
         return T.reshape(4, 4), it.value
+
+    def ransac(self, src, tgt, cq, cm, max_iter=2000, thresh=1500.0):
+        """A10 with every hypothesis scored on the GPU (bshot_ransac_dev); same result as ransac()."""
+        src = _f32(src).reshape(-1, 3)
+        tgt = _f32(tgt).reshape(-1, 3)
+        cq = np.ascontiguousarray(cq, np.int32)
+        cm = np.ascontiguousarray(cm, np.int32)
+        T = np.zeros(16, np.float32)
+        iq = np.zeros(max(len(cq), 1), np.int32)
+        im = np.zeros(max(len(cq), 1), np.int32)
+        ni = ctypes.c_int()
+        rc = self.L.bshot_ransac_dev(self.h, _ptr(src), len(src), _ptr(tgt), len(tgt), _ptr(cq), _ptr(cm), len(cq),
+                                     max_iter, ctypes.c_double(thresh), _ptr(T), _ptr(iq), _ptr(im), ctypes.byref(ni))
+        self._chk(rc, "ransac_dev")
+        return rc, T.reshape(4, 4), iq[: ni.value].copy(), im[: ni.value].copy()
 
     def set_timing(self, on):
         self.L.bshot_set_timing(self.h, 1 if on else 0)
@@ -413,6 +430,11 @@ class KeypointMap:
 
     def size(self):
         return self.L.bshot_map_size(self.h)
+
+    def set_query_mode(self, mode):
+        """0: visit the map's blocks when cheaper (default), 1: the reference's lookup loop."""
+        if self.L.bshot_map_set_query_mode(self.h, int(mode)) < 0:
+            raise BshotError("set_query_mode")
 
     @staticmethod
     def block_id(pos):

@@ -439,4 +439,40 @@ BM_HD void umeyama_finish(const T sigma[9], const T sm[3], const T dm[3], T out[
     out[12] = T(0); out[13] = T(0); out[14] = T(0); out[15] = T(1);
 }
 
+// Eigen::umeyama(src, dst, false) over n AoS points in precision T (host ICP/RANSAC and the GPU
+// RANSAC scorer share it): sequential sums in point order for the means and the
+// cross-covariance. The independent accumulators advance together in one loop (instruction-level
+// parallelism); each one's own order of additions is the sequential one. out: row-major 4x4.
+template <typename T>
+BM_HD void umeyama_seq(const T* src, const T* dst, int n, T out[16]) {
+    const T one_over_n = T(1) / T(n);
+    T ss[3] = {src[0], src[1], src[2]}, ds[3] = {dst[0], dst[1], dst[2]};
+    for (int i = 1; i < n; ++i) {
+        const T* a = src + 3 * i;
+        const T* b = dst + 3 * i;
+        ss[0] = ss[0] + a[0]; ss[1] = ss[1] + a[1]; ss[2] = ss[2] + a[2];
+        ds[0] = ds[0] + b[0]; ds[1] = ds[1] + b[1]; ds[2] = ds[2] + b[2];
+    }
+    T sm[3], dm[3];
+    for (int d = 0; d < 3; ++d) {
+        sm[d] = ss[d] * one_over_n;
+        dm[d] = ds[d] * one_over_n;
+    }
+    T acc[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = (dst[r] - dm[r]) * (src[c] - sm[c]);
+    for (int i = 1; i < n; ++i) {
+        const T* a = src + 3 * i;
+        const T* b = dst + 3 * i;
+        const T s0 = a[0] - sm[0], s1 = a[1] - sm[1], s2 = a[2] - sm[2];
+        const T d0 = b[0] - dm[0], d1 = b[1] - dm[1], d2 = b[2] - dm[2];
+        acc[0] = acc[0] + d0 * s0; acc[1] = acc[1] + d0 * s1; acc[2] = acc[2] + d0 * s2;
+        acc[3] = acc[3] + d1 * s0; acc[4] = acc[4] + d1 * s1; acc[5] = acc[5] + d1 * s2;
+        acc[6] = acc[6] + d2 * s0; acc[7] = acc[7] + d2 * s1; acc[8] = acc[8] + d2 * s2;
+    }
+    T sigma[9];
+    for (int r = 0; r < 9; ++r) sigma[r] = acc[r] * one_over_n;
+    umeyama_finish<T>(sigma, sm, dm, out);
+}
+
 }  // namespace bm

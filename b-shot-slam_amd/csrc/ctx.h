@@ -161,10 +161,17 @@ struct bshot_ctx {
     // icp
     DBuf<bsh::IcpState> istate;
     PinBuf<bsh::IcpState> p_istate;
+    int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
     int opt_icp_dev = 0;  // 1: ICP loop resident on the device (one sync); 0: host Umeyama per iteration (faster under load)
     DBuf<float> isrc, itgt3;
     DBuf<float4> itgt;
     DBuf<unsigned long long> ibest;
+
+    // RANSAC scoring (bshot_ransac_dev): correspondence points, hypotheses, scores
+    DBuf<float> rpts;
+    DBuf<int> rhyp, rcnt;
+    PinBuf<float> p_rpts;
+    PinBuf<int> p_rhyp, p_rcnt;
 
     // generic gather
     DBuf<int> gidx;

@@ -694,6 +694,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->ma.release(); c->lbest.release(); c->left.release();
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
+    c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
     c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
@@ -760,7 +761,7 @@ int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
     CloudState& s = c->cs;
     HIPCHK(hipEventSynchronize(s.ev_sr), "sync ratio");
     c->resolve_events();
-    if (s.h_err.p[0]) return c->fail("seg_ratio: neighbourhood with > 1024 exactly tied boundary keys", BSHOT_ECAP);
+    if (s.h_err.p[0]) return c->fail("seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)", BSHOT_ECAP);
     const int n = s.n;
     const float* h = s.h_ratio.p;
     int m = 0;
@@ -825,7 +826,7 @@ int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf
         }
         HIPCHK(hipStreamSynchronize(c->stream), "sync describe");
     }
-    if (herr & 2) return c->fail("normals: neighbourhood with > 1024 exactly tied boundary keys", BSHOT_ECAP);
+    if (herr & 2) return c->fail("normals: neighbourhood with too many exactly tied boundary keys (kNN list overflow)", BSHOT_ECAP);
     return BSHOT_OK;
 }
 
@@ -948,6 +949,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
+    else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

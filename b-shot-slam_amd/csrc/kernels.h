@@ -74,4 +74,8 @@ struct Describe2Args {
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 
+// A10 RANSAC: score (inlier count) of every hypothesis (csrc/ransac.hip)
+hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,
+                               int* cnt, hipStream_t s);
+
 }  // namespace bsh

@@ -1,0 +1,72 @@
+// ransac.hip -- A10 on gfx950: scores of every RANSAC hypothesis in one launch (SURVEY.md §8f
+// rank 2). The reference's RandomSampleConsensus (src/lidar_odometry.cpp:251-261, PCL
+// CorrespondenceRejectorSampleConsensus) draws its 3-point samples from a stream that does not
+// depend on model scores, so the host draws them all first (host/ransac.cpp, mt19937(12345) >> 1,
+// partial Fisher-Yates, isSampleGood), this kernel scores them all at once, and the host replays
+// PCL's best-model / adaptive-k scan over the scores. Same arithmetic as the host scorer: double
+// umeyama over the 3 sample pairs (bm::umeyama_seq) rounded to float, pcl::transformPointCloud's
+// float expression, Vector4f squaredNorm's SSE order, (double)d2 < thresh^2.
+#include <hip/hip_runtime.h>
+
+#include "bshot_math.h"
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace bsk {
+
+#define RS_WAVES 4
+
+// wave per hypothesis. cs/ct: correspondence source/target points (3 floats each, correspondence
+// order); hyp: 3 correspondence positions per hypothesis
+__global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score(const float* __restrict__ cs,
+                                                                const float* __restrict__ ct, int nidx,
+                                                                const int* __restrict__ hyp, int nhyp, double thr2,
+                                                                int* __restrict__ cnt) {
+    __builtin_amdgcn_s_setprio(3);  // main-stream kernel on the odometry chain's critical path
+    const int h = blockIdx.x * RS_WAVES + (threadIdx.x >> 6);
+    const int lane = lane_id();
+    if (h >= nhyp) return;
+    double sd[9], td[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int p = hyp[3 * h + i];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            sd[3 * i + d] = (double)cs[3 * p + d];
+            td[3 * i + d] = (double)ct[3 * p + d];
+        }
+    }
+    // every lane computes the (uniform) model: no divergence, no broadcast
+    double md[16];
+    bm::umeyama_seq<double>(sd, td, 3, md);
+    float T[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) T[i] = (float)md[i];
+    int c = 0;
+    for (int i = lane; i < nidx; i += 64) {
+        const float x = cs[3 * i], y = cs[3 * i + 1], z = cs[3 * i + 2];
+        const float px = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
+        const float py = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
+        const float pz = ((T[8] * x + T[9] * y) + T[10] * z) + T[11];
+        const float dx = px - ct[3 * i], dy = py - ct[3 * i + 1], dz = pz - ct[3 * i + 2];
+        const float d2 = (dx * dx + dz * dz) + (dy * dy + 0.0f);
+        c += (double)d2 < thr2 ? 1 : 0;
+    }
+    // integer sum: order-free
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) cnt[h] = c;
+}
+
+}  // namespace bsk
+
+namespace bsh {
+
+hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,
+                               int* cnt, hipStream_t s) {
+    if (nhyp <= 0) return hipSuccess;
+    bsk::k_ransac_score<<<(nhyp + RS_WAVES - 1) / RS_WAVES, 64 * RS_WAVES, 0, s>>>(cs, ct, nidx, hyp, nhyp, thr2, cnt);
+    return hipGetLastError();
+}
+
+}  // namespace bsh

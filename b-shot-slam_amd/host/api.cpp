@@ -1,4 +1,5 @@
 // api.cpp -- Frame (src/frame.cpp), Keypoint (src/keypoint.cpp), Map (src/mymap.cpp) of the C++ API.
+#include <algorithm>
 #include <bitset>
 #include <cmath>
 
@@ -114,27 +115,62 @@ void Map::getKeypoints(Vector3f pos, float range, PointCloudXYZ& kpts_pos, std::
     const int y_max = (int)std::round((pos[1] + range) / (float)prec) * prec;
     const int z_min = (int)std::round((pos[2] - range) / (float)prec) * prec;
     const int z_max = (int)std::round((pos[2] + range) / (float)prec) * prec;
+    auto append = [&](BlockMap::iterator it) {
+        BlockAux& ax = aux_[it->first];
+        if (ax.dirty) {
+            // the block's iteration order, as the reference loop visits it
+            ax.pos.clear();
+            ax.desc.clear();
+            ax.pos.reserve(it->second.size());
+            ax.desc.reserve(it->second.size());
+            for (auto& kp : it->second) {
+                ax.pos.push_back(kp.first);
+                ax.desc.push_back(kp.second->getDescriptor());
+            }
+            ax.dirty = false;
+        }
+        kpts_pos.insert(kpts_pos.end(), ax.pos.begin(), ax.pos.end());
+        descriptors.insert(descriptors.end(), ax.desc.begin(), ax.desc.end());
+    };
+    if (x_max < x_min || y_max < y_min || z_max < z_min) return;
+    const long long nx = (x_max - x_min) / prec + 1, ny = (y_max - y_min) / prec + 1, nz = (z_max - z_min) / prec + 1;
+    const long long M = 0x1FFFFF, span = M + 1;
+    if (query_mode_ == 0 && (long long)keypoints_.size() < nx * ny * nz && nx * prec < span && ny * prec < span &&
+        nz * prec < span) {
+        // Same blocks in the same order as the reference's x/y/z loop of lookups
+        // (src/mymap.cpp:28-74), found by visiting the map's blocks instead: a loop position's
+        // block id holds the low 21 bits of each coordinate (getBlockID), and with the box
+        // narrower than 2^21 mm per axis at most one loop position has a block's 21-bit residues.
+        auto slot = [&](long long r, int lo, long long cnt) -> long long {
+            const long long d = (r - ((long long)lo & M)) & M;  // i * prec == d, both < 2^21
+            if (d % prec) return -1;
+            const long long i = d / prec;
+            return i < cnt ? i : -1;
+        };
+        std::vector<std::pair<long long, BlockMap::iterator>> hits;
+        for (auto it = keypoints_.begin(); it != keypoints_.end(); ++it) {
+            const unsigned long long id = it->first;
+            const long long i = slot((long long)((id >> 42) & M), x_min, nx);
+            if (i < 0) continue;
+            const long long j = slot((long long)((id >> 21) & M), y_min, ny);
+            if (j < 0) continue;
+            const long long k = slot((long long)(id & M), z_min, nz);
+            if (k < 0) continue;
+            hits.emplace_back((i * ny + j) * nz + k, it);
+        }
+        std::sort(hits.begin(), hits.end(),
+                  [](const std::pair<long long, BlockMap::iterator>& a,
+                     const std::pair<long long, BlockMap::iterator>& b) { return a.first < b.first; });
+        for (auto& h : hits) append(h.second);
+        return;
+    }
     for (int x = x_min; x <= x_max; x += prec)
         for (int y = y_min; y <= y_max; y += prec)
             for (int z = z_min; z <= z_max; z += prec) {
                 const unsigned long id = getBlockID(Vector3f((float)x, (float)y, (float)z));
                 auto it = keypoints_.find(id);
                 if (it == keypoints_.end()) continue;
-                BlockAux& ax = aux_[id];
-                if (ax.dirty) {
-                    // the block's iteration order, as the reference loop visits it
-                    ax.pos.clear();
-                    ax.desc.clear();
-                    ax.pos.reserve(it->second.size());
-                    ax.desc.reserve(it->second.size());
-                    for (auto& kp : it->second) {
-                        ax.pos.push_back(kp.first);
-                        ax.desc.push_back(kp.second->getDescriptor());
-                    }
-                    ax.dirty = false;
-                }
-                kpts_pos.insert(kpts_pos.end(), ax.pos.begin(), ax.pos.end());
-                descriptors.insert(descriptors.end(), ax.desc.begin(), ax.desc.end());
+                append(it);
             }
 }
 
@@ -206,6 +242,12 @@ int bshot_map_query(bshot_map* m, const float* pos, float range, float* xyz, uin
 }
 
 int bshot_map_size(bshot_map* m) { return m ? m->m.size() : 0; }
+
+int bshot_map_set_query_mode(bshot_map* m, int mode) {
+    if (!m || mode < 0 || mode > 1) return BSHOT_EINVAL;
+    m->m.setQueryMode(mode);
+    return BSHOT_OK;
+}
 
 uint64_t bshot_map_block_id(const float* pos) {
     myslam::Map tmp;

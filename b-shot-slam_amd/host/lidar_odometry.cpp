@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
+#include <mutex>
 #include <thread>
 
 #include "../csrc/ctx.h"
@@ -29,6 +30,13 @@ struct LidarOdometry::Lookahead {
     PointCloudXYZ kps, iss;
     std::vector<uint32_t> words;
     float ms[3] = {0.f, 0.f, 0.f};  // extract, iss, describe (worker-thread wall time)
+    // the sweep after next (queueFrameDevice): its grids/SR/ISS launches are issued by the worker
+    // once its own describe is queued, off the main thread; whichever thread comes second issues them
+    std::mutex qmu;
+    const float* q_xyz = nullptr;
+    int q_n = 0;
+    bool q_pending = false, q_worker_passed = false;
+    int q_rc = BSHOT_OK;
 };
 
 LidarOdometry::LidarOdometry()
@@ -127,6 +135,17 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
 }
 
 void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
+    if (ahead_) {
+        std::lock_guard<std::mutex> lk(ahead_->qmu);
+        if (!ahead_->q_worker_passed) {
+            // the worker issues the launches after queueing its describe (runAhead)
+            ahead_->q_xyz = d_xyz;
+            ahead_->q_n = n;
+            ahead_->q_pending = true;
+            ctx_->hmark("M_queued");
+            return;
+        }
+    }
     check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
     ctx_->hmark("M_queued");
 }
@@ -142,7 +161,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
     c->hmark("W_start");
     if (hipEventSynchronize(S.ev_sr) != hipSuccess) fail("lookahead sr");
     c->hmark("W_sr_ready");
-    if (S.h_err.p[0]) throw std::runtime_error("seg_ratio: neighbourhood with > 1024 exactly tied boundary keys");
+    if (S.h_err.p[0]) throw std::runtime_error("seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)");
     const int n = S.n;
     std::vector<int32_t> idx(n > 0 ? n : 1);
     std::vector<float> ratio(n > 0 ? n : 1);
@@ -171,6 +190,16 @@ void LidarOdometry::runAhead(Lookahead& la) {
     c->hmark("W_topk_done");
     if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
     c->hmark("W_describe_queued");
+    {
+        // the sweep after next, if the main thread asked for it (queueFrameDevice)
+        std::lock_guard<std::mutex> lk(la.qmu);
+        la.q_worker_passed = true;
+        if (la.q_pending) {
+            la.q_pending = false;
+            if (bshot_queue_cloud_device(c, la.q_xyz, la.q_n) != BSHOT_OK) fail("lookahead queue");
+            c->hmark("W_queued");
+        }
+    }
     TicToc t_iss;
     if (prm_.run_iss) {
         if (S.iss_state != 1 || hipEventSynchronize(S.ev_iss) != hipSuccess) fail("lookahead iss");
@@ -362,9 +391,16 @@ void LidarOdometry::featureMatching() {
     std::vector<int32_t> iq(nc > 0 ? nc : 1), im(nc > 0 ? nc : 1);
     int ni = 0;
     float T[16];
-    check(bshot_ransac(na ? &cloud1_kps_[0][0] : nullptr, na, nb ? &cloud2_kps_[0][0] : nullptr, nb, cq.data(),
-                       cm.data(), nc, prm_.ransac_max_iter, prm_.ransac_thresh, T, iq.data(), im.data(), &ni),
-          "ransac");
+    const float* s1 = na ? &cloud1_kps_[0][0] : nullptr;
+    const float* s2 = nb ? &cloud2_kps_[0][0] : nullptr;
+    if (ctx_->opt_ransac_dev)
+        check(bshot_ransac_dev(ctx_, s1, na, s2, nb, cq.data(), cm.data(), nc, prm_.ransac_max_iter,
+                               prm_.ransac_thresh, T, iq.data(), im.data(), &ni),
+              "ransac");
+    else
+        check(bshot_ransac(s1, na, s2, nb, cq.data(), cm.data(), nc, prm_.ransac_max_iter, prm_.ransac_thresh, T,
+                           iq.data(), im.data(), &ni),
+              "ransac");
     std::memcpy(T_ransac_.m, T, sizeof(T));
     ctx_->hmark("M_ransac");
     corr_.resize(ni);

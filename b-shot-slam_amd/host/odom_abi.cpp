@@ -14,7 +14,12 @@
 struct bshot_odom {
     std::unique_ptr<myslam::LidarOdometry> lo;
     std::string err;
-    std::vector<float> delta;  // last frame's map delta, 15 floats per keypoint
+    std::vector<float> delta;  // last frame's map delta, 15 floats per keypoint (built on request)
+    bool delta_ready = true;
+    myslam::Matrix4f d_pose;                     // what bshot_odom_map_delta builds it from
+    myslam::Frame::PCPtr d_kps;
+    myslam::Frame::DCPPtr d_ds;
+    std::vector<float> d_ratios;
     std::vector<myslam::Map> replicas;
     const float* next_d = nullptr;  // lookahead cloud (bshot_odom_set_next_device)
     int next_n = 0;
@@ -56,30 +61,38 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     lo.updateMap();
     lo.updateCorrespondence();
     if (st) *st = lo.lastStats();
-    // map delta: the K keypoint records this frame offered to Map::addKeypoint
-    const myslam::Matrix4f P = f->getPose();
-    const myslam::Matrix3f R = P.block33();
-    const myslam::Vector3f T = P.topRightCorner();
-    auto kps = f->getKeypoints();
-    auto ds = f->getDescriptors();
-    const auto& ratios = lo.segRatios();
-    const size_t k = kps ? kps->size() : 0;
+    // map delta inputs (the records are built only when bshot_odom_map_delta asks for them)
+    o->d_pose = f->getPose();
+    o->d_kps = f->getKeypoints();
+    o->d_ds = f->getDescriptors();
+    o->d_ratios = lo.segRatios();
+    o->delta_ready = false;
+    return BSHOT_OK;
+}
+
+// the K keypoint records the last frame offered to Map::addKeypoint: world position on the
+// 10 mm keypoint grid, ratio, descriptor words
+void build_delta(bshot_odom* o) {
+    if (o->delta_ready) return;
+    const myslam::Matrix3f R = o->d_pose.block33();
+    const myslam::Vector3f T = o->d_pose.topRightCorner();
+    const size_t k = o->d_kps ? o->d_kps->size() : 0;
     o->delta.assign(k * kRec, 0.f);
     for (size_t i = 0; i < k; ++i) {
-        myslam::Vector3f w = R * kps->at(i) + T;
+        myslam::Vector3f w = R * o->d_kps->at(i) + T;
         bshot_descriptor d;
-        d.bits = ds->at(i);
-        auto kp = myslam::Keypoint::createKeypoint(w, ratios[i], d);
+        d.bits = o->d_ds->at(i);
+        auto kp = myslam::Keypoint::createKeypoint(w, o->d_ratios[i], d);
         float* r = &o->delta[i * kRec];
         r[0] = kp->getPosition()[0];
         r[1] = kp->getPosition()[1];
         r[2] = kp->getPosition()[2];
-        r[3] = ratios[i];
+        r[3] = o->d_ratios[i];
         uint32_t words[11];
         myslam::bits_to_words(d.bits, words);
         std::memcpy(r + 4, words, sizeof(words));
     }
-    return BSHOT_OK;
+    o->delta_ready = true;
 }
 
 }  // namespace
@@ -200,6 +213,8 @@ int bshot_odom_get_iss(bshot_odom* o, float* xyz, int cap) {
 bshot_ctx* bshot_odom_ctx(bshot_odom* o) { return o ? o->lo->context() : nullptr; }
 
 int bshot_odom_map_delta(bshot_odom* o, float* rec, int cap) {
+    if (!o) return BSHOT_EINVAL;
+    build_delta(o);
     const int n = (int)(o->delta.size() / kRec);
     if (n > cap) return -n;
     if (n) std::memcpy(rec, o->delta.data(), sizeof(float) * kRec * n);

@@ -5,19 +5,20 @@
 // Structure: the hypothesis stream does not depend on model scores (draws happen only in
 // getSamples: mt19937(12345) >> 1, partial Fisher-Yates on the persistent shuffled index vector,
 // isSampleGood redraws), so phase 1 generates every sample triplet up front and phase 2 scans the
-// hypotheses in order applying PCL's best-model / adaptive-k / max-iteration rules. Phase 2's
-// scoring is independent per hypothesis (the batched-GPU evaluation of SURVEY.md §8f rank 2 slots in
-// here).
+// hypotheses in order applying PCL's best-model / adaptive-k / max-iteration rules. The scores
+// phase 2 reads come either from the host (bshot_ransac: each hypothesis scored when the scan
+// reaches it) or from one GPU launch that scores them all (bshot_ransac_dev, csrc/ransac.hip;
+// SURVEY.md §8f rank 2). Both compute the same integers, so both give the same result.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <limits>
 #include <random>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/bshot_abi.h"
+#include "../csrc/ctx.h"
 #include "geom.h"
 
 namespace {
@@ -46,11 +47,10 @@ double sample_threshold(const Pt* src, const std::vector<int>& ind) {
     return t * t;
 }
 
-}  // namespace
-
-extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, int nt, const int32_t* corr_q,
-                            const int32_t* corr_m, int n_corr, int max_iter, double thresh, float* T_out,
-                            int32_t* inl_q, int32_t* inl_m, int* n_inl) {
+// ctx == nullptr: host scoring; else the GPU scores every hypothesis in one launch on ctx->stream
+int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_xyz, int nt, const int32_t* corr_q,
+                const int32_t* corr_m, int n_corr, int max_iter, double thresh, float* T_out, int32_t* inl_q,
+                int32_t* inl_m, int* n_inl) {
     if (!T_out || !n_inl || n_corr < 0 || ns < 0 || nt < 0) return BSHOT_EINVAL;
     const Pt* src = reinterpret_cast<const Pt*>(src_xyz);
     const Pt* tgt = reinterpret_cast<const Pt*>(tgt_xyz);
@@ -63,24 +63,31 @@ extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, 
     };
     std::vector<int> indices(corr_q, corr_q + n_corr);
     if ((int)indices.size() > ns) indices.clear();  // SampleConsensusModel ctor index check
-    std::unordered_map<int, int> tgt_of;
-    tgt_of.reserve(n_corr * 2 + 1);
+    // source index -> target index (the last correspondence of a source index wins, as PCL's map)
+    for (int i = 0; i < n_corr; ++i)
+        if (corr_q[i] < 0 || corr_q[i] >= ns || corr_m[i] < 0 || corr_m[i] >= nt) return BSHOT_EINVAL;
+    std::vector<int> tgt_of(ns > 0 ? ns : 1, -1);
     for (int i = 0; i < n_corr; ++i) tgt_of[corr_q[i]] = corr_m[i];
     const int nidx = (int)indices.size();
     if (nidx < 3) return fallback();
     const double sample_thresh = sample_threshold(src, indices);
 
-    // ---- phase 1: the hypothesis stream (getSamples for iterations 0..max_iter)
+    // ---- phase 1: the hypothesis stream (getSamples for iterations 0..max_iter). `pos` follows
+    // the shuffle of index values with their positions in `indices` (what the GPU scorer reads).
     std::mt19937 rng(12345u);
-    std::vector<int> shuffled = indices;
-    std::vector<int> samples;
+    std::vector<int> shuffled = indices, pos(nidx);
+    for (int i = 0; i < nidx; ++i) pos[i] = i;
+    std::vector<int> samples, spos;
     samples.reserve(3 * (size_t)(max_iter + 1));
+    spos.reserve(3 * (size_t)(max_iter + 1));
     for (int it = 0; it <= max_iter; ++it) {
         bool got = false;
         for (unsigned chk = 0; chk < 1000 && !got; ++chk) {
             for (int i = 0; i < 3; ++i) {
                 const unsigned r = rng() >> 1;
-                std::swap(shuffled[i], shuffled[i + (int)(r % (unsigned)(nidx - i))]);
+                const int j = i + (int)(r % (unsigned)(nidx - i));
+                std::swap(shuffled[i], shuffled[j]);
+                std::swap(pos[i], pos[j]);
             }
             const Pt &a = src[shuffled[0]], &b = src[shuffled[1]], &c = src[shuffled[2]];
             const float p10x = b.x - a.x, p10y = b.y - a.y, p10z = b.z - a.z;
@@ -91,9 +98,10 @@ extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, 
                   (double)((p21x * p21x + p21y * p21y) + p21z * p21z) > sample_thresh;
         }
         if (!got) break;
-        samples.push_back(shuffled[0]);
-        samples.push_back(shuffled[1]);
-        samples.push_back(shuffled[2]);
+        for (int i = 0; i < 3; ++i) {
+            samples.push_back(shuffled[i]);
+            spos.push_back(pos[i]);
+        }
     }
     const int nhyp = (int)samples.size() / 3;
 
@@ -123,6 +131,29 @@ extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, 
         return bg::umeyama<double>(sd, td, 3);
     };
 
+    // ---- GPU scores of every hypothesis (sample positions index cs/ct)
+    const int* gcnt = nullptr;
+    if (ctx && nhyp > 0) {
+        bshot_ctx* c = ctx;
+        const size_t np = 6 * (size_t)nidx;
+        if (c->rpts.ensure(np) || c->rhyp.ensure(3 * (size_t)nhyp) || c->rcnt.ensure(nhyp) || c->p_rpts.ensure(np) ||
+            c->p_rhyp.ensure(3 * (size_t)nhyp) || c->p_rcnt.ensure(nhyp))
+            return c->fail("ransac: alloc", BSHOT_EHIP);
+        std::memcpy(c->p_rpts.p, cs.data(), sizeof(float) * 3 * nidx);
+        std::memcpy(c->p_rpts.p + 3 * nidx, ct.data(), sizeof(float) * 3 * nidx);
+        std::memcpy(c->p_rhyp.p, spos.data(), sizeof(int) * 3 * nhyp);
+        const int sg = c->stage_begin(BSHOT_STAGE_RANSAC);
+        if (hipMemcpyAsync(c->rpts.p, c->p_rpts.p, sizeof(float) * np, hipMemcpyHostToDevice, c->stream) ||
+            hipMemcpyAsync(c->rhyp.p, c->p_rhyp.p, sizeof(int) * 3 * nhyp, hipMemcpyHostToDevice, c->stream) ||
+            bsh::launch_ransac_score(c->rpts.p, c->rpts.p + 3 * nidx, nidx, c->rhyp.p, nhyp, thr2, c->rcnt.p,
+                                     c->stream) ||
+            hipMemcpyAsync(c->p_rcnt.p, c->rcnt.p, sizeof(int) * nhyp, hipMemcpyDeviceToHost, c->stream))
+            return c->fail("ransac: launch", BSHOT_EHIP);
+        c->stage_end(sg);
+        if (hipStreamSynchronize(c->stream)) return c->fail("ransac: sync", BSHOT_EHIP);
+        gcnt = c->p_rcnt.p;
+    }
+
     // ---- phase 2: RandomSampleConsensus::computeModel acceptance scan
     const double log_prob = std::log(1.0 - 0.99);
     const double one_over_indices = 1.0 / (double)nidx;
@@ -131,8 +162,15 @@ extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, 
     bg::Mat4f best_T = bg::Mat4f::identity();
     bool have = false;
     for (int it = 0; it < nhyp && (double)it < k; ++it) {
-        const bg::Mat4f T = model_of(it);
-        const int cnt = count_within(T, nullptr);
+        int cnt;
+        bg::Mat4f T;
+        if (gcnt) {
+            cnt = gcnt[it];
+            if (cnt > best_cnt) T = model_of(it);
+        } else {
+            T = model_of(it);
+            cnt = count_within(T, nullptr);
+        }
         if (cnt > best_cnt) {
             best_cnt = cnt;
             best_T = T;
@@ -149,7 +187,7 @@ extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, 
     std::vector<int> inl;
     count_within(best_T, &inl);
     if (inl.size() < 3) return fallback();
-    std::unordered_map<int, int> pos_of;
+    std::vector<int> pos_of(ns > 0 ? ns : 1, -1);
     for (int i = 0; i < n_corr; ++i) pos_of[corr_q[i]] = i;
     for (size_t i = 0; i < inl.size(); ++i) {
         const int p = pos_of[inl[i]];
@@ -159,4 +197,24 @@ extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, 
     *n_inl = (int)inl.size();
     std::memcpy(T_out, best_T.m, sizeof(best_T.m));
     return 1;
+}
+
+}  // namespace
+
+extern "C" int bshot_ransac(const float* src_xyz, int ns, const float* tgt_xyz, int nt, const int32_t* corr_q,
+                            const int32_t* corr_m, int n_corr, int max_iter, double thresh, float* T_out,
+                            int32_t* inl_q, int32_t* inl_m, int* n_inl) {
+    return ransac_impl(nullptr, src_xyz, ns, tgt_xyz, nt, corr_q, corr_m, n_corr, max_iter, thresh, T_out, inl_q,
+                       inl_m, n_inl);
+}
+
+extern "C" int bshot_ransac_dev(bshot_ctx* c, const float* src_xyz, int ns, const float* tgt_xyz, int nt,
+                                const int32_t* corr_q, const int32_t* corr_m, int n_corr, int max_iter,
+                                double thresh, float* T_out, int32_t* inl_q, int32_t* inl_m, int* n_inl) {
+    if (!c) return BSHOT_EINVAL;
+    (void)hipSetDevice(c->device);
+    const int rc = ransac_impl(c, src_xyz, ns, tgt_xyz, nt, corr_q, corr_m, n_corr, max_iter, thresh, T_out, inl_q,
+                               inl_m, n_inl);
+    c->resolve_events();
+    return rc;
 }

@@ -33,10 +33,14 @@ class Map {
     void getBlockKeypoints(std::vector<KPointCloud>& kpc);
     unsigned long getBlockID(Vector3f pos);
     int size();
+    // getKeypoints strategy (same output either way): 0 visits the map's blocks when that is
+    // cheaper than the reference's 21^3 lookups, 1 always runs the lookup loop (tests)
+    void setQueryMode(int mode) { query_mode_ = mode; }
 
   private:
     BlockMap keypoints_;
     int prec = 10000;  // map grid (mm)
+    int query_mode_ = 0;
 
     // acceleration only (contents and iteration order of keypoints_ are untouched): per block, its
     // keypoints bucketed in 1 m cells for the 800 mm suppression test of addKeypoint, and a flat

@@ -102,6 +102,11 @@ int bshot_match(bshot_ctx* c, const uint32_t* a, int na, const uint32_t* b, int 
  *      Returns 1 when a model was found, 0 on PCL's identity/all-correspondences fallback. -- */
 int bshot_ransac(const float* src, int ns, const float* tgt, int nt, const int32_t* corr_q, const int32_t* corr_m,
                  int n_corr, int max_iter, double thresh, float* T_out, int32_t* inl_q, int32_t* inl_m, int* n_inl);
+/*      Same result, hypotheses scored on the GPU in one launch on the context's main stream
+ *      (csrc/ransac.hip). ----------------------------------------------- */
+int bshot_ransac_dev(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, const int32_t* corr_q,
+                     const int32_t* corr_m, int n_corr, int max_iter, double thresh, float* T_out, int32_t* inl_q,
+                     int32_t* inl_m, int* n_inl);
 
 /* ---- A11: point-to-point ICP (PCL IterativeClosestPoint defaults, src/lidar_odometry.cpp:291-297).
  *      src is already transformed by the initial guess; T_out = ICP final transformation. ---- */
@@ -162,6 +167,9 @@ int bshot_map_add(bshot_map* m, const float* xyz, float ratio, const uint32_t* b
 int bshot_map_query(bshot_map* m, const float* pos, float range, float* xyz, uint32_t* bits, int cap);
 int bshot_map_size(bshot_map* m);
 uint64_t bshot_map_block_id(const float* pos);
+/* getKeypoints strategy, same output: 0 (default) visits the map's blocks when cheaper than the
+ * reference's 21^3 block lookups, 1 always runs the reference's lookup loop */
+int bshot_map_set_query_mode(bshot_map* m, int mode);
 
 /* ---- tuning knobs (results never depend on them): "ladder_grids" 4 (default) or 2 grids for the
  *      exact-kNN radius ladder (4: seven radii r 2^(-k/2)); "describe2" 1 (default) load-balanced
@@ -183,7 +191,8 @@ enum {
     BSHOT_STAGE_HIST = 7,
     BSHOT_STAGE_MATCH = 8,
     BSHOT_STAGE_ICP = 9,
-    BSHOT_NSTAGES = 10
+    BSHOT_STAGE_RANSAC = 10,
+    BSHOT_NSTAGES = 11
 };
 int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n);
 void bshot_stage_reset(bshot_ctx* c);

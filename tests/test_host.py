@@ -138,3 +138,29 @@ def test_map_suppression_random_model():
     want = sorted((tuple(float(v) for v in k), tuple(int(v) for v in w)) for blk in blocks.values()
                   for k, (_, w) in blk.items())
     assert got == want
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_map_query_block_scan_order(seed):
+    """Map::getKeypoints visiting the map's blocks must return exactly what the reference's
+    x/y/z loop of 21^3 block lookups returns (src/mymap.cpp:28-74), in the same order -- including
+    blocks whose 21-bit id residues alias positions 2^21 mm away (block-id wraparound)."""
+    rng = np.random.default_rng(seed)
+    maps = [bshot_py.KeypointMap(), bshot_py.KeypointMap()]
+    maps[1].set_query_mode(1)
+    span = float(1 << 21)
+    for t in range(3000):
+        p = rng.uniform(-150000, 150000, 3).astype(np.float32)
+        if t % 5 == 0:
+            p[rng.integers(0, 3)] += np.float32(span * rng.choice([-1.0, 1.0]))  # aliases a near block id
+        bits = rng.integers(0, 2 ** 32, 11, dtype=np.uint64).astype(np.uint32)
+        r = float(rng.uniform(0, 1))
+        for m in maps:
+            m.add(p, r, bits)
+    for q in range(40):
+        pos = rng.uniform(-120000, 120000, 3).astype(np.float32)
+        rng_mm = float(rng.choice([100000.0, 35000.0, 5000.0]))
+        a = maps[0].query(pos, rng_mm)
+        b = maps[1].query(pos, rng_mm)
+        assert len(a[0]) == len(b[0])
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])

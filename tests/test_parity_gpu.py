@@ -112,3 +112,21 @@ def test_icp_exact(ctx, cloud, sr_ref):
     Tr, itr = orc.icp(src, tgt)
     assert it == itr
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+
+
+@pytest.mark.parametrize("seed,frac", [(1, 0.6), (2, 0.3), (3, 0.9), (4, 0.05), (6, 0.15)])
+def test_ransac_dev_matches_host(ctx, seed, frac):
+    """A10 with the hypotheses scored on the GPU (bshot_ransac_dev) == host RANSAC == oracle, bit for bit."""
+    from test_host import _corr_set
+    src, tgt, cq, cm = _corr_set(seed, inlier_frac=frac)
+    rc, T, iq, im = ctx.ransac(src, tgt, cq, cm)
+    hrc, hT, hq, hm = bshot_py.ransac(src, tgt, cq, cm)
+    orc_rc, oT, oq, om = orc.ransac(src, tgt, cq, cm)
+    assert rc == hrc == orc_rc
+    assert np.array_equal(T.view(np.uint32), hT.view(np.uint32))
+    assert np.array_equal(T.view(np.uint32), oT.view(np.uint32))
+    assert np.array_equal(iq, oq) and np.array_equal(im, om)
+    for ncorr in (0, 2, 3):
+        r2 = ctx.ransac(src, tgt, cq[:ncorr], cm[:ncorr])
+        o2 = orc.ransac(src, tgt, cq[:ncorr], cm[:ncorr])
+        assert r2[0] == o2[0] and np.array_equal(r2[1], o2[1]) and np.array_equal(r2[2], o2[2])
