@@ -30,13 +30,6 @@ struct LidarOdometry::Lookahead {
     PointCloudXYZ kps, iss;
     std::vector<uint32_t> words;
     float ms[3] = {0.f, 0.f, 0.f};  // extract, iss, describe (worker-thread wall time)
-    // the sweep after next (queueFrameDevice): its grids/SR/ISS launches are issued by the worker
-    // once its own describe is queued, off the main thread; whichever thread comes second issues them
-    std::mutex qmu;
-    const float* q_xyz = nullptr;
-    int q_n = 0;
-    bool q_pending = false, q_worker_passed = false;
-    int q_rc = BSHOT_OK;
 };
 
 LidarOdometry::LidarOdometry()
@@ -135,17 +128,8 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
 }
 
 void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
-    if (ahead_) {
-        std::lock_guard<std::mutex> lk(ahead_->qmu);
-        if (!ahead_->q_worker_passed) {
-            // the worker issues the launches after queueing its describe (runAhead)
-            ahead_->q_xyz = d_xyz;
-            ahead_->q_n = n;
-            ahead_->q_pending = true;
-            ctx_->hmark("M_queued");
-            return;
-        }
-    }
+    // on the main thread: issued from the worker (after its describe) it started the sweep after
+    // next's SR too late and slowed the describe it then overlapped (measured 260 -> 237 sweeps/s)
     check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
     ctx_->hmark("M_queued");
 }
@@ -190,16 +174,6 @@ void LidarOdometry::runAhead(Lookahead& la) {
     c->hmark("W_topk_done");
     if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
     c->hmark("W_describe_queued");
-    {
-        // the sweep after next, if the main thread asked for it (queueFrameDevice)
-        std::lock_guard<std::mutex> lk(la.qmu);
-        la.q_worker_passed = true;
-        if (la.q_pending) {
-            la.q_pending = false;
-            if (bshot_queue_cloud_device(c, la.q_xyz, la.q_n) != BSHOT_OK) fail("lookahead queue");
-            c->hmark("W_queued");
-        }
-    }
     TicToc t_iss;
     if (prm_.run_iss) {
         if (S.iss_state != 1 || hipEventSynchronize(S.ev_iss) != hipSuccess) fail("lookahead iss");
