@@ -143,7 +143,10 @@ struct bshot_ctx {
     DBuf<float4> recB;
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
-    int opt_describe2 = 1;  // tuning knob "describe2": 1 load-balanced SHOT, 0 wave/WG per keypoint
+    DBuf<unsigned int> sbh, sbst;  // bucketed gather: per-keypoint d2 histogram and bucket starts
+    // tuning knob "describe2": 2 load-balanced SHOT with the bucketed gather + in-bucket rank
+    // (default), 1 load-balanced SHOT with the piece sort, 0 wave/WG per keypoint
+    int opt_describe2 = 2;
     int ladder_mode(const CloudState& s) const { return s.fine_ladder ? (opt_ladder_front ? 2 : 1) : 0; }
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag

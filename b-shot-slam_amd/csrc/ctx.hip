@@ -397,7 +397,13 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     c->stage_end(sg4, st);
     const float R = c->prm.shot_radius;
     const int sg5 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
-    HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st), "shot count");
+    const bool bucketed = c->opt_describe2 == 2 && !force_v1;
+    if (bucketed) {
+        HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
+        HIPCHK(c->sbst.ensure(1024 * (size_t)k), "alloc bucket starts");
+    }
+    HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st, bucketed ? c->sbh.p : nullptr),
+           "shot count");
     c->stage_end(sg5, st);
     HIPCHK(c->p_offs.ensure((size_t)k + 1), "alloc pinned offs");
     HIPCHK(hipMemcpyAsync(c->p_offs.p, c->offs.p, sizeof(long long) * ((size_t)k + 1), hipMemcpyDeviceToHost,
@@ -409,7 +415,11 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
     const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
-    HIPCHK(launch_shot_gather(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, st), "shot gather");
+    if (bucketed)
+        HIPCHK(launch_shot_gather_b(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->sbh.p, c->sbst.p, c->seg.p, st),
+               "shot gather");
+    else
+        HIPCHK(launch_shot_gather(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, st), "shot gather");
     c->stage_end(sg6, st);
     if (!c->opt_describe2 || force_v1) {
         const int sg7 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
@@ -473,6 +483,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
     A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recA = c->recA.p; A.recB = c->recB.p;
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
+    A.bstart = bucketed ? c->sbst.p : nullptr;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -695,6 +706,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
     c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
+    c->sbh.release(); c->sbst.release();
     c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
@@ -943,7 +955,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     if (!c || !name) return BSHOT_EINVAL;
     const std::string k(name);
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
-    else if (k == "describe2") c->opt_describe2 = value ? 1 : 0;
+    else if (k == "describe2") c->opt_describe2 = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;

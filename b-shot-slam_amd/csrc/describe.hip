@@ -25,19 +25,40 @@
 namespace bsk {
 
 #define SB_BUCKETS 1024
+#define SG_BUCKETS 1024
 
+// d2 bucket of the bucketed gather (k_shot_count/k_shot_gather_b/k_shot_rank): monotone in d2
+__device__ __forceinline__ int sg_bucket(float d2, float sc) {
+    int b = (int)(d2 * sc);
+    return b < 0 ? 0 : (b > SG_BUCKETS - 1 ? SG_BUCKETS - 1 : b);
+}
+
+// bh (nullable): per-keypoint histogram of the in-radius d2 over SG_BUCKETS buckets, [k][SG_BUCKETS]
 __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __restrict__ kps, int k, float R,
-                                                    int* __restrict__ counts) {
+                                                    int* __restrict__ counts, unsigned int* __restrict__ bh) {
     __shared__ CandLds lds[4];
+    __shared__ unsigned int hist[4][SG_BUCKETS];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
+    const float sc = (float)SG_BUCKETS / R2;
+    unsigned int* h = hist[wave];
     for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        if (bh) {
+            for (int j = lane; j < SG_BUCKETS; j += 64) h[j] = 0u;
+            __builtin_amdgcn_wave_barrier();
+        }
         int c = 0;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))
-            for_candidates(g, &lds[wave], kx, ky, kz, R, R2,
-                           [&](bool v, float, unsigned int) { c += __popcll(__ballot(v)); });
+            for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int) {
+                c += __popcll(__ballot(v));
+                if (bh && v) atomicAdd(&h[sg_bucket(d2, sc)], 1u);
+            });
+        if (bh) {
+            __builtin_amdgcn_wave_barrier();
+            for (int j = lane; j < SG_BUCKETS; j += 64) bh[(size_t)q * SG_BUCKETS + j] = h[j];
+        }
         if (lane == 0) counts[q] = c;
     }
 }
@@ -89,6 +110,97 @@ __global__ void __launch_bounds__(256) k_shot_gather(GridView g, const float* __
             cnt += __popcll(m);
         });
     }
+}
+
+// Bucketed gather: the keys land grouped by d2 bucket (buckets ascending, any order inside a
+// bucket): each wave scans its keypoint's bucket histogram (bh, from k_shot_count) into LDS
+// cursors, writes the bucket starts (bstart, relative to the segment) for k_shot_rank, and
+// scatters every in-radius key to its bucket's next slot.
+__global__ void __launch_bounds__(256) k_shot_gather_b(GridView g, const float* __restrict__ kps, int k, float R,
+                                                       const long long* __restrict__ offs,
+                                                       const unsigned int* __restrict__ bh,
+                                                       unsigned int* __restrict__ bstart,
+                                                       unsigned long long* __restrict__ seg) {
+    __shared__ CandLds lds[4];
+    __shared__ unsigned int cur[4][SG_BUCKETS];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    cand_init(&lds[wave]);
+    const float R2 = (float)((double)R * (double)R);
+    const float sc = (float)SG_BUCKETS / R2;
+    unsigned int* cu = cur[wave];
+    constexpr int PER = SG_BUCKETS / 64;
+    for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        if (!(__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))) continue;
+        // exclusive scan of the histogram: lane owns buckets [PER lane, PER lane + PER)
+        unsigned int hv[PER];
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            hv[j] = bh[(size_t)q * SG_BUCKETS + PER * lane + j];
+            s += (int)hv[j];
+        }
+        int tot;
+        unsigned int run = (unsigned int)wave_excl_scan(s, tot);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            cu[PER * lane + j] = run;
+            bstart[(size_t)q * SG_BUCKETS + PER * lane + j] = run;
+            run += hv[j];
+        }
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long* out = seg + offs[q];
+        for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
+            if (v) out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+        });
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// wave per 64-rank chunk of a bucket-grouped segment: every key's exact (d2, idx) rank inside its
+// bucket -> the sorted segment (keys are unique, buckets hold a few keys each). The buckets the
+// chunk's keys belong to span [lo, hi) of the segment (the chunk plus the parts of its two end
+// buckets outside it); when that fits SR_STAGE keys it is staged in LDS and ranked from there.
+#define SR_STAGE 256
+__global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long long* __restrict__ offs,
+                                                   const int* __restrict__ cb, const int* __restrict__ owner,
+                                                   const unsigned int* __restrict__ bstart,
+                                                   const unsigned long long* __restrict__ seg,
+                                                   unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long stage[4][SR_STAGE];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int c = blockIdx.x * 4 + wave;
+    if (c >= cb[k]) return;
+    const int q = owner[c];
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    const int c0 = (c - cb[q]) * 64;
+    const int i = c0 + lane;
+    const int last = min(n, c0 + 64) - 1;  // last valid rank of the chunk (wave-uniform)
+    const float R2 = (float)((double)R * (double)R);
+    const float sc = (float)SG_BUCKETS / R2;
+    const unsigned int* bs = bstart + (size_t)q * SG_BUCKETS;
+    const unsigned long long* sg = seg + o;
+    const unsigned long long key = i < n ? sg[i] : ~0ull;
+    const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
+    const int b_lo = readlane_i(b, 0), b_hi = readlane_i(b, last - c0);
+    const unsigned int lo = bs[b_lo], hi = b_hi + 1 < SG_BUCKETS ? bs[b_hi + 1] : (unsigned int)n;
+    unsigned int s0 = 0, e0 = 0;
+    if (i < n) {
+        s0 = bs[b];
+        e0 = b + 1 < SG_BUCKETS ? bs[b + 1] : (unsigned int)n;
+    }
+    unsigned int rank = 0;
+    if (hi - lo <= SR_STAGE) {
+        unsigned long long* st = stage[wave];
+        for (unsigned int j = lane; j < hi - lo; j += 64) st[j] = sg[lo + j];
+        __builtin_amdgcn_wave_barrier();
+        if (i < n)
+            for (unsigned int j = s0; j < e0; ++j) rank += st[j - lo] < key ? 1u : 0u;
+    } else if (i < n) {
+        for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
+    }
+    if (i < n) out[o + s0 + rank] = key;
 }
 
 // counting sort of one keypoint's segment by d2 bucket, then exact rank inside the bucket
@@ -514,9 +626,9 @@ __global__ void __launch_bounds__(64) k_shot_hist(const float4* __restrict__ pts
 namespace bsh {
 
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
-                             hipStream_t s) {
+                             hipStream_t s, unsigned int* bh) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_count<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, counts);
+    bsk::k_shot_count<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, counts, bh);
     bsk::k_excl_scan<<<1, 1024, 0, s>>>(counts, k, offs);
     return hipGetLastError();
 }
@@ -525,6 +637,21 @@ hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R
                               unsigned long long* seg, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     bsk::k_shot_gather<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, offs, seg);
+    return hipGetLastError();
+}
+
+hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
+                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    bsk::k_shot_gather_b<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg);
+    return hipGetLastError();
+}
+
+hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
+                            const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
+                            hipStream_t s) {
+    if (k <= 0 || n_chunks <= 0) return hipSuccess;
+    bsk::k_shot_rank<<<(n_chunks + 3) / 4, 256, 0, s>>>(k, R, offs, cb, owner, bstart, seg, out);
     return hipGetLastError();
 }
 

@@ -587,12 +587,20 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     hipError_t e;
     const int cblocks = (A.n_chunks + 3) / 4;
     if (part == 0) {
-        if (A.n_plan > 0) bsk::k_sort2<<<A.n_plan, 256, 0, s>>>(A.plan, A.offs, A.R, A.seg, A.sorted, A.err);
+        if (A.bstart) {
+            if (A.n_chunks > 0) {
+                bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
+                if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s)))
+                    return e;
+            }
+        } else if (A.n_plan > 0) {
+            bsk::k_sort2<<<A.n_plan, 256, 0, s>>>(A.plan, A.offs, A.R, A.seg, A.sorted, A.err);
+        }
         return hipGetLastError();
     }
     if (part == 1) {
         if (A.n_chunks > 0) {
-            bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
+            if (!A.bstart) bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
             bsk::k_lrf_chunks<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.R, A.offs, A.cb, A.owner, A.sorted,
                                                        A.csum);
         }

@@ -16,10 +16,17 @@ hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc,
                       int* err, hipStream_t s);
+// bh (nullable, [k][1024] u32): per-keypoint d2-bucket histogram for the bucketed gather
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
-                             hipStream_t s);
+                             hipStream_t s, unsigned int* bh = nullptr);
 hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
                               unsigned long long* seg, hipStream_t s);
+// bucket-grouped gather (bstart: per-keypoint bucket starts) and the in-bucket rank that sorts it
+hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
+                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s);
+hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
+                            const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
+                            hipStream_t s);
 hipError_t launch_shot_sort(const long long* offs, int k, float R, unsigned long long* seg, unsigned long long* tmp,
                             hipStream_t s);
 hipError_t launch_lrf(const float4* pts4, const float* kps, int k, float R, const long long* offs,
@@ -71,6 +78,8 @@ struct Describe2Args {
     float* shot = nullptr;
     unsigned int* bits = nullptr;
     int* err = nullptr;  // |= 8 when a sort piece overflows its LDS buffer
+    // part 0 by in-bucket rank of a bucket-grouped segment (bstart) instead of the piece sort
+    const unsigned int* bstart = nullptr;
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 

@@ -1,0 +1,32 @@
+"""Diagnostic: standalone (uncontended) describe timing per stage for describe2 knob settings.
+usage: python describe_bench.py [knob values, default 2 1]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np  # noqa: E402
+
+import bshot_py  # noqa: E402
+
+pc, _ = bshot_py.synth_sweep(3)
+c = bshot_py.Context(0)
+c.set_cloud(pc)
+idx, rat = c.seg_ratio()
+kp, _ = bshot_py.select_topk(idx, rat, 2048)
+kps = pc[kp]
+ref = None
+for d2 in [int(x) for x in sys.argv[1:]] or [2, 1]:
+    c.set_option("describe2", d2)
+    c.describe(kps)
+    c.set_timing(True)
+    c.stage_reset()
+    for _ in range(10):
+        bits, shot, rf = c.describe(kps)
+    st = c.stage_times()
+    c.set_timing(False)
+    same = ref is None or np.array_equal(bits, ref)
+    ref = bits if ref is None else ref
+    ms = {k: round(v[0] / 10, 4) for k, v in st.items() if v[1]}
+    print(json.dumps({"describe2": d2, "identical_bits": bool(same), "total_ms": round(sum(ms.values()), 4), **ms}))
+c.close()
