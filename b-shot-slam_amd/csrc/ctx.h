@@ -139,14 +139,15 @@ struct bshot_ctx {
     DBuf<int4> plan;
     DBuf<int> cb, owner, okf, signs, perm;
     DBuf<double> csum, eig;
-    DBuf<uint4> recA;
-    DBuf<float4> recB;
+    DBuf<unsigned short> recS;
+    DBuf<float> recV;
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
     DBuf<unsigned int> sbh, sbst;  // bucketed gather: per-keypoint d2 histogram and bucket starts
     // tuning knob "describe2": 2 load-balanced SHOT with the bucketed gather + in-bucket rank
     // (default), 1 load-balanced SHOT with the piece sort, 0 wave/WG per keypoint
     int opt_describe2 = 2;
+    int opt_chunk_blocks = 0;  // grid cap of the 64-rank chunk kernels (0: one block per 4 chunks)
     int ladder_mode(const CloudState& s) const { return s.fine_ladder ? (opt_ladder_front ? 2 : 1) : 0; }
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag

@@ -470,8 +470,8 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
     HIPCHK(c->okf.ensure(k), "alloc okf");
     HIPCHK(c->signs.ensure(2 * (size_t)k), "alloc signs");
-    HIPCHK(c->recA.ensure(total > 0 ? (size_t)total : 1), "alloc records");
-    HIPCHK(c->recB.ensure(total > 0 ? (size_t)total : 1), "alloc records");
+    HIPCHK(c->recS.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
+    HIPCHK(c->recV.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
     if (n_plan > 0)
         HIPCHK(hipMemcpyAsync(c->plan.p, hp, sizeof(int4) * n_plan, hipMemcpyHostToDevice, st), "H2D plan");
     HIPCHK(c->perm.ensure(k), "alloc perm");
@@ -481,9 +481,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     A.k = k; A.n_plan = n_plan; A.n_chunks = cbr; A.R = R;
     A.plan = c->plan.p; A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p; A.pts4 = S.pts4.p; A.normals = c->normals.p;
     A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
-    A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recA = c->recA.p; A.recB = c->recB.p;
+    A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
     A.bstart = bucketed ? c->sbst.p : nullptr;
+    A.max_blocks = c->opt_chunk_blocks;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -962,6 +963,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
+    else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

@@ -169,38 +169,40 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
                                                    unsigned long long* __restrict__ out) {
     __shared__ unsigned long long stage[4][SR_STAGE];
     const int wave = threadIdx.x >> 6, lane = lane_id();
-    const int c = blockIdx.x * 4 + wave;
-    if (c >= cb[k]) return;
-    const int q = owner[c];
-    const long long o = offs[q];
-    const int n = (int)(offs[q + 1] - o);
-    const int c0 = (c - cb[q]) * 64;
-    const int i = c0 + lane;
-    const int last = min(n, c0 + 64) - 1;  // last valid rank of the chunk (wave-uniform)
-    const float R2 = (float)((double)R * (double)R);
-    const float sc = (float)SG_BUCKETS / R2;
-    const unsigned int* bs = bstart + (size_t)q * SG_BUCKETS;
-    const unsigned long long* sg = seg + o;
-    const unsigned long long key = i < n ? sg[i] : ~0ull;
-    const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
-    const int b_lo = readlane_i(b, 0), b_hi = readlane_i(b, last - c0);
-    const unsigned int lo = bs[b_lo], hi = b_hi + 1 < SG_BUCKETS ? bs[b_hi + 1] : (unsigned int)n;
-    unsigned int s0 = 0, e0 = 0;
-    if (i < n) {
-        s0 = bs[b];
-        e0 = b + 1 < SG_BUCKETS ? bs[b + 1] : (unsigned int)n;
-    }
-    unsigned int rank = 0;
-    if (hi - lo <= SR_STAGE) {
-        unsigned long long* st = stage[wave];
-        for (unsigned int j = lane; j < hi - lo; j += 64) st[j] = sg[lo + j];
-        __builtin_amdgcn_wave_barrier();
-        if (i < n)
-            for (unsigned int j = s0; j < e0; ++j) rank += st[j - lo] < key ? 1u : 0u;
-    } else if (i < n) {
-        for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
-    }
-    if (i < n) out[o + s0 + rank] = key;
+    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
+    for (int c = blockIdx.x * 4 + wave; c < cb[k]; c += gridDim.x * 4) [&]() {
+        const int q = owner[c];
+        const long long o = offs[q];
+        const int n = (int)(offs[q + 1] - o);
+        const int c0 = (c - cb[q]) * 64;
+        const int i = c0 + lane;
+        const int last = min(n, c0 + 64) - 1;  // last valid rank of the chunk (wave-uniform)
+        const float R2 = (float)((double)R * (double)R);
+        const float sc = (float)SG_BUCKETS / R2;
+        const unsigned int* bs = bstart + (size_t)q * SG_BUCKETS;
+        const unsigned long long* sg = seg + o;
+        const unsigned long long key = i < n ? sg[i] : ~0ull;
+        const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
+        const int b_lo = readlane_i(b, 0), b_hi = readlane_i(b, last - c0);
+        const unsigned int lo = bs[b_lo], hi = b_hi + 1 < SG_BUCKETS ? bs[b_hi + 1] : (unsigned int)n;
+        unsigned int s0 = 0, e0 = 0;
+        if (i < n) {
+            s0 = bs[b];
+            e0 = b + 1 < SG_BUCKETS ? bs[b + 1] : (unsigned int)n;
+        }
+        unsigned int rank = 0;
+        if (hi - lo <= SR_STAGE) {
+            unsigned long long* st = stage[wave];
+            for (unsigned int j = lane; j < hi - lo; j += 64) st[j] = sg[lo + j];
+            __builtin_amdgcn_wave_barrier();
+            if (i < n)
+                for (unsigned int j = s0; j < e0; ++j) rank += st[j - lo] < key ? 1u : 0u;
+        } else if (i < n) {
+            for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
+        }
+        if (i < n) out[o + s0 + rank] = key;
+        __builtin_amdgcn_wave_barrier();  // the next chunk restages
+    }();
 }
 
 // counting sort of one keypoint's segment by d2 bucket, then exact rank inside the bucket
@@ -649,9 +651,11 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
 
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
-                            hipStream_t s) {
+                            hipStream_t s, int max_blocks) {
     if (k <= 0 || n_chunks <= 0) return hipSuccess;
-    bsk::k_shot_rank<<<(n_chunks + 3) / 4, 256, 0, s>>>(k, R, offs, cb, owner, bstart, seg, out);
+    int blocks = (n_chunks + 3) / 4;
+    if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+    bsk::k_shot_rank<<<blocks, 256, 0, s>>>(k, R, offs, cb, owner, bstart, seg, out);
     return hipGetLastError();
 }
 

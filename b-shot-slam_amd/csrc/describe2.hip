@@ -128,37 +128,38 @@ __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ p
                                                     const unsigned long long* __restrict__ seg,
                                                     double* __restrict__ csum) {
     const int lane = lane_id();
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= cb[k]) return;
-    const int q = owner[c];
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const long long o = offs[q];
-    const int n = (int)(offs[q + 1] - o);
-    const int i = (c - cb[q]) * 64 + lane;
-    double v[7] = {0, 0, 0, 0, 0, 0, 0};
-    int isv = 0;
-    if (i < n) {
-        const unsigned long long key = seg[o + i];
-        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
-        if (!(p.x == kx && p.y == ky && p.z == kz)) {
-            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-            const double w = (double)R - sqrt((double)__uint_as_float((unsigned)(key >> 32)));
-            v[0] = w * (vx * vx); v[1] = w * (vx * vy); v[2] = w * (vx * vz);
-            v[3] = w * (vy * vy); v[4] = w * (vy * vz); v[5] = w * (vz * vz);
-            v[6] = w;
-            isv = 1;
+    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+        const int q = owner[c];
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        const long long o = offs[q];
+        const int n = (int)(offs[q + 1] - o);
+        const int i = (c - cb[q]) * 64 + lane;
+        double v[7] = {0, 0, 0, 0, 0, 0, 0};
+        int isv = 0;
+        if (i < n) {
+            const unsigned long long key = seg[o + i];
+            const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+            if (!(p.x == kx && p.y == ky && p.z == kz)) {
+                const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+                const double w = (double)R - sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+                v[0] = w * (vx * vx); v[1] = w * (vx * vy); v[2] = w * (vx * vz);
+                v[3] = w * (vy * vy); v[4] = w * (vy * vz); v[5] = w * (vz * vz);
+                v[6] = w;
+                isv = 1;
+            }
         }
-    }
-#pragma unroll
-    for (int j = 0; j < 7; ++j) v[j] = wave_tree_sum_d(v[j]);
-    const int nv = __popcll(__ballot(isv != 0));
-    if (lane < 8) {
-        double x = (double)nv;
-#pragma unroll
-        for (int j = 0; j < 7; ++j)
-            if (lane == j) x = v[j];
-        csum[8 * (size_t)c + lane] = x;
-    }
+    #pragma unroll
+        for (int j = 0; j < 7; ++j) v[j] = wave_tree_sum_d(v[j]);
+        const int nv = __popcll(__ballot(isv != 0));
+        if (lane < 8) {
+            double x = (double)nv;
+    #pragma unroll
+            for (int j = 0; j < 7; ++j)
+                if (lane == j) x = v[j];
+            csum[8 * (size_t)c + lane] = x;
+        }
+    }();
 }
 
 // eig[8 q + 0..2] = x axis (largest), [3..5] = z axis (smallest), [6] = valid count; okf[q]
@@ -215,31 +216,32 @@ __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts
                                                   const double* __restrict__ eig, const int* __restrict__ okf,
                                                   int* __restrict__ signs) {
     const int lane = lane_id();
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= cb[k]) return;
-    const int q = owner[c];
-    if (!okf[q]) return;
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const long long o = offs[q];
-    const int n = (int)(offs[q + 1] - o);
-    const int i = (c - cb[q]) * 64 + lane;
-    const double* e = eig + 8 * (size_t)q;
-    int pt = 0, pn = 0;
-    if (i < n) {
-        const unsigned long long key = seg[o + i];
-        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
-        if (!(p.x == kx && p.y == ky && p.z == kz)) {
-            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-            if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
-            if (((vx * e[3] + vy * e[4]) + vz * e[5]) >= 0) pn = 1;
+    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+        const int q = owner[c];
+        if (!okf[q]) return;
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        const long long o = offs[q];
+        const int n = (int)(offs[q + 1] - o);
+        const int i = (c - cb[q]) * 64 + lane;
+        const double* e = eig + 8 * (size_t)q;
+        int pt = 0, pn = 0;
+        if (i < n) {
+            const unsigned long long key = seg[o + i];
+            const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+            if (!(p.x == kx && p.y == ky && p.z == kz)) {
+                const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+                if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
+                if (((vx * e[3] + vy * e[4]) + vz * e[5]) >= 0) pn = 1;
+            }
         }
-    }
-    pt = __popcll(__ballot(pt != 0));
-    pn = __popcll(__ballot(pn != 0));
-    if (lane == 0) {
-        if (pt) atomicAdd(&signs[2 * q], pt);
-        if (pn) atomicAdd(&signs[2 * q + 1], pn);
-    }
+        pt = __popcll(__ballot(pt != 0));
+        pn = __popcll(__ballot(pn != 0));
+        if (lane == 0) {
+            if (pt) atomicAdd(&signs[2 * q], pt);
+            if (pn) atomicAdd(&signs[2 * q + 1], pn);
+        }
+    }();
 }
 
 __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
@@ -320,9 +322,9 @@ __device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0,
 #define PST2_RAD_135 2.3561944901923449288469825374596
 #define PST2_RAD_PI_7_8 2.7488935718910690836548129603691
 
-// record of neighbour r: A = {b0 | b1 << 16, b2 | b3 << 16, b4 | sector mask << 16, bits(v4)},
-// B = {v0, v1, v2, v3};
-// unused slots -> bin 360 (padding) with value +0
+// records of chunk c (64 ranks): recS[320 c + 64 j + r] = bin of slot j of rank r (u16),
+// recV[...] = its value; slot order = PCL's add order per neighbour (cos neighbour, radius,
+// inclination, azimuth, main bin); unused slots and padding ranks -> bin 360 with value +0
 __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__ pts4,
                                                       const float4* __restrict__ normals,
                                                       const float* __restrict__ kps, int k, float R,
@@ -330,111 +332,114 @@ __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__
                                                       const int* __restrict__ owner,
                                                       const unsigned long long* __restrict__ seg,
                                                       const float* __restrict__ rf_in, const int* __restrict__ ok_in,
-                                                      uint4* __restrict__ recA, float4* __restrict__ recB) {
+                                                      unsigned short* __restrict__ recS, float* __restrict__ recV) {
     const int lane = lane_id();
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= cb[k]) return;
-    const int q = owner[c];
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const long long o = offs[q];
-    const int n = (int)(offs[q + 1] - o);
-    const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
-    if (!(fin && ok_in[q] && n >= 5)) return;
-    const int i = (c - cb[q]) * 64 + lane;
-    if (i >= n) return;
-    const double Rd = (double)R;
-    const double r12 = Rd / 2, r34 = (Rd * 3) / 4, r14 = Rd / 4;
-    const int nr_bins = 10;
-    float rf[9];
-#pragma unroll
-    for (int j = 0; j < 9; ++j) rf[j] = rf_in[9 * (size_t)q + j];
-    int bins[5] = {-1, -1, -1, -1, -1};
-    float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    const unsigned long long key = seg[o + i];
-    const unsigned int idx = (unsigned int)(key & 0xFFFFFFFFu);
-    const float4 nv = normals[idx];
-    if (__builtin_isfinite(nv.x) && __builtin_isfinite(nv.y) && __builtin_isfinite(nv.z)) {
-        double cosd = (double)dot4f_2(nv.x, nv.y, nv.z, rf[6], rf[7], rf[8]);
-        if (cosd > 1.0) cosd = 1.0;
-        if (cosd < -1.0) cosd = -1.0;
-        double bd = ((1.0 + cosd) * nr_bins) / 2;
-        const float4 p = pts4[idx];
-        const float dx = p.x - kx, dy = p.y - ky, dz = p.z - kz;
-        const double distance = sqrt((double)__uint_as_float((unsigned)(key >> 32)));
-        if (!(fabs(distance - 0.0) < 1e-15)) {
-            double xr = (double)dot4f_2(dx, dy, dz, rf[0], rf[1], rf[2]);
-            double yr = (double)dot4f_2(dx, dy, dz, rf[3], rf[4], rf[5]);
-            double zr = (double)dot4f_2(dx, dy, dz, rf[6], rf[7], rf[8]);
-            if (fabs(yr) < 1E-30) yr = 0;
-            if (fabs(xr) < 1E-30) xr = 0;
-            if (fabs(zr) < 1E-30) zr = 0;
-            const unsigned bit4 = ((yr > 0) || ((yr == 0.0) && (xr < 0))) ? 1u : 0u;
-            const unsigned bit3 = ((xr > 0) || ((xr == 0.0) && (yr > 0))) ? (bit4 ? 0u : 1u) : bit4;
-            int desc = (int)((bit4 << 3) + (bit3 << 2));
-            desc = desc << 1;
-            if ((xr * yr > 0) || (xr == 0.0)) desc += (fabs(xr) >= fabs(yr)) ? 0 : 4;
-            else desc += (fabs(xr) > fabs(yr)) ? 4 : 0;
-            desc += zr > 0 ? 1 : 0;
-            desc += (distance > r12) ? 2 : 0;
-            const int step = (int)floor(bd + 0.5);
-            const int vol = desc * (nr_bins + 1);
-            bd -= step;
-            double w = (1 - fabs(bd));
-            if (bd > 0) { bins[0] = vol + ((step + 1) % nr_bins); vals[0] = (float)bd; }
-            else { bins[0] = vol + ((step - 1 + nr_bins) % nr_bins); vals[0] = -(float)bd; }
-            if (distance > r12) {
-                const double rd = (distance - r34) / r12;
-                if (distance > r34) w += 1 - rd;
-                else { w += 1 + rd; bins[1] = (desc - 2) * (nr_bins + 1) + step; vals[1] = (float)(-rd); }
-            } else {
-                const double rd = (distance - r14) / r12;
-                if (distance < r14) w += 1 + rd;
-                else { w += 1 - rd; bins[1] = (desc + 2) * (nr_bins + 1) + step; vals[1] = (float)rd; }
-            }
-            double ic = zr / distance;
-            if (ic < -1.0) ic = -1.0;
-            if (ic > 1.0) ic = 1.0;
-            const double incl = bm::acos_(ic);
-            if (incl > PST2_RAD_90 || (fabs(incl - PST2_RAD_90) < 1e-30 && zr <= 0)) {
-                const double id = (incl - PST2_RAD_135) / PST2_RAD_90;
-                if (incl > PST2_RAD_135) w += 1 - id;
-                else { w += 1 + id; bins[2] = (desc + 1) * (nr_bins + 1) + step; vals[2] = -(float)id; }
-            } else {
-                const double id = (incl - PST2_RAD_45) / PST2_RAD_90;
-                if (incl < PST2_RAD_45) w += 1 + id;
-                else { w += 1 - id; bins[2] = (desc - 1) * (nr_bins + 1) + step; vals[2] = (float)id; }
-            }
-            if (yr != 0.0 || xr != 0.0) {
-                const double az = bm::atan2_(yr, xr);
-                const int sel = desc >> 2;
-                double ad = (az - (-PST2_RAD_PI_7_8 + PST2_RAD_45 * sel)) / PST2_RAD_45;
-                ad = fmax(-0.5, fmin(ad, 0.5));
-                if (ad > 0) {
-                    w += 1 - ad;
-                    bins[3] = ((desc + 4) % 32) * (nr_bins + 1) + step; vals[3] = (float)ad;
-                } else {
-                    w += 1 + ad;
-                    bins[3] = ((desc - 4 + 32) % 32) * (nr_bins + 1) + step; vals[3] = -(float)ad;
-                }
-            }
-            bins[4] = vol + step;
-            vals[4] = (float)w;
+    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+        const int q = owner[c];
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        const long long o = offs[q];
+        const int n = (int)(offs[q + 1] - o);
+        const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
+        if (!(fin && ok_in[q] && n >= 5)) return;
+        const int i = (c - cb[q]) * 64 + lane;
+        unsigned short* rs = recS + (size_t)c * 320 + lane;  // slot-major chunk rows: [slot][64 ranks]
+        float* rv = recV + (size_t)c * 320 + lane;
+        if (i >= n) {
+            // padding ranks of the keypoint's last chunk: no-op records
+    #pragma unroll
+            for (int j = 0; j < 5; ++j) { rs[64 * j] = (unsigned short)360; rv[64 * j] = 0.f; }
+            return;
         }
-    }
-    unsigned int bb[5];
-    float vv[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        bb[j] = bins[j] < 0 ? 360u : (unsigned)bins[j];
-        vv[j] = bins[j] < 0 ? 0.f : vals[j];
-    }
-    unsigned int smask = 0;  // azimuth sectors (bins [44 s, 44 s + 44)) this neighbour touches
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-        if (bb[j] < 352u) smask |= 1u << (bb[j] / 44u);
-    recA[o + i] = make_uint4(bb[0] | (bb[1] << 16), bb[2] | (bb[3] << 16), bb[4] | (smask << 16),
-                             __float_as_uint(vv[4]));
-    recB[o + i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        const double Rd = (double)R;
+        const double r12 = Rd / 2, r34 = (Rd * 3) / 4, r14 = Rd / 4;
+        const int nr_bins = 10;
+        float rf[9];
+    #pragma unroll
+        for (int j = 0; j < 9; ++j) rf[j] = rf_in[9 * (size_t)q + j];
+        int bins[5] = {-1, -1, -1, -1, -1};
+        float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        const unsigned long long key = seg[o + i];
+        const unsigned int idx = (unsigned int)(key & 0xFFFFFFFFu);
+        const float4 nv = normals[idx];
+        if (__builtin_isfinite(nv.x) && __builtin_isfinite(nv.y) && __builtin_isfinite(nv.z)) {
+            double cosd = (double)dot4f_2(nv.x, nv.y, nv.z, rf[6], rf[7], rf[8]);
+            if (cosd > 1.0) cosd = 1.0;
+            if (cosd < -1.0) cosd = -1.0;
+            double bd = ((1.0 + cosd) * nr_bins) / 2;
+            const float4 p = pts4[idx];
+            const float dx = p.x - kx, dy = p.y - ky, dz = p.z - kz;
+            const double distance = sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+            if (!(fabs(distance - 0.0) < 1e-15)) {
+                double xr = (double)dot4f_2(dx, dy, dz, rf[0], rf[1], rf[2]);
+                double yr = (double)dot4f_2(dx, dy, dz, rf[3], rf[4], rf[5]);
+                double zr = (double)dot4f_2(dx, dy, dz, rf[6], rf[7], rf[8]);
+                if (fabs(yr) < 1E-30) yr = 0;
+                if (fabs(xr) < 1E-30) xr = 0;
+                if (fabs(zr) < 1E-30) zr = 0;
+                const unsigned bit4 = ((yr > 0) || ((yr == 0.0) && (xr < 0))) ? 1u : 0u;
+                const unsigned bit3 = ((xr > 0) || ((xr == 0.0) && (yr > 0))) ? (bit4 ? 0u : 1u) : bit4;
+                int desc = (int)((bit4 << 3) + (bit3 << 2));
+                desc = desc << 1;
+                if ((xr * yr > 0) || (xr == 0.0)) desc += (fabs(xr) >= fabs(yr)) ? 0 : 4;
+                else desc += (fabs(xr) > fabs(yr)) ? 4 : 0;
+                desc += zr > 0 ? 1 : 0;
+                desc += (distance > r12) ? 2 : 0;
+                const int step = (int)floor(bd + 0.5);
+                const int vol = desc * (nr_bins + 1);
+                bd -= step;
+                double w = (1 - fabs(bd));
+                if (bd > 0) { bins[0] = vol + ((step + 1) % nr_bins); vals[0] = (float)bd; }
+                else { bins[0] = vol + ((step - 1 + nr_bins) % nr_bins); vals[0] = -(float)bd; }
+                if (distance > r12) {
+                    const double rd = (distance - r34) / r12;
+                    if (distance > r34) w += 1 - rd;
+                    else { w += 1 + rd; bins[1] = (desc - 2) * (nr_bins + 1) + step; vals[1] = (float)(-rd); }
+                } else {
+                    const double rd = (distance - r14) / r12;
+                    if (distance < r14) w += 1 + rd;
+                    else { w += 1 - rd; bins[1] = (desc + 2) * (nr_bins + 1) + step; vals[1] = (float)rd; }
+                }
+                double ic = zr / distance;
+                if (ic < -1.0) ic = -1.0;
+                if (ic > 1.0) ic = 1.0;
+                const double incl = bm::acos_(ic);
+                if (incl > PST2_RAD_90 || (fabs(incl - PST2_RAD_90) < 1e-30 && zr <= 0)) {
+                    const double id = (incl - PST2_RAD_135) / PST2_RAD_90;
+                    if (incl > PST2_RAD_135) w += 1 - id;
+                    else { w += 1 + id; bins[2] = (desc + 1) * (nr_bins + 1) + step; vals[2] = -(float)id; }
+                } else {
+                    const double id = (incl - PST2_RAD_45) / PST2_RAD_90;
+                    if (incl < PST2_RAD_45) w += 1 + id;
+                    else { w += 1 - id; bins[2] = (desc - 1) * (nr_bins + 1) + step; vals[2] = (float)id; }
+                }
+                if (yr != 0.0 || xr != 0.0) {
+                    const double az = bm::atan2_(yr, xr);
+                    const int sel = desc >> 2;
+                    double ad = (az - (-PST2_RAD_PI_7_8 + PST2_RAD_45 * sel)) / PST2_RAD_45;
+                    ad = fmax(-0.5, fmin(ad, 0.5));
+                    if (ad > 0) {
+                        w += 1 - ad;
+                        bins[3] = ((desc + 4) % 32) * (nr_bins + 1) + step; vals[3] = (float)ad;
+                    } else {
+                        w += 1 + ad;
+                        bins[3] = ((desc - 4 + 32) % 32) * (nr_bins + 1) + step; vals[3] = -(float)ad;
+                    }
+                }
+                bins[4] = vol + step;
+                vals[4] = (float)w;
+            }
+        }
+        unsigned int bb[5];
+        float vv[5];
+    #pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            bb[j] = bins[j] < 0 ? 360u : (unsigned)bins[j];
+            vv[j] = bins[j] < 0 ? 0.f : vals[j];
+        }
+    #pragma unroll
+        for (int j = 0; j < 5; ++j) { rs[64 * j] = (unsigned short)bb[j]; rv[64 * j] = vv[j]; }
+    }();
 }
 
 // wave per keypoint: records applied in rank order to the LDS histogram (lanes 0..4 own record
@@ -443,13 +448,16 @@ __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__
 // descending neighbourhood size (perm, host-sorted) and the LDS reservation caps residency at
 // 4 keypoints per CU: the largest start first and smaller ones fill in as CUs free up.
 #define HA_LDS_PAD 8192
+#ifndef HA_SKIP
+#define HA_SKIP 0
+#endif
 __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps, int k, const int* __restrict__ perm,
-                                                   const long long* __restrict__ offs, const int* __restrict__ ok_in,
-                                                   const uint4* __restrict__ recA, const float4* __restrict__ recB,
-                                                   float* __restrict__ shot_out, unsigned int* __restrict__ bits_out) {
+                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
+                                                   const int* __restrict__ ok_in,
+                                                   const unsigned short* __restrict__ recS,
+                                                   const float* __restrict__ recV, float* __restrict__ shot_out,
+                                                   unsigned int* __restrict__ bits_out) {
     __shared__ float hist[384];
-    __shared__ int rbin[64 * 5];
-    __shared__ float rval[64 * 5];
     __shared__ unsigned int gcode[88];
     __shared__ float pad_[HA_LDS_PAD];  // residency cap (see above)
     const int lane = lane_id();
@@ -462,44 +470,49 @@ __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps
     const bool good = fin && ok_in[q] && n >= 5;
     for (int j = lane; j < 384; j += 64) hist[j] = 0.0f;
     __builtin_amdgcn_wave_barrier();
-    if (good) {
-        // records of 8 chunks are loaded per batch (one wait per 512 neighbours), then applied
-        // chunk by chunk in rank order
-        for (int c0 = 0; c0 < n; c0 += 64 * 8) {
-            uint4 ra[8];
-            float4 rb[8];
+    if (good && lane < 5) {
+        // lane j applies record slot j of every rank, in rank order: one ds_add_f32 per rank with
+        // lanes 0..4 (distinct bins within a rank), so every bin sees its adds in PCL's order. A
+        // lane reads its slot's chunk rows straight from memory (64 bins as 32 dwords, 64 values),
+        // the next chunk's rows in flight while this one is applied.
+        const int c_end = cb[q + 1];
+        auto load = [&](int c, uint4* bw, float4* vw) {
+            const uint4* b4 = reinterpret_cast<const uint4*>(recS + (size_t)c * 320 + 64 * lane);
+            const float4* v4 = reinterpret_cast<const float4*>(recV + (size_t)c * 320 + 64 * lane);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bw[u] = b4[u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) vw[u] = v4[u];
+        };
+        uint4 bw[8], nbw[8];
+        float4 vw[16], nvw[16];
+        int c = cb[q];
+        load(c, bw, vw);
+        for (; c < c_end; ++c) {
+            if (c + 1 < c_end) load(c + 1, nbw, nvw);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int i = c0 + 64 * u + lane;
-                ra[u] = make_uint4(360u | (360u << 16), 360u | (360u << 16), 360u, 0u);
-                rb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (i < n) { ra[u] = recA[o + i]; rb[u] = recB[o + i]; }
-            }
+                const unsigned int w[4] = {bw[u].x, bw[u].y, bw[u].z, bw[u].w};
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (c0 + 64 * u >= n) break;
-                rbin[lane * 5 + 0] = (int)(ra[u].x & 0xFFFFu); rval[lane * 5 + 0] = rb[u].x;
-                rbin[lane * 5 + 1] = (int)(ra[u].x >> 16);     rval[lane * 5 + 1] = rb[u].y;
-                rbin[lane * 5 + 2] = (int)(ra[u].y & 0xFFFFu); rval[lane * 5 + 2] = rb[u].z;
-                rbin[lane * 5 + 3] = (int)(ra[u].y >> 16);     rval[lane * 5 + 3] = rb[u].w;
-                rbin[lane * 5 + 4] = (int)(ra[u].z & 0xFFFFu); rval[lane * 5 + 4] = __uint_as_float(ra[u].w);
-                __builtin_amdgcn_wave_barrier();
-                if (lane < 5) {
-#pragma unroll
-                    for (int g = 0; g < 64; g += 16) {
-                        int bb[16];
-                        float vv[16];
-#pragma unroll
-                        for (int v = 0; v < 16; ++v) {
-                            bb[v] = rbin[(g + v) * 5 + lane];
-                            vv[v] = rval[(g + v) * 5 + lane];
-                        }
-#pragma unroll
-                        for (int v = 0; v < 16; ++v) atomicAdd(&hist[bb[v]], vv[v]);
-                    }
+                for (int h = 0; h < 4; ++h) {
+                    const int r = 8 * u + 2 * h;  // ranks r, r + 1 of the chunk
+                    const float4 va = vw[r >> 2];
+                    const float v0 = (r & 3) == 0 ? va.x : va.z;
+                    const float v1 = (r & 3) == 0 ? va.y : va.w;
+#if HA_SKIP
+                    // no-op records (bin 360, +0) issue no LDS atomic
+                    if ((w[h] & 0xFFFFu) < 352u) atomicAdd(&hist[w[h] & 0xFFFFu], v0);
+                    if ((w[h] >> 16) < 352u) atomicAdd(&hist[w[h] >> 16], v1);
+#else
+                    atomicAdd(&hist[w[h] & 0xFFFFu], v0);
+                    atomicAdd(&hist[w[h] >> 16], v1);
+#endif
                 }
-                __builtin_amdgcn_wave_barrier();
             }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bw[u] = nbw[u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) vw[u] = nvw[u];
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -585,12 +598,14 @@ namespace bsh {
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.k <= 0) return hipSuccess;
     hipError_t e;
-    const int cblocks = (A.n_chunks + 3) / 4;
+    int cblocks = (A.n_chunks + 3) / 4;
+    if (A.max_blocks > 0 && cblocks > A.max_blocks) cblocks = A.max_blocks;
     if (part == 0) {
         if (A.bstart) {
             if (A.n_chunks > 0) {
                 bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
-                if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s)))
+                if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
+                                            A.max_blocks)))
                     return e;
             }
         } else if (A.n_plan > 0) {
@@ -615,8 +630,8 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     }
     if (A.n_chunks > 0)
         bsk::k_hist_contrib<<<cblocks, 256, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.offs, A.cb, A.owner,
-                                                     A.sorted, A.rf, A.ok, A.recA, A.recB);
-    bsk::k_hist_apply<<<A.k, 64, 0, s>>>(A.kps, A.k, A.perm, A.offs, A.ok, A.recA, A.recB, A.shot, A.bits);
+                                                     A.sorted, A.rf, A.ok, A.recS, A.recV);
+    bsk::k_hist_apply<<<A.k, 64, 0, s>>>(A.kps, A.k, A.perm, A.offs, A.cb, A.ok, A.recS, A.recV, A.shot, A.bits);
     return hipGetLastError();
 }
 

@@ -26,7 +26,7 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
                                 const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s);
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
-                            hipStream_t s);
+                            hipStream_t s, int max_blocks = 0);
 hipError_t launch_shot_sort(const long long* offs, int k, float R, unsigned long long* seg, unsigned long long* tmp,
                             hipStream_t s);
 hipError_t launch_lrf(const float4* pts4, const float* kps, int k, float R, const long long* offs,
@@ -73,13 +73,14 @@ struct Describe2Args {
     int* signs = nullptr;                     // 2 per keypoint
     float* rf = nullptr;
     int* ok = nullptr;
-    uint4* recA = nullptr;
-    float4* recB = nullptr;
+    unsigned short* recS = nullptr;  // histogram records, slot-major per 64-rank chunk (320 per chunk)
+    float* recV = nullptr;
     float* shot = nullptr;
     unsigned int* bits = nullptr;
     int* err = nullptr;  // |= 8 when a sort piece overflows its LDS buffer
     // part 0 by in-bucket rank of a bucket-grouped segment (bstart) instead of the piece sort
     const unsigned int* bstart = nullptr;
+    int max_blocks = 0;  // grid cap of the chunk kernels (0: one block per 4 chunks)
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 

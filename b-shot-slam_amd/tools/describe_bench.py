@@ -16,8 +16,12 @@ idx, rat = c.seg_ratio()
 kp, _ = bshot_py.select_topk(idx, rat, 2048)
 kps = pc[kp]
 ref = None
-for d2 in [int(x) for x in sys.argv[1:]] or [2, 1]:
-    c.set_option("describe2", d2)
+# arguments: describe2 knob values, or name=value option sets ("chunk_blocks=2048,describe2=2")
+for arg in sys.argv[1:] or ["2", "1"]:
+    opts = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in arg.split(",")) if "=" in arg else {"describe2": int(arg)}
+    for kk, vv in opts.items():
+        c.set_option(kk, vv)
+    d2 = arg
     c.describe(kps)
     c.set_timing(True)
     c.stage_reset()
