@@ -469,7 +469,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->csum.ensure(8 * (size_t)(cbr > 0 ? cbr : 1)), "alloc csum");
     HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
     HIPCHK(c->okf.ensure(k), "alloc okf");
-    HIPCHK(c->signs.ensure(2 * (size_t)k), "alloc signs");
+    HIPCHK(c->signs.ensure(2 * (size_t)(cbr > 0 ? cbr : 1)), "alloc signs");  // per-chunk sign counts
     HIPCHK(c->recS.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
     HIPCHK(c->recV.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
     if (n_plan > 0)

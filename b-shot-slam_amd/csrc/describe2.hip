@@ -208,13 +208,14 @@ __global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ c
     okf[q] = ok;
 }
 
-// signs[2 q] += #(v . x >= 0), signs[2 q + 1] += #(v . z >= 0) over valid neighbours
+// csign[2 c] = #(v . x >= 0), csign[2 c + 1] = #(v . z >= 0) over chunk c's valid neighbours
+// (per-chunk counts, summed by k_lrf_fin: no same-address atomics)
 __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
                                                   const int* __restrict__ owner,
                                                   const unsigned long long* __restrict__ seg,
                                                   const double* __restrict__ eig, const int* __restrict__ okf,
-                                                  int* __restrict__ signs) {
+                                                  int* __restrict__ csign) {
     const int lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
     for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
@@ -237,18 +238,15 @@ __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts
         }
         pt = __popcll(__ballot(pt != 0));
         pn = __popcll(__ballot(pn != 0));
-        if (lane == 0) {
-            if (pt) atomicAdd(&signs[2 * q], pt);
-            if (pn) atomicAdd(&signs[2 * q + 1], pn);
-        }
+        if (lane == 0) reinterpret_cast<int2*>(csign)[c] = make_int2(pt, pn);
     }();
 }
 
 __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
-                                                const long long* __restrict__ offs,
+                                                const long long* __restrict__ offs, const int* __restrict__ cb,
                                                 const unsigned long long* __restrict__ seg,
                                                 const double* __restrict__ eig, const int* __restrict__ okf,
-                                                const int* __restrict__ signs, float* __restrict__ rf_out,
+                                                const int* __restrict__ csign, float* __restrict__ rf_out,
                                                 int* __restrict__ ok_out) {
     const int q = blockIdx.x * 64 + threadIdx.x;
     if (q >= k) return;
@@ -262,8 +260,23 @@ __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4,
     const int valid_total = (int)e[6];
     const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
     double x[3] = {e[0], e[1], e[2]}, z[3] = {e[3], e[4], e[5]};
-    int PT = 2 * signs[2 * q] - valid_total;
-    int PN = 2 * signs[2 * q + 1] - valid_total;
+    // sign counts: sum of the keypoint's per-chunk counts (integers, any order)
+    int st = 0, sn = 0;
+    {
+        const int2* cs2 = reinterpret_cast<const int2*>(csign);
+        const int c0 = cb[q], c1 = cb[q + 1];
+        int cc = c0;
+        for (; cc + 8 <= c1; cc += 8) {
+            int2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = cs2[cc + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { st += v[u].x; sn += v[u].y; }
+        }
+        for (; cc < c1; ++cc) { st += cs2[cc].x; sn += cs2[cc].y; }
+    }
+    int PT = 2 * st - valid_total;
+    int PN = 2 * sn - valid_total;
     if (PT == 0 || PN == 0) {
         // median-5 rule over valid neighbours by rank. Excluded neighbours (exact duplicates of the
         // keypoint) have d2 == 0, so they sit in the leading d2 == 0 run: scan that run, then the
@@ -620,12 +633,11 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
                                                        A.csum);
         }
         bsk::k_lrf_eig<<<(A.k + 63) / 64, 64, 0, s>>>(A.k, A.cb, A.csum, A.eig, A.okf);
-        if ((e = hipMemsetAsync(A.signs, 0, sizeof(int) * 2 * (size_t)A.k, s)) != hipSuccess) return e;
         if (A.n_chunks > 0)
             bsk::k_lrf_sign<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.owner, A.sorted, A.eig,
                                                      A.okf, A.signs);
-        bsk::k_lrf_fin<<<(A.k + 63) / 64, 64, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.sorted, A.eig, A.okf, A.signs,
-                                                      A.rf, A.ok);
+        bsk::k_lrf_fin<<<(A.k + 63) / 64, 64, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.sorted, A.eig, A.okf,
+                                                      A.signs, A.rf, A.ok);
         return hipGetLastError();
     }
     if (A.n_chunks > 0)

@@ -70,7 +70,7 @@ struct Describe2Args {
     double* csum = nullptr;                   // 8 per chunk
     double* eig = nullptr;                    // 8 per keypoint
     int* okf = nullptr;                       // eigen ok per keypoint
-    int* signs = nullptr;                     // 2 per keypoint
+    int* signs = nullptr;                     // 2 per chunk: sign counts (k_lrf_sign)
     float* rf = nullptr;
     int* ok = nullptr;
     unsigned short* recS = nullptr;  // histogram records, slot-major per 64-rank chunk (320 per chunk)
