@@ -547,23 +547,25 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
     bg::Mat4f fin = bg::Mat4f::identity();
     int it = 0;
     if (ns >= 3 && nt > 0) {
-        // device: src double buffer (moved in place by each iteration's kernel), best double buffer
+        // device: target then source in one staging buffer (one H2D copy), src double buffer
+        // (moved by each iteration's kernel)
         HIPCHK(c->isrc.ensure(6 * (size_t)ns), "alloc icp src");
-        HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
-        HIPCHK(c->ibest.ensure(2 * (size_t)ns), "alloc icp best");
-        HIPCHK(c->itgt3.ensure(3 * (size_t)std::max(nt, 1)), "alloc icp staging");
-        HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
-        HIPCHK(c->p_src.ensure(3 * (size_t)ns), "alloc pinned src");
+        HIPCHK(c->itgt3.ensure(3 * ((size_t)nt + ns)), "alloc icp staging");
+        HIPCHK(c->p_tgt.ensure(3 * ((size_t)nt + ns)), "alloc pinned tgt");
         HIPCHK(c->p_best.ensure(ns), "alloc pinned best");
         std::memcpy(c->p_tgt.p, tgt, sizeof(float) * 3 * nt);
-        std::memcpy(c->p_src.p, src, sizeof(float) * 3 * ns);
-        HIPCHK(hipMemcpyAsync(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * nt, hipMemcpyHostToDevice, c->stream),
-               "H2D tgt");
-        HIPCHK(hipMemcpyAsync(c->isrc.p, c->p_src.p, sizeof(float) * 3 * ns, hipMemcpyHostToDevice, c->stream),
-               "H2D src");
-        HIPCHK(hipMemsetAsync(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
-        HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
+        std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
+        HIPCHK(hipMemcpyAsync(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * ((size_t)nt + ns), hipMemcpyHostToDevice,
+                              c->stream),
+               "H2D icp points");
+        const float* d_src0 = c->itgt3.p + 3 * (size_t)nt;
         if (c->opt_icp_dev) {
+            HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
+            HIPCHK(c->ibest.ensure(2 * (size_t)ns), "alloc icp best");
+            HIPCHK(hipMemcpyAsync(c->isrc.p, d_src0, sizeof(float) * 3 * ns, hipMemcpyDeviceToDevice, c->stream),
+                   "icp src");
+            HIPCHK(hipMemsetAsync(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
+            HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
             // max_iter (NN, update) pairs queued at once; converged iterations return immediately
             HIPCHK(c->istate.ensure(1), "alloc icp state");
             HIPCHK(c->p_istate.ensure(1), "alloc pinned icp state");
@@ -602,14 +604,12 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         while (true) {
             const int b = it & 1;
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-            HIPCHK(launch_icp_iter(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1), Ts.m, it > 0,
-                                   ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b, c->ibest.p + (size_t)ns * (b ^ 1),
+            // one launch per iteration; the NN keys land in pinned host memory (no copy)
+            const float* s_in = it == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
+            HIPCHK(launch_icp_wave(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt, c->p_best.p,
                                    c->stream),
                    "icp iteration");
             c->stage_end(sg14);
-            HIPCHK(hipMemcpyAsync(c->p_best.p, c->ibest.p + (size_t)ns * b, sizeof(unsigned long long) * ns,
-                                  hipMemcpyDeviceToHost, c->stream),
-                   "D2H nn");
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
             for (int i = 0; i < ns; ++i) {
                 const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);

@@ -90,6 +90,54 @@ __global__ void __launch_bounds__(ICP_THREADS) k_icp_iter(const float* __restric
     if (i < ns) atomicMin(&best[i], m);
 }
 
+// One ICP iteration, wave per source point: the previous step T is applied (same float expression
+// as the host's bg::xform; the moved point goes to src_out), the 64 lanes stride over the targets
+// with 4 float4 loads in flight, and the packed (d2 bits << 32 | target index) minimum is reduced
+// in the wave and stored by lane 0 straight into best_out, which may be pinned host memory: no
+// atomics, no reset of a best array and no device-to-host copy between the iterations.
+__global__ void __launch_bounds__(256) k_icp_wave(const float* __restrict__ src_in, float* __restrict__ src_out,
+                                                  Xf16 T, int apply, int ns, const float* __restrict__ tgt, int nt,
+                                                  unsigned long long* __restrict__ best_out) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
+    const int lane = lane_id();
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= ns) return;
+    const float x = src_in[3 * i], y = src_in[3 * i + 1], z = src_in[3 * i + 2];
+    float qx = x, qy = y, qz = z;
+    if (apply) {
+        qx = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
+        qy = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
+        qz = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
+    }
+    if (lane == 0) {
+        src_out[3 * i] = qx; src_out[3 * i + 1] = qy; src_out[3 * i + 2] = qz;
+    }
+    unsigned long long m = ~0ull;
+    int j = lane;
+    for (; j + 192 < nt; j += 256) {
+        float p[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float* t3 = tgt + 3 * (size_t)(j + 64 * u);
+            p[u][0] = t3[0]; p[u][1] = t3[1]; p[u][2] = t3[2];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float d2 = d2_flann(qx, qy, qz, p[u][0], p[u][1], p[u][2]);
+            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)(j + 64 * u);
+            m = key < m ? key : m;
+        }
+    }
+    for (; j < nt; j += 64) {
+        const float* t3 = tgt + 3 * (size_t)j;
+        const float d2 = d2_flann(qx, qy, qz, t3[0], t3[1], t3[2]);
+        const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)j;
+        m = key < m ? key : m;
+    }
+    m = wave_min_u64(m);
+    if (lane == 0) best_out[i] = m;
+}
+
 // ---- device-resident ICP loop: the host enqueues max_iter (NN, update) pairs and syncs once.
 // The update kernel restates ctx_icp's host step exactly (bg::umeyama<float> sequential sums,
 // bm::umeyama_finish, bg::mul, PCL's convergence tests); once converged, later launches return.
@@ -322,6 +370,15 @@ hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16
     for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
     bsk::k_icp_iter<<<dim3(qb, splits), ICP_THREADS, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, tile, best,
                                                               best_next);
+    return hipGetLastError();
+}
+
+hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
+                           int nt, unsigned long long* best_out, hipStream_t s) {
+    if (ns <= 0 || nt <= 0) return hipSuccess;
+    bsk::Xf16 T;
+    for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
+    bsk::k_icp_wave<<<(ns + 3) / 4, 256, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, best_out);
     return hipGetLastError();
 }
 

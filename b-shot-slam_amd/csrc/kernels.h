@@ -38,6 +38,9 @@ hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, in
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
+// wave per source point, results stored straight to best_out (may be pinned host memory)
+hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
+                           int nt, unsigned long long* best_out, hipStream_t s);
 hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,
                            int nt, unsigned long long* best, unsigned long long* best_next, hipStream_t s);
 // device-resident ICP loop state (ctx_icp with opt icp_dev): step T, accumulated fin, PCL
