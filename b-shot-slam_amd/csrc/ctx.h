@@ -144,10 +144,17 @@ struct bshot_ctx {
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
     DBuf<unsigned int> sbh, sbst;  // bucketed gather: per-keypoint d2 histogram and bucket starts
+    // lookahead keypoint gather (ctx_gather_kps_async): own index and staging buffers
+    DBuf<int> kidx;
+    PinBuf<int> p_kidx;
+    PinBuf<float> p_kps3;
     // tuning knob "describe2": 2 load-balanced SHOT with the bucketed gather + in-bucket rank
     // (default), 1 load-balanced SHOT with the piece sort, 0 wave/WG per keypoint
     int opt_describe2 = 2;
     int opt_chunk_blocks = 0;  // grid cap of the 64-rank chunk kernels (0: one block per 4 chunks)
+    int opt_dev_plan = 1;      // describe planned on the device (no mid-describe host sync) once sizes are known
+    bool plan_on_host = false;  // next describe: plan on the host (after a device-plan overflow)
+    long long seg_hint = 0;     // largest neighbourhood total seen (device-plan capacities)
     int ladder_mode(const CloudState& s) const { return s.fine_ladder ? (opt_ladder_front ? 2 : 1) : 0; }
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag
@@ -224,10 +231,15 @@ int ctx_sync_main(bshot_ctx* c);
 // explicit-cloud / explicit-stream variants (the lookahead task runs them on the side stream)
 int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1 = false);
+// after a describe's error word reached the host (err[0..3] as copied from c->errw): true when the
+// describe must be run again -- errw bit 16, a device plan over capacity (the re-run plans on the
+// host; the capacity hint grows to the total the device counted)
+bool ctx_describe_replan(bshot_ctx* c, const int* err);
 int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst);
 int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst,
                        float* out);
 // device gather of cloud points -> host (pinned staging), synchronous
 int ctx_gather_host(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst, float* out);
+int ctx_gather_kps_async(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k);
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters);
 }  // namespace bsh

@@ -382,8 +382,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
                "zero normals");
     c->normals_size = n;
     if (k <= 0) return BSHOT_OK;
-    HIPCHK(c->errw.ensure(1), "alloc err");
-    HIPCHK(hipMemsetAsync(c->errw.p, 0, sizeof(int), st), "memset err");
+    // errw: [0] error bits (2 normals overflow, 8 sort piece overflow, 16 device plan over
+    // capacity), [2..3] the neighbourhood total as planned on the device
+    HIPCHK(c->errw.ensure(4), "alloc err");
+    HIPCHK(hipMemsetAsync(c->errw.p, 0, 4 * sizeof(int), st), "memset err");
     HIPCHK(c->counts.ensure(k), "alloc counts");
     HIPCHK(c->offs.ensure(k + 1), "alloc offs");
     HIPCHK(c->rf.ensure(9 * (size_t)k), "alloc rf");
@@ -402,6 +404,54 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
         HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
         HIPCHK(c->sbst.ensure(1024 * (size_t)k), "alloc bucket starts");
     }
+    if (bucketed && c->opt_dev_plan && !c->plan_on_host && k <= 8192 && c->seg_hint > 0) {
+        // the whole describe queued without a host round trip: the plan (segment offsets, chunk
+        // bases, LPT order) is computed on the device against capacities sized from the largest
+        // neighbourhood total seen so far (+25%); an overflow (errw bit 16) makes the caller
+        // re-run this describe with the host-side plan
+        const long long seg_cap = c->seg_hint + c->seg_hint / 4 + 65536;
+        const int chunk_cap = (int)(seg_cap / 64) + k + 1;
+        HIPCHK(c->seg.ensure((size_t)seg_cap), "alloc seg");
+        HIPCHK(c->segtmp.ensure((size_t)seg_cap), "alloc segtmp");
+        HIPCHK(c->cb.ensure((size_t)k + 1), "alloc cb");
+        HIPCHK(c->perm.ensure(k), "alloc perm");
+        HIPCHK(c->owner.ensure((size_t)chunk_cap), "alloc owner");
+        HIPCHK(c->csum.ensure(8 * (size_t)chunk_cap), "alloc csum");
+        HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
+        HIPCHK(c->okf.ensure(k), "alloc okf");
+        HIPCHK(c->signs.ensure(2 * (size_t)chunk_cap), "alloc signs");
+        HIPCHK(c->recS.ensure(320 * (size_t)chunk_cap), "alloc records");
+        HIPCHK(c->recV.ensure(320 * (size_t)chunk_cap), "alloc records");
+        HIPCHK(launch_shot_count_plan(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->sbh.p, seg_cap, chunk_cap,
+                                      c->offs.p, c->cb.p, c->perm.p, c->errw.p, st),
+               "shot count + plan");
+        c->stage_end(sg5, st);
+        const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
+        HIPCHK(launch_shot_gather_b(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->sbh.p, c->sbst.p, c->seg.p, st,
+                                    c->errw.p),
+               "shot gather");
+        c->stage_end(sg6, st);
+        Describe2Args A;
+        A.k = k; A.n_plan = 0; A.n_chunks = chunk_cap; A.R = R;
+        A.plan = nullptr; A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p;
+        A.pts4 = S.pts4.p; A.normals = c->normals.p;
+        A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
+        A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
+        A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
+        A.bstart = c->sbst.p;
+        A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
+        const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
+        HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
+        c->stage_end(sg10, st);
+        const int sg11 = c->stage_begin(BSHOT_STAGE_LRF, st);
+        HIPCHK(launch_describe2(A, 1, st), "describe2 lrf");
+        c->stage_end(sg11, st);
+        const int sg12 = c->stage_begin(BSHOT_STAGE_HIST, st);
+        HIPCHK(launch_describe2(A, 2, st), "describe2 hist");
+        c->stage_end(sg12, st);
+        return BSHOT_OK;
+    }
+    c->plan_on_host = false;
     HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st, bucketed ? c->sbh.p : nullptr),
            "shot count");
     c->stage_end(sg5, st);
@@ -412,6 +462,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(hipStreamSynchronize(st), "sync offs");
     const long long total = c->p_offs.p[k];
     c->work[0] = total;
+    if (total > c->seg_hint) c->seg_hint = total;
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
     const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
@@ -497,6 +548,15 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     return BSHOT_OK;
 }
 
+bool ctx_describe_replan(bshot_ctx* c, const int* err) {
+    if (!(err[0] & 16)) return false;
+    long long total = 0;
+    std::memcpy(&total, err + 2, sizeof(total));
+    if (total > c->seg_hint) c->seg_hint = total;
+    c->plan_on_host = true;
+    return true;
+}
+
 int ctx_describe_dev(bshot_ctx* c, int k, bool force_v1) { return ctx_describe_on(c, c->cs, c->stream, k, force_v1); }
 
 int ctx_match_dev(bshot_ctx* c, int na, int nb) {
@@ -531,6 +591,22 @@ int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h
     HIPCHK(hipMemcpyAsync(c->p_g3.p, dst.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, st), "D2H gather");
     HIPCHK(hipStreamSynchronize(st), "sync gather");
     std::memcpy(out, c->p_g3.p, sizeof(float) * 3 * k);
+    return BSHOT_OK;
+}
+
+// keypoint gather for the lookahead describe, asynchronous: H2D indices, gather into c->kps and
+// D2H of the coordinates into c->p_kps3 are queued on st with buffers of their own (the ISS gather
+// runs concurrently); the caller syncs st before reading c->p_kps3
+int ctx_gather_kps_async(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k) {
+    HIPCHK(c->kidx.ensure(k > 0 ? k : 1), "alloc kidx");
+    HIPCHK(c->kps.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc kps");
+    if (k <= 0) return BSHOT_OK;
+    HIPCHK(c->p_kidx.ensure(k), "alloc pinned kidx");
+    HIPCHK(c->p_kps3.ensure(3 * (size_t)k), "alloc pinned kps");
+    std::memcpy(c->p_kidx.p, h_idx, sizeof(int) * k);
+    HIPCHK(hipMemcpyAsync(c->kidx.p, c->p_kidx.p, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D kidx");
+    HIPCHK(launch_gather(S.pts4.p, c->kidx.p, k, c->kps.p, st), "gather kps");
+    HIPCHK(hipMemcpyAsync(c->p_kps3.p, c->kps.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, st), "D2H kps");
     return BSHOT_OK;
 }
 
@@ -707,7 +783,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
     c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
-    c->sbh.release(); c->sbst.release();
+    c->sbh.release(); c->sbst.release(); c->kidx.release(); c->p_kidx.release(); c->p_kps3.release();
     c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
@@ -817,29 +893,27 @@ int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf
     if (k > 0) HIPCHK(hipMemcpyAsync(c->kps.p, kps, sizeof(float) * 3 * k, hipMemcpyHostToDevice, c->stream), "H2D kps");
     int rc = ctx_describe_dev(c, k);
     if (rc) return rc;
-    int herr = 0;
-    if (k > 0) {
-        HIPCHK(hipMemcpyAsync(bits, c->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost, c->stream), "D2H bits");
-        if (shot) HIPCHK(hipMemcpyAsync(shot, c->shot.p, sizeof(float) * 352 * k, hipMemcpyDeviceToHost, c->stream), "D2H shot");
-        if (rf) HIPCHK(hipMemcpyAsync(rf, c->rf.p, sizeof(float) * 9 * k, hipMemcpyDeviceToHost, c->stream), "D2H rf");
-        HIPCHK(hipMemcpyAsync(&herr, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H err");
-    }
-    HIPCHK(hipStreamSynchronize(c->stream), "sync describe");
-    c->resolve_events();
-    if (herr & 8) {
-        // a describe2 sort piece overflowed its LDS buffer (pathological duplicate d2): rerun the
-        // SHOT stages one workgroup per keypoint
-        rc = ctx_describe_dev(c, k, true);
-        if (rc) return rc;
+    int herr[4] = {0, 0, 0, 0};
+    for (int attempt = 0; attempt < 3; ++attempt) {
         if (k > 0) {
             HIPCHK(hipMemcpyAsync(bits, c->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost, c->stream), "D2H bits");
             if (shot) HIPCHK(hipMemcpyAsync(shot, c->shot.p, sizeof(float) * 352 * k, hipMemcpyDeviceToHost, c->stream), "D2H shot");
             if (rf) HIPCHK(hipMemcpyAsync(rf, c->rf.p, sizeof(float) * 9 * k, hipMemcpyDeviceToHost, c->stream), "D2H rf");
-            HIPCHK(hipMemcpyAsync(&herr, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H err");
+            HIPCHK(hipMemcpyAsync(herr, c->errw.p, 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H err");
         }
         HIPCHK(hipStreamSynchronize(c->stream), "sync describe");
+        c->resolve_events();
+        if (k > 0 && ctx_describe_replan(c, herr)) {
+            // the device-side plan ran out of capacity: again, planned on the host
+            if ((rc = ctx_describe_dev(c, k))) return rc;
+            continue;
+        }
+        if (!(herr[0] & 8)) break;
+        // a describe2 sort piece overflowed its LDS buffer (pathological duplicate d2): rerun the
+        // SHOT stages one workgroup per keypoint
+        if ((rc = ctx_describe_dev(c, k, true))) return rc;
     }
-    if (herr & 2) return c->fail("normals: neighbourhood with too many exactly tied boundary keys (kNN list overflow)", BSHOT_ECAP);
+    if (herr[0] & 2) return c->fail("normals: neighbourhood with too many exactly tied boundary keys (kNN list overflow)", BSHOT_ECAP);
     return BSHOT_OK;
 }
 
@@ -964,6 +1038,8 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
+    else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;
+    else if (k == "dev_plan_hint") c->seg_hint = value < 0 ? 0 : value;  // tests: force / avoid a re-plan
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);

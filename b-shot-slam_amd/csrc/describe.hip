@@ -63,6 +63,74 @@ __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __r
     }
 }
 
+// Device-side describe plan (no host round trip): offs = exclusive scan of counts (segment
+// starts, offs[k] = total), cb = exclusive scan of ceil(counts / 64) (chunk bases), perm = keypoints
+// by descending neighbourhood size, ties by index (the apply's LPT launch order; results do not
+// depend on it). When the total or the chunk count exceed the preallocated capacities, err |= 16
+// and every segment / chunk range is emptied so no later kernel writes out of bounds; the host
+// then re-plans on its side. One workgroup, k <= DP_MAXK.
+#define DP_MAXK 8192
+__global__ void __launch_bounds__(1024) k_desc_plan(const int* __restrict__ counts, int k, long long seg_cap,
+                                                    int chunk_cap, long long* __restrict__ offs, int* __restrict__ cb,
+                                                    int* __restrict__ perm, int* __restrict__ err) {
+    __shared__ long long ps[1024];
+    __shared__ int pc[1024];
+    __shared__ unsigned long long keys[DP_MAXK];
+    __shared__ int bad;
+    const int t = threadIdx.x;
+    const int per = (k + 1023) / 1024;
+    const int b = t * per, e = min(k, b + per);
+    long long s = 0;
+    int sc = 0;
+    for (int i = b; i < e; ++i) { s += counts[i]; sc += (counts[i] + 63) / 64; }
+    ps[t] = s;
+    pc[t] = sc;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const long long v = t >= off ? ps[t - off] : 0;
+        const int w = t >= off ? pc[t - off] : 0;
+        __syncthreads();
+        ps[t] += v;
+        pc[t] += w;
+        __syncthreads();
+    }
+    if (t == 0) bad = (ps[1023] > seg_cap || pc[1023] > chunk_cap) ? 1 : 0;
+    __syncthreads();
+    long long run = ps[t] - s;
+    int runc = pc[t] - sc;
+    for (int i = b; i < e; ++i) {
+        offs[i] = bad ? 0 : run;
+        cb[i] = bad ? 0 : runc;
+        run += counts[i];
+        runc += (counts[i] + 63) / 64;
+    }
+    if (t == 1023) {
+        offs[k] = bad ? 0 : ps[1023];
+        cb[k] = bad ? 0 : pc[1023];
+        *reinterpret_cast<long long*>(err + 2) = ps[1023];  // err is 16-byte aligned (errw)
+        if (bad) atomicOr(err, 16);
+    }
+    // perm: bitonic sort of (~count << 32 | q) ascending = count descending, q ascending
+    int P = 1;
+    while (P < k) P <<= 1;
+    for (int i = t; i < P; i += 1024)
+        keys[i] = i < k ? (((unsigned long long)(~(unsigned int)counts[i])) << 32) | (unsigned int)i : ~0ull;
+    __syncthreads();
+    for (int sz = 2; sz <= P; sz <<= 1)
+        for (int st = sz >> 1; st > 0; st >>= 1) {
+            for (int i = t; i < P; i += 1024) {
+                const int j = i ^ st;
+                if (j > i) {
+                    const unsigned long long x = keys[i], y = keys[j];
+                    const bool up = (i & sz) == 0;
+                    if ((x > y) == up) { keys[i] = y; keys[j] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = t; i < k; i += 1024) perm[i] = (int)(keys[i] & 0xFFFFFFFFu);
+}
+
 // exclusive scan of counts[0, k) by one workgroup of 1024 threads; offs[k] = total
 __global__ void __launch_bounds__(1024) k_excl_scan(const int* __restrict__ counts, int k,
                                                     long long* __restrict__ offs) {
@@ -120,7 +188,8 @@ __global__ void __launch_bounds__(256) k_shot_gather_b(GridView g, const float* 
                                                        const long long* __restrict__ offs,
                                                        const unsigned int* __restrict__ bh,
                                                        unsigned int* __restrict__ bstart,
-                                                       unsigned long long* __restrict__ seg) {
+                                                       unsigned long long* __restrict__ seg,
+                                                       const int* __restrict__ err) {
     __shared__ CandLds lds[4];
     __shared__ unsigned int cur[4][SG_BUCKETS];
     const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -129,6 +198,7 @@ __global__ void __launch_bounds__(256) k_shot_gather_b(GridView g, const float* 
     const float sc = (float)SG_BUCKETS / R2;
     unsigned int* cu = cur[wave];
     constexpr int PER = SG_BUCKETS / 64;
+    if (err && (*err & 16)) return;  // device plan overflowed its capacity: the host re-plans
     for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         if (!(__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))) continue;
@@ -642,10 +712,21 @@ hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R
     return hipGetLastError();
 }
 
-hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
-                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s) {
+hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, float R, int* counts, unsigned int* bh,
+                                  long long seg_cap, int chunk_cap, long long* offs, int* cb, int* perm, int* err,
+                                  hipStream_t s) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_gather_b<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg);
+    if (k > DP_MAXK) return hipErrorInvalidValue;
+    bsk::k_shot_count<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, counts, bh);
+    bsk::k_desc_plan<<<1, 1024, 0, s>>>(counts, k, seg_cap, chunk_cap, offs, cb, perm, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
+                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s,
+                                const int* err) {
+    if (k <= 0) return hipSuccess;
+    bsk::k_shot_gather_b<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg, err);
     return hipGetLastError();
 }
 

@@ -23,7 +23,13 @@ hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R
                               unsigned long long* seg, hipStream_t s);
 // bucket-grouped gather (bstart: per-keypoint bucket starts) and the in-bucket rank that sorts it
 hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
-                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s);
+                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s,
+                                const int* err = nullptr);
+// count + device-side plan (offs, chunk bases cb, LPT perm) against preallocated capacities;
+// err |= 16 (and empty ranges) when they do not suffice. k <= 8192.
+hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, float R, int* counts, unsigned int* bh,
+                                  long long seg_cap, int chunk_cap, long long* offs, int* cb, int* perm, int* err,
+                                  hipStream_t s);
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
                             hipStream_t s, int max_blocks = 0);

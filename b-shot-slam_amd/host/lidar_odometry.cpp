@@ -166,8 +166,9 @@ void LidarOdometry::runAhead(Lookahead& la) {
     la.kidx.resize(k);
     la.kr.resize(k);
     la.kps.resize(k);
-    if (k > 0 && bsh::ctx_gather_host_on(c, S, c->side, la.kidx.data(), k, c->kps, &la.kps[0][0]) != BSHOT_OK)
-        fail("lookahead gather");
+    // queued without a sync: the describe below follows it on the side stream, and the coordinates
+    // are copied out after the side stream's final sync
+    if (bsh::ctx_gather_kps_async(c, S, c->side, la.kidx.data(), k) != BSHOT_OK) fail("lookahead gather");
     la.ms[0] = (float)t_ex.toc();
     TicToc t_d;
     // describe is queued on the side stream; while it runs, ISS (own stream) is collected
@@ -190,20 +191,27 @@ void LidarOdometry::runAhead(Lookahead& la) {
     }
     la.ms[1] = (float)t_iss.toc();
     c->hmark("W_iss_done");
-    if (c->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) != hipSuccess || c->p_err.ensure(1) != hipSuccess)
+    if (c->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) != hipSuccess || c->p_err.ensure(4) != hipSuccess)
         fail("alloc pinned");
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    for (int attempt = 0; attempt < 3; ++attempt) {
         c->p_err.p[0] = 0;
         if (k > 0 && (hipMemcpyAsync(c->p_bits.p, c->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
                                      c->side) != hipSuccess ||
-                      hipMemcpyAsync(c->p_err.p, c->errw.p, sizeof(int), hipMemcpyDeviceToHost, c->side) != hipSuccess))
+                      hipMemcpyAsync(c->p_err.p, c->errw.p, 4 * sizeof(int), hipMemcpyDeviceToHost, c->side) !=
+                          hipSuccess))
             fail("D2H bits");
         if (hipStreamSynchronize(c->side) != hipSuccess) fail("lookahead sync");
+        if (k > 0 && bsh::ctx_describe_replan(c, c->p_err.p)) {
+            // the device-side plan ran out of capacity: again, planned on the host
+            if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe (replan)");
+            continue;
+        }
         if (!(c->p_err.p[0] & 8)) break;
         if (bsh::ctx_describe_on(c, S, c->side, k, true) != BSHOT_OK) fail("lookahead describe (fallback)");
     }
     if (k > 0 && (c->p_err.p[0] & 2)) throw std::runtime_error("normals neighbourhood overflow");
     la.words.assign(c->p_bits.p, c->p_bits.p + 11 * (size_t)k);
+    if (k > 0) std::memcpy(&la.kps[0][0], c->p_kps3.p, sizeof(float) * 3 * k);
     c->hmark("W_done");
     la.ms[2] = (float)t_d.toc();
 
@@ -303,19 +311,24 @@ void LidarOdometry::computeDescriptors() {
     }
     check(bsh::ctx_describe_dev(ctx_, k), "describe");
     check(ctx_->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned bits");
-    check(ctx_->p_err.ensure(1) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned err");
+    check(ctx_->p_err.ensure(4) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned err");
     const uint32_t* words = ctx_->p_bits.p;
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    for (int attempt = 0; attempt < 3; ++attempt) {
         ctx_->p_err.p[0] = 0;
         if (k > 0) {
             if (hipMemcpyAsync(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
                                ctx_->stream) != hipSuccess ||
-                hipMemcpyAsync(ctx_->p_err.p, ctx_->errw.p, sizeof(int), hipMemcpyDeviceToHost, ctx_->stream) !=
+                hipMemcpyAsync(ctx_->p_err.p, ctx_->errw.p, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx_->stream) !=
                     hipSuccess)
                 check(BSHOT_EHIP, "D2H bits");
         }
         check(bsh::ctx_sync_main(ctx_), "describe sync");
         ctx_->resolve_events();
+        if (k > 0 && bsh::ctx_describe_replan(ctx_, ctx_->p_err.p)) {
+            // the device-side plan ran out of capacity: again, planned on the host
+            check(bsh::ctx_describe_dev(ctx_, k), "describe (replan)");
+            continue;
+        }
         if (!(ctx_->p_err.p[0] & 8)) break;
         // a load-balanced sort piece overflowed (pathological duplicate d2): one workgroup per keypoint
         check(bsh::ctx_describe_dev(ctx_, k, true), "describe (fallback)");

@@ -87,6 +87,23 @@ def test_describe_parity(ctx, cloud, sr_ref, k, d2):
     ctx.set_option("describe2", 2)
 
 
+@pytest.mark.parametrize("hint", [1 << 26, 1])
+def test_describe_device_plan(ctx, cloud, sr_ref, hint):
+    """Describe planned on the device (capacity hint ample) and the re-plan after a device plan
+    overflows its capacity (hint 1): both give the host-planned bits."""
+    ridx, rrat = sr_ref
+    kidx, _ = orc.select_topk(ridx, rrat, 2048)
+    kps = cloud[kidx]
+    ctx.set_cloud(cloud)
+    ctx.set_option("dev_plan", 0)
+    ref_bits, ref_shot, _ = ctx.describe(kps)
+    ctx.set_option("dev_plan", 1)
+    ctx.set_option("dev_plan_hint", hint)
+    bits, shot, _ = ctx.describe(kps)
+    np.testing.assert_array_equal(bits, ref_bits)
+    np.testing.assert_array_equal(shot.view(np.uint32), ref_shot.view(np.uint32))
+
+
 def test_match_exact_random_and_ties(ctx):
     rng = np.random.default_rng(7)
     for na, nb in ((1, 1), (5, 300), (600, 1800), (2048, 4096), (257, 1)):
