@@ -15,9 +15,9 @@ LIB_PATH = os.environ.get("BSHOT_LIB") or os.path.join(HERE, "lib", "libbshot_am
 SYNTH_PATH = os.path.join(HERE, "lib", "libbshot_synth.so")
 P = ctypes.c_void_p
 
-NSTAGES = 11
+NSTAGES = 12
 STAGE_NAMES = ["grid", "seg_ratio", "iss", "normals", "shot_gather", "shot_sort", "lrf", "shot_hist", "match", "icp",
-               "ransac"]
+               "ransac", "preprocess"]
 
 
 class Params(ctypes.Structure):
@@ -64,7 +64,38 @@ ABI_SYMBOLS = [
     "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
     "bshot_odom_set_option", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
+    "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
 ]
+
+# velodyne::Laser (include/VelodyneCapture.h:43-50) == bshot_laser: 32 B, int64 time at offset 24
+LASER_DTYPE = np.dtype({"names": ["azimuth", "vertical", "distance", "intensity", "id", "time"],
+                        "formats": ["<f8", "<f8", "<u2", "u1", "u1", "<i8"],
+                        "offsets": [0, 8, 16, 18, 19, 24], "itemsize": 32})
+# bshot_pre_cell: one getRangeImage entry with its getRemoveMap / getSelMap values (-1: no entry)
+CELL_DTYPE = np.dtype([("azimuth", "<f8"), ("vertical", "<f8"), ("distance", "<f8"), ("rm", "<i4"), ("sel", "<i4")])
+# HDL-32E vertical table (include/VelodyneCapture.h:572), laser-id order
+HDL32_VERTICAL = [-30.67, -9.3299999, -29.33, -8.0, -28, -6.6700001, -26.67, -5.3299999, -25.33, -4.0, -24.0,
+                  -2.6700001, -22.67, -1.33, -21.33, 0.0, -20.0, 1.33, -18.67, 2.6700001, -17.33, 4.0, -16,
+                  5.3299999, -14.67, 6.6700001, -13.33, 8.0, -12.0, 9.3299999, -10.67, 10.67]
+
+
+class PreParams(ctypes.Structure):
+    _fields_ = [("vert_init", ctypes.c_double), ("lowpt_th", ctypes.c_double), ("have_sel_list", ctypes.c_int),
+                ("save_sel", ctypes.c_int)]
+
+
+def pre_params(vert_init=-0.6, lowpt_th=-2000.0, have_sel_list=False, save_sel=True):
+    return PreParams(vert_init, lowpt_th, 1 if have_sel_list else 0, 1 if save_sel else 0)
+
+
+def sensor_vertical_angles(sensor):
+    """Vertical angle table (degrees) of synth_lasers' sensors, as capture.getVerticalAngle() gives it."""
+    if sensor == 0:
+        return [2.0 + (-8.33 - 2.0) * i / 31.0 for i in range(32)] + \
+               [-8.83 + (-24.33 + 8.83) * i / 31.0 for i in range(32)]
+    if sensor == 1:
+        return [-25.0 + 40.0 * i / 127.0 for i in range(128)]
+    return list(HDL32_VERTICAL)
 
 _lib = None
 _synth = None
@@ -168,6 +199,34 @@ class Context:
         out = np.zeros(max(self.n, 1), np.int32)
         m = ctypes.c_int()
         self._chk(self.L.bshot_iss(self.h, _ptr(out), len(out), ctypes.byref(m)), "iss")
+        return out[: m.value].copy()
+
+    def preprocess(self, lasers, vert_deg, vert_init=-0.6, lowpt_th=-2000.0, sel=None, save_sel=True):
+        """myslam::Preprocessor::run on the GPU (bshot_preprocess): laser records -> kept points."""
+        lasers = np.ascontiguousarray(lasers, dtype=LASER_DTYPE)
+        vd = np.ascontiguousarray(vert_deg, dtype=np.float64)
+        pp = pre_params(vert_init, lowpt_th, sel is not None, save_sel)
+        sa = np.ascontiguousarray(sel if sel is not None else np.zeros(0), dtype=np.int32)
+        n = len(lasers)
+        out = np.zeros((max(n, 1), 3), np.float32)
+        m = ctypes.c_int()
+        self._chk(self.L.bshot_preprocess(self.h, _ptr(lasers), n, _ptr(vd), len(vd), ctypes.byref(pp), _ptr(sa),
+                                          len(sa), _ptr(out), n, ctypes.byref(m)), "preprocess")
+        return out[: m.value].copy()
+
+    def preprocess_device(self, d_lasers, n, vert_deg, d_xyz, cap, vert_init=-0.6, lowpt_th=-2000.0):
+        vd = np.ascontiguousarray(vert_deg, dtype=np.float64)
+        pp = pre_params(vert_init, lowpt_th)
+        m = ctypes.c_int()
+        self._chk(self.L.bshot_preprocess_device(self.h, P(d_lasers), n, _ptr(vd), len(vd), ctypes.byref(pp), None,
+                                                 0, P(d_xyz), cap, ctypes.byref(m)), "preprocess_device")
+        return m.value
+
+    def preprocess_cells(self):
+        m = ctypes.c_int()
+        self.L.bshot_preprocess_cells(self.h, None, 0, ctypes.byref(m))
+        out = np.zeros(max(m.value, 1), CELL_DTYPE)
+        self._chk(self.L.bshot_preprocess_cells(self.h, _ptr(out), len(out), ctypes.byref(m)), "preprocess_cells")
         return out[: m.value].copy()
 
     def describe(self, kps, want_shot=True):
@@ -443,6 +502,27 @@ class KeypointMap:
 
 
 # ---------------------------------------------------------------- synthetic input (not the product)
+def _synth_lib():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise RuntimeError(f"{SYNTH_PATH} not built")
+        _synth = ctypes.CDLL(SYNTH_PATH)
+    return _synth
+
+
+def synth_lasers(frame, sensor=2, seed=42, max_range=120000.0, sensor_height=2450.0):
+    """One rotation of synthetic Velodyne laser records (tools/synth.cpp synth_lasers), firing order.
+    sensor 0 HDL-64, 1 VLP-128 style, 2 HDL-32E."""
+    cap = 300000
+    buf = np.zeros(cap, LASER_DTYPE)
+    n = _synth_lib().synth_lasers(sensor, seed, frame, ctypes.c_float(max_range), ctypes.c_float(sensor_height),
+                                  _ptr(buf), cap)
+    if n < 0:
+        raise RuntimeError("synth capacity")
+    return buf[:n].copy()
+
+
 def synth_sweep(frame, sensor=0, seed=42, no_ground=False, max_range=120000.0):
     """Deterministic synthetic Velodyne sweep (b-shot-slam_amd/tools/synth.cpp), sensor frame, mm."""
     global _synth

@@ -98,6 +98,10 @@ struct CloudState {
     void release();
 };
 
+namespace bsh {
+struct PreState;  // csrc/preprocess.hip
+}
+
 struct bshot_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // main: describe, match, ICP, and everything synchronous
@@ -143,6 +147,7 @@ struct bshot_ctx {
     DBuf<float> recV;
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
+    bsh::PreState* prep = nullptr;  // GPU preprocessor state (csrc/preprocess.hip), created on first use
     DBuf<unsigned int> sbh, sbst;  // bucketed gather: per-keypoint d2 histogram and bucket starts
     // lookahead keypoint gather (ctx_gather_kps_async): own index and staging buffers
     DBuf<int> kidx;

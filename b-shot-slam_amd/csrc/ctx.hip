@@ -17,6 +17,7 @@
 #include "../host/geom.h"
 #include "ctx.h"
 #include "kernels.h"
+#include "preprocess.h"
 
 // BSHOT_TRACE=1: entry/exit trace of the C ABI calls on stderr (diagnostics only)
 static bool trace_on() {
@@ -784,6 +785,8 @@ void bshot_destroy(bshot_ctx* c) {
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
     c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
     c->sbh.release(); c->sbst.release(); c->kidx.release(); c->p_kidx.release(); c->p_kps3.release();
+    bsh::pre_free(c->prep);
+    c->prep = nullptr;
     c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);

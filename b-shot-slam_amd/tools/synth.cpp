@@ -245,4 +245,82 @@ int synth_sweep(int sensor, uint32_t scene_seed, int frame, int no_ground, float
     return n;
 }
 
+// Velodyne laser returns of one rotation (velodyne::Laser records, include/VelodyneCapture.h:43-50,
+// 32 B: azimuth deg, vertical deg, distance in 2 mm units, intensity, id, time) -- the input of the
+// preprocessor (src/preprocess.cpp:38-70). sensor: 0 HDL-64 (64 x 2048), 1 VLP-128 style
+// (128 x 2000), 2 HDL-32E (32 x 2170, the capture's vertical table, include/VelodyneCapture.h:572).
+// Records come in firing order (azimuth-major, laser id inside a firing), azimuth in the packet's
+// 0.01 deg steps; a return beyond max_range or without a hit is distance 0 (a lost point, as the
+// sensor reports it). The sensor sits sensor_height mm above the ground plane. Returns the record
+// count (or -needed when cap is too small).
+struct SynthLaser {
+    double azimuth;
+    double vertical;
+    uint16_t distance;
+    uint8_t intensity;
+    uint8_t id;
+    int64_t time;
+};
+static_assert(sizeof(SynthLaser) == 32, "velodyne::Laser layout");
+
+int synth_lasers(int sensor, uint32_t scene_seed, int frame, float max_range, float sensor_height, void* out_v,
+                 int cap) {
+    SynthLaser* out = static_cast<SynthLaser*>(out_v);
+    auto sc = get_scene(scene_seed);
+    std::vector<double> beams;
+    int A;
+    if (sensor == 0) {
+        A = 2048;
+        for (int i = 0; i < 32; ++i) beams.push_back(2.0 + (-8.33 - 2.0) * i / 31.0);
+        for (int i = 0; i < 32; ++i) beams.push_back(-8.83 + (-24.33 + 8.83) * i / 31.0);
+    } else if (sensor == 1) {
+        A = 2000;
+        for (int i = 0; i < 128; ++i) beams.push_back(-25.0 + 40.0 * i / 127.0);
+    } else {
+        A = 2170;
+        beams = {-30.67, -9.3299999, -29.33, -8.0, -28, -6.6700001, -26.67, -5.3299999, -25.33, -4.0, -24.0,
+                 -2.6700001, -22.67, -1.33, -21.33, 0.0, -20.0, 1.33, -18.67, 2.6700001, -17.33, 4.0, -16,
+                 5.3299999, -14.67, 6.6700001, -13.33, 8.0, -12.0, 9.3299999, -10.67, 10.67};
+    }
+    const int V = (int)beams.size();
+    if ((long long)A * V > cap) return -(A * V);
+    const double yaw = 0.5 * M_PI / 180.0 * std::sin(2 * M_PI * frame / 200.0);
+    const double cy = std::cos(yaw), sy = std::sin(yaw);
+    const double o[3] = {0.0, 800.0 * frame, sensor_height - 1730.0};
+    std::vector<const Prim*> near;
+    for (const Prim& p : sc->prims)
+        if (p.ymax >= o[1] - max_range - 1000 && p.ymin <= o[1] + max_range + 1000) near.push_back(&p);
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < A; ++j) {
+        const int rot = (int)std::lround(36000.0 * j / A) % 36000;  // rotational position, 0.01 deg
+        const double az_deg = rot / 100.0;
+        const double az = az_deg * M_PI / 180.0;
+        for (int b = 0; b < V; ++b) {
+            const double v = beams[b] * M_PI / 180.0;
+            const double ds[3] = {std::cos(v) * std::sin(az), std::cos(v) * std::cos(az), std::sin(v)};
+            const double d[3] = {cy * ds[0] - sy * ds[1], sy * ds[0] + cy * ds[1], ds[2]};
+            double best = 1e300;
+            if (d[2] < -1e-12) best = (-1730.0 - o[2]) / d[2];
+            for (const Prim* p : near) {
+                bool g;
+                const double t = hit(*p, o, d, g);
+                if (t < best) best = t;
+            }
+            const uint64_t h = splitmix(((uint64_t)scene_seed << 40) ^ ((uint64_t)(frame + 1000) << 20) ^ (uint64_t)(j * V + b));
+            const double u1 = u01(h), u2 = u01(splitmix(h));
+            const double g = std::sqrt(-2.0 * std::log(u1)) * std::cos(2 * M_PI * u2);
+            double r = best >= 1e299 ? 0.0 : std::round((best + 20.0 * g) / 2.0) * 2.0;
+            if (!(r < max_range) || r <= 0) r = 0;
+            SynthLaser& L = out[(size_t)j * V + b];
+            L.azimuth = az_deg;
+            L.vertical = beams[b];
+            L.distance = (uint16_t)(r / 2);
+            L.intensity = (uint8_t)(splitmix(h) & 0xFF);
+            L.id = (uint8_t)b;
+            L.time = frame;
+        }
+    }
+    return A * V;
+}
+
 }  // extern "C"

@@ -113,6 +113,43 @@ int bshot_ransac_dev(bshot_ctx* c, const float* src, int ns, const float* tgt, i
 int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T_out,
               int* iters);
 
+/* ---- Point-cloud preprocessor (myslam::Preprocessor, include/preprocess.h:7-57,
+ *      src/preprocess.cpp:38-227): Velodyne laser returns -> range image (azimuth x vertical) ->
+ *      ground removal -> occluded-edge removal -> point cloud in the reference's map order
+ *      (azimuth, then vertical ascending). ------------------------------------------------------ */
+typedef struct {           /* velodyne::Laser (include/VelodyneCapture.h:43-50), same 32-B layout */
+    double azimuth;        /* degrees */
+    double vertical;       /* degrees */
+    uint16_t distance;     /* 2 mm units (src/preprocess.cpp:45) */
+    uint8_t intensity;
+    uint8_t id;
+    int64_t time;
+} bshot_laser;
+typedef struct {
+    double vert_init;      /* setVerticalInitial, radians; default -0.6 (src/preprocess.cpp:7) */
+    double lowpt_th;       /* setLowPtThreshold, mm; default -2000 (include/preprocess.h:43) */
+    int have_sel_list;     /* haveSelectList; default 0 */
+    int save_sel;          /* saveSelectPoints; default 1 */
+} bshot_pre_params;
+typedef struct {           /* one getRangeImage entry with its getRemoveMap / getSelMap values */
+    double azimuth, vertical, distance; /* radians, radians, mm */
+    int32_t rm;            /* 0 kept, 1 ground / lost / vert_init, 2 self-car, 3 occluded; -1 no entry */
+    int32_t sel;           /* 1 / 0; -1 no entry */
+} bshot_pre_cell;
+void bshot_pre_default_params(bshot_pre_params* p);
+/* vert_deg: setVerticalAngles (degrees, any order); sel: setSelectedPoints (any order, used when
+ * have_sel_list). xyz: caller's host buffer of cap points; *n_out = points written. */
+int bshot_preprocess(bshot_ctx* c, const bshot_laser* lasers, int n, const double* vert_deg, int nv,
+                     const bshot_pre_params* prm, const int32_t* sel, int nsel, float* xyz, int cap, int* n_out);
+/* device-resident lasers and output (d_xyz: cap points); the call syncs the context's stream for
+ * the count, so d_xyz can go straight to bshot_set_cloud_device / bshot_odom_process_device */
+int bshot_preprocess_device(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* vert_deg, int nv,
+                            const bshot_pre_params* prm, const int32_t* sel, int nsel, float* d_xyz, int cap,
+                            int* n_out);
+/* getRangeImage / getRemoveMap / getSelMap of the last run, merged over rimg's keys in map order
+ * (including the zero entries removeOccluded's operator[] reads insert) */
+int bshot_preprocess_cells(bshot_ctx* c, bshot_pre_cell* cells, int cap, int* n_out);
+
 /* ---- Headless odometry (test/odometry_test.cpp:159-194 frame loop over LidarOdometry) ----- */
 typedef struct bshot_odom bshot_odom;
 typedef struct {
@@ -192,7 +229,8 @@ enum {
     BSHOT_STAGE_MATCH = 8,
     BSHOT_STAGE_ICP = 9,
     BSHOT_STAGE_RANSAC = 10,
-    BSHOT_NSTAGES = 11
+    BSHOT_STAGE_PRE = 11,
+    BSHOT_NSTAGES = 12
 };
 int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n);
 void bshot_stage_reset(bshot_ctx* c);

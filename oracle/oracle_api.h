@@ -56,6 +56,29 @@ int oracle_ransac(const float* src_xyz, int ns, const float* tgt_xyz, int nt, co
 int oracle_icp(const float* src_xyz, int ns, const float* tgt_xyz, int nt, int max_iter, float* T_final,
                int* iters);
 
+/* point-cloud preprocessor (src/preprocess.cpp), oracle_pre.cpp */
+typedef struct {          /* velodyne::Laser, include/VelodyneCapture.h:43-50 (32 B) */
+    double azimuth;       /* degrees */
+    double vertical;      /* degrees */
+    uint16_t distance;    /* 2 mm units */
+    uint8_t intensity;
+    uint8_t id;
+    int64_t time;
+} oracle_laser;
+typedef struct {
+    double vert_init;     /* radians, setVerticalInitial (test/odometry_test.cpp:32: -0.6) */
+    double lowpt_th;      /* mm, setLowPtThreshold (test/odometry_test.cpp:33: -1950) */
+    int have_sel_list;    /* haveSelectList */
+    int save_sel;         /* saveSelectPoints */
+} oracle_pre_params;
+typedef struct {          /* one rimg entry after run(): rm / sel = -1 where rmmap / selmap lack the key */
+    double azimuth, vertical, distance;
+    int32_t rm, sel;
+} oracle_pre_cell;
+int oracle_preprocess(const oracle_laser* lasers, int n, const double* vert_deg, int nv, const oracle_pre_params* prm,
+                      const int32_t* sel, int nsel, float* xyz, int cap, int* n_out, oracle_pre_cell* cells,
+                      int cell_cap, int* n_cells);
+
 /* test hooks: exact radius search (FLANN semantics), Jacobi eigen, umeyama */
 int oracle_radius_search(const float* xyz, int n, const float* q, float radius, int max_nn, int32_t* idx,
                          float* d2, int cap);

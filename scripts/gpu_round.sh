@@ -9,7 +9,7 @@ O=$R/gpurun_out
 mkdir -p $O
 cd $R
 echo "[gpu_round] $(date +%T) pytest -m gpu" &&
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu_$TAG.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1 &&
 tail -3 $O/pytest_gpu_$TAG.log &&
 echo "[gpu_round] $(date +%T) smoke" &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 &&

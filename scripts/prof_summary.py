@@ -40,7 +40,19 @@ def main(tag):
             e = out["kernels"].setdefault(k, {"dispatches": len(v)})
             e["hbm_read_bytes" if sub == "fetch" else "hbm_write_bytes"] = sum(v) / len(v) * scale
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    for f in (f"bench_{tag}.json", f"bench_{tag}.err", f"pytest_gpu_{tag}.log", f"smoke_{tag}.log"):
+    # per-kernel median launch duration from the same kernel trace (the rocprofv3 mean is skewed by
+    # the cold first launches and by the launch that overlaps process teardown)
+    tr = os.path.join(src, f"prof_{tag}", "trace_kernel_trace.csv")
+    if os.path.exists(tr):
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            durs[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        with open(os.path.join(dst, f"{tag}_kernel_median.csv"), "w") as f:
+            f.write("kernel,launches,median_us,mean_us,min_us,max_us\n")
+            for k, v in sorted(durs.items(), key=lambda kv: -sum(kv[1])):
+                v.sort()
+                f.write(f"{k},{len(v)},{v[len(v) // 2]:.1f},{sum(v) / len(v):.1f},{v[0]:.1f},{v[-1]:.1f}\n")
+    for f in (f"prof_bench_{tag}.json", f"bench_{tag}.json", f"bench_{tag}.err", f"pytest_gpu_{tag}.log", f"smoke_{tag}.log"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f"{tag}_{f.replace('_' + tag, '')}"))
     print(json.dumps({k: v for k, v in out["kernels"].items() if "k_seg_ratio" in k or "k_shot_hist" in k}))

@@ -247,3 +247,30 @@ def set_threads(n):
     """OpenMP threads for the oracle's normals/SHOT stages (the reference's OpenMP stages)."""
     lib().oracle_set_threads(int(n))
     return lib().oracle_get_threads()
+
+
+# ---- preprocessor (oracle/oracle_pre.cpp; reference src/preprocess.cpp) ----------------------------
+class OPreParams(ctypes.Structure):
+    _fields_ = [("vert_init", ctypes.c_double), ("lowpt_th", ctypes.c_double), ("have_sel_list", ctypes.c_int),
+                ("save_sel", ctypes.c_int)]
+
+
+def preprocess(lasers, vert_deg, vert_init=-0.6, lowpt_th=-2000.0, sel=None, save_sel=True):
+    """Preprocessor::run restated with the reference's std::maps. Returns (xyz, cells): cells is the
+    rimg table after run() with rmmap / selmap values (-1 where those maps lack the key)."""
+    import bshot_py
+    lasers = np.ascontiguousarray(lasers, dtype=bshot_py.LASER_DTYPE)
+    vd = np.ascontiguousarray(vert_deg, dtype=np.float64)
+    pp = OPreParams(vert_init, lowpt_th, 1 if sel is not None else 0, 1 if save_sel else 0)
+    sa = np.ascontiguousarray(sel if sel is not None else np.zeros(0), dtype=np.int32)
+    n = len(lasers)
+    out = np.zeros((max(n, 1), 3), np.float32)
+    m = ctypes.c_int()
+    nc = ctypes.c_int()
+    ccap = 2 * n + 64 * (len(vd) + 1) * (n + 1) // 32 + 1024
+    cells = np.zeros(ccap, bshot_py.CELL_DTYPE)
+    rc = lib().oracle_preprocess(_p(lasers), n, _p(vd), len(vd), ctypes.byref(pp), _p(sa), len(sa), _p(out), n,
+                                 ctypes.byref(m), _p(cells), ccap, ctypes.byref(nc))
+    if rc < 0:
+        raise RuntimeError(f"oracle_preprocess capacity ({rc})")
+    return out[: m.value].copy(), cells[: nc.value].copy()

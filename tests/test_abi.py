@@ -39,3 +39,11 @@ def test_no_gpu_context_fails_loudly_or_works():
         bshot_py.lib().bshot_destroy(h)
     else:
         assert rc < 0
+
+
+def test_preprocessor_defaults_match_reference():
+    p = bshot_py.PreParams()
+    bshot_py.lib().bshot_pre_default_params(ctypes.byref(p))
+    # src/preprocess.cpp:5-7, include/preprocess.h:43
+    assert p.vert_init == -0.6 and p.lowpt_th == -2000.0 and p.have_sel_list == 0 and p.save_sel == 1
+    assert bshot_py.LASER_DTYPE.itemsize == 32 and bshot_py.CELL_DTYPE.itemsize == 32
