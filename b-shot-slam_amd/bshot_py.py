@@ -65,6 +65,7 @@ ABI_SYMBOLS = [
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
     "bshot_odom_set_option", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
     "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
+    "bshot_pcap_load", "bshot_velodyne_decode", "bshot_velodyne_decode_device",
 ]
 
 # velodyne::Laser (include/VelodyneCapture.h:43-50) == bshot_laser: 32 B, int64 time at offset 24
@@ -221,6 +222,30 @@ class Context:
         self._chk(self.L.bshot_preprocess_device(self.h, P(d_lasers), n, _ptr(vd), len(vd), ctypes.byref(pp), None,
                                                  0, P(d_xyz), cap, ctypes.byref(m)), "preprocess_device")
         return m.value
+
+    def velodyne_decode(self, payloads, unixtime, max_lasers=32, specified_frame=0):
+        """VelodyneCapture's packet loop on the GPU (bshot_velodyne_decode): 1206-B packets ->
+        (records of the pushed rotations back to back, rot_start, rot_count)."""
+        pk = np.ascontiguousarray(payloads, dtype=np.uint8).reshape(-1, 1206)
+        ut = np.ascontiguousarray(unixtime, dtype=np.int64)
+        npk = len(pk)
+        out = np.zeros(max(npk * 384, 1), LASER_DTYPE)
+        rs = np.zeros(npk * 384 + 2, np.int32)
+        rc = np.zeros(npk * 384 + 2, np.int32)
+        nr, no = ctypes.c_int(), ctypes.c_int()
+        self._chk(self.L.bshot_velodyne_decode(self.h, _ptr(pk), _ptr(ut), npk, max_lasers, specified_frame, _ptr(out),
+                                               len(out), _ptr(rs), _ptr(rc), len(rs), ctypes.byref(nr), ctypes.byref(no)),
+                  "velodyne_decode")
+        return out[: no.value].copy(), rs[: nr.value].copy(), rc[: nr.value].copy()
+
+    def velodyne_decode_device(self, d_payloads, d_unixtime, npk, d_out, max_lasers=32, specified_frame=0):
+        rs = np.zeros(npk * 384 + 2, np.int32)
+        rc = np.zeros(npk * 384 + 2, np.int32)
+        nr = ctypes.c_int()
+        self._chk(self.L.bshot_velodyne_decode_device(self.h, P(d_payloads), P(d_unixtime), npk, max_lasers,
+                                                      specified_frame, P(d_out), _ptr(rs), _ptr(rc), len(rs),
+                                                      ctypes.byref(nr)), "velodyne_decode_device")
+        return rs[: nr.value].copy(), rc[: nr.value].copy()
 
     def preprocess_cells(self):
         m = ctypes.c_int()
@@ -502,6 +527,21 @@ class KeypointMap:
 
 
 # ---------------------------------------------------------------- synthetic input (not the product)
+def pcap_load(path):
+    """bshot_pcap_load: the 1206-B data packets of a pcap file and their capture times (reference rule)."""
+    L = lib()
+    n = ctypes.c_int()
+    rc = L.bshot_pcap_load(str(path).encode(), None, None, 0, ctypes.byref(n))
+    if rc < 0:
+        raise BshotError(f"pcap_load {path} ({rc})")
+    pk = np.zeros((max(n.value, 1), 1206), np.uint8)
+    ut = np.zeros(max(n.value, 1), np.int64)
+    rc = L.bshot_pcap_load(str(path).encode(), _ptr(pk), _ptr(ut), n.value, ctypes.byref(n))
+    if rc < 0:
+        raise BshotError(f"pcap_load {path} ({rc})")
+    return pk[: n.value].copy(), ut[: n.value].copy()
+
+
 def _synth_lib():
     global _synth
     if _synth is None:

@@ -99,7 +99,8 @@ struct CloudState {
 };
 
 namespace bsh {
-struct PreState;  // csrc/preprocess.hip
+struct PreState;   // csrc/preprocess.hip
+struct VeloState;  // csrc/velodyne.hip
 }
 
 struct bshot_ctx {
@@ -148,6 +149,7 @@ struct bshot_ctx {
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
     bsh::PreState* prep = nullptr;  // GPU preprocessor state (csrc/preprocess.hip), created on first use
+    bsh::VeloState* velo = nullptr;  // GPU packet decode state (csrc/velodyne.hip), created on first use
     DBuf<unsigned int> sbh, sbst;  // bucketed gather: per-keypoint d2 histogram and bucket starts
     // lookahead keypoint gather (ctx_gather_kps_async): own index and staging buffers
     DBuf<int> kidx;

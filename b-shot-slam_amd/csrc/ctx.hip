@@ -18,6 +18,7 @@
 #include "ctx.h"
 #include "kernels.h"
 #include "preprocess.h"
+#include "velodyne.h"
 
 // BSHOT_TRACE=1: entry/exit trace of the C ABI calls on stderr (diagnostics only)
 static bool trace_on() {
@@ -787,6 +788,8 @@ void bshot_destroy(bshot_ctx* c) {
     c->sbh.release(); c->sbst.release(); c->kidx.release(); c->p_kidx.release(); c->p_kps3.release();
     bsh::pre_free(c->prep);
     c->prep = nullptr;
+    bsh::velo_free(c->velo);
+    c->velo = nullptr;
     c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);

@@ -4,7 +4,9 @@
 // through myslam::Preprocessor as odometry_test feeds them (:111-117, :143-163).
 // Output: one line per frame, "frame <id> <n_points> <n_inliers> <pose row-major, 16 x %a>".
 //
-//   bin/odometry_headless [frames=5] [keypoints=600] [sensor=0] [sr_type=CV] [pre=0]
+//   bin/odometry_headless [frames=5] [keypoints=600] [sensor=0] [sr_type=CV] [pre=0] [pcap=<file>]
+// With a pcap file (HDL-32E packets) the loop is odometry_test's whole chain: HDL32ECapture ->
+// Preprocessor -> LidarOdometry (:60-61, :111-194).
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -15,6 +17,7 @@
 
 #include "../../include/bshot/lidar_odometry.h"
 #include "../../include/bshot/preprocess.h"
+#include "../../include/bshot/velodyne.h"
 
 extern "C" int synth_sweep(int sensor, uint32_t scene_seed, int frame, int no_ground, float max_range, float* xyz,
                            int cap, float* pose_out);
@@ -26,7 +29,8 @@ int main(int argc, char** argv) {
     const int k = argc > 2 ? std::atoi(argv[2]) : 600;
     const int sensor = argc > 3 ? std::atoi(argv[3]) : 0;
     const std::string sr = argc > 4 ? argv[4] : "CV";
-    const bool pre = argc > 5 && std::atoi(argv[5]) != 0;
+    const std::string pcap = argc > 6 ? argv[6] : "";
+    const bool pre = (argc > 5 && std::atoi(argv[5]) != 0) || !pcap.empty();
     bshot_params p;
     bshot_default_params(&p);
     p.num_keypoints = k;
@@ -37,7 +41,12 @@ int main(int argc, char** argv) {
         // odometry_test.cpp:111-117: vertical table, vert_init -0.6, lowpt_th -1950
         std::unique_ptr<myslam::Preprocessor> prep;
         std::vector<double> vertAngle;
-        if (pre) {
+        std::unique_ptr<velodyne::HDL32ECapture> capture;
+        if (!pcap.empty()) {
+            capture.reset(new velodyne::HDL32ECapture(pcap, 0));
+            vertAngle = capture->getVerticalAngle();
+            std::sort(vertAngle.begin(), vertAngle.end());
+        } else if (pre) {
             std::vector<velodyne::Laser> probe(400000);
             const int nl = synth_lasers(sensor, 42, 0, 120000.f, 2450.f, probe.data(), (int)probe.size());
             if (nl < 0) return 2;
@@ -46,6 +55,8 @@ int main(int argc, char** argv) {
                 vertAngle.push_back(probe[i].vertical);
             }
             std::sort(vertAngle.begin(), vertAngle.end());
+        }
+        if (pre) {
             prep.reset(new myslam::Preprocessor());
             prep->setVerticalAngles(vertAngle);
             prep->setVerticalInitial(-0.6);
@@ -55,10 +66,17 @@ int main(int argc, char** argv) {
             auto pc = std::make_shared<std::vector<myslam::Vector3f>>();
             int n = 0;
             if (pre) {
-                std::vector<velodyne::Laser> lasers(400000);
-                const int nl = synth_lasers(sensor, 42, f, 120000.f, 2450.f, lasers.data(), (int)lasers.size());
-                if (nl < 0) return 2;
-                lasers.resize(nl);
+                std::vector<velodyne::Laser> lasers;
+                if (capture) {
+                    if (!capture->isRun()) break;
+                    *capture >> lasers;
+                    if (lasers.empty()) { --f; continue; }
+                } else {
+                    lasers.resize(400000);
+                    const int nl = synth_lasers(sensor, 42, f, 120000.f, 2450.f, lasers.data(), (int)lasers.size());
+                    if (nl < 0) return 2;
+                    lasers.resize(nl);
+                }
                 prep->setPointCloud(pc);
                 prep->setLasers(lasers);
                 prep->haveSelectList(false);

@@ -150,6 +150,27 @@ int bshot_preprocess_device(bshot_ctx* c, const bshot_laser* d_lasers, int n, co
  * (including the zero entries removeOccluded's operator[] reads insert) */
 int bshot_preprocess_cells(bshot_ctx* c, bshot_pre_cell* cells, int cap, int* n_out);
 
+/* ---- Velodyne capture (include/VelodyneCapture.h:413-525): PCAP file ->
+ *      1206-B data packets (host) -> laser records grouped into rotations (GPU). -------------- */
+/* Reads a classic pcap file (usec or nsec timestamps, either byte order) the way capturePCAP
+ * consumes it: keeps the records whose wire length - 42 == 1206 (:432-434), copies their UDP
+ * payloads (bytes 42..1247) into payloads (cap packets x 1206 B; NULL: count only) and each
+ * packet's time as the reference builds it, tv_sec followed by tv_usec left-aligned zero-filled to
+ * 6 digits (:437-439). Host only, no GPU. Returns 0, *n_packets = packets found. */
+int bshot_pcap_load(const char* path, uint8_t* payloads, int64_t* unixtime, int cap, int* n_packets);
+/* Decodes npk packets (max_lasers 32: HDL-32E, 16: VLP-16 with the interpolated second half of each
+ * firing) with the reference's rotation split and specifiedframe skip. out: the pushed rotations'
+ * records back to back (cap records); rotation i = out[rot_start[i] .. + rot_count[i]). A packet
+ * whose sensor type is not 0x21/0x22 is an error (the reference asserts, :453). */
+int bshot_velodyne_decode(bshot_ctx* c, const uint8_t* payloads, const int64_t* unixtime, int npk, int max_lasers,
+                          int specified_frame, bshot_laser* out, int cap, int32_t* rot_start, int32_t* rot_count,
+                          int rot_cap, int* n_rot, int* n_out);
+/* device-resident packets / times; d_out holds npk x 384 records in the reference's loop order and
+ * rot_start / rot_count (host) index it */
+int bshot_velodyne_decode_device(bshot_ctx* c, const uint8_t* d_payloads, const int64_t* d_unixtime, int npk,
+                                 int max_lasers, int specified_frame, bshot_laser* d_out, int32_t* rot_start,
+                                 int32_t* rot_count, int rot_cap, int* n_rot);
+
 /* ---- Headless odometry (test/odometry_test.cpp:159-194 frame loop over LidarOdometry) ----- */
 typedef struct bshot_odom bshot_odom;
 typedef struct {

@@ -79,6 +79,13 @@ int oracle_preprocess(const oracle_laser* lasers, int n, const double* vert_deg,
                       const int32_t* sel, int nsel, float* xyz, int cap, int* n_out, oracle_pre_cell* cells,
                       int cell_cap, int* n_cells);
 
+/* Velodyne data-packet decode (include/VelodyneCapture.h:413-525), oracle_velo.cpp: packets of
+ * 1206 B, max_lasers 32 (HDL-32E) or 16 (VLP-16); out = the pushed rotations' records in order,
+ * rot_count = records per pushed rotation. */
+int oracle_velodyne_decode(const uint8_t* payloads, const int64_t* unixtime, int npk, int max_lasers,
+                           int specified_frame, oracle_laser* out, int cap, int32_t* rot_count, int rot_cap,
+                           int* n_out, int* n_rot);
+
 /* test hooks: exact radius search (FLANN semantics), Jacobi eigen, umeyama */
 int oracle_radius_search(const float* xyz, int n, const float* q, float radius, int max_nn, int32_t* idx,
                          float* d2, int cap);

@@ -274,3 +274,24 @@ def preprocess(lasers, vert_deg, vert_init=-0.6, lowpt_th=-2000.0, sel=None, sav
     if rc < 0:
         raise RuntimeError(f"oracle_preprocess capacity ({rc})")
     return out[: m.value].copy(), cells[: nc.value].copy()
+
+
+# ---- Velodyne packet decode (oracle/oracle_velo.cpp; reference include/VelodyneCapture.h:413-525) ----
+def velodyne_decode(payloads, unixtime, max_lasers=32, specified_frame=0):
+    """capturePCAP's loop: returns (records of the pushed rotations back to back, rot_count)."""
+    import bshot_py
+    pk = np.ascontiguousarray(payloads, dtype=np.uint8).reshape(-1, 1206)
+    ut = np.ascontiguousarray(unixtime, dtype=np.int64)
+    npk = len(pk)
+    out = np.zeros(max(npk * 384, 1), bshot_py.LASER_DTYPE)
+    rc = np.zeros(npk * 384 + 2, np.int32)
+    no, nr = ctypes.c_int(), ctypes.c_int()
+    r = lib().oracle_velodyne_decode(_p(pk), _p(ut), npk, max_lasers, specified_frame, _p(out), len(out), _p(rc),
+                                     len(rc), ctypes.byref(no), ctypes.byref(nr))
+    if r == -1:
+        raise ValueError("sensor type")
+    if r < 0:
+        raise RuntimeError("oracle_velodyne_decode capacity")
+    out = out[: no.value].copy()
+    out.view(np.uint8).reshape(-1, 32)[:, 20:24] = 0  # struct padding (indeterminate in the reference too)
+    return out, rc[: nr.value].copy()
