@@ -677,6 +677,12 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         }
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
         const unsigned long long* best = c->p_best.p;
+        const int splits = icp_tile_splits(ns, nt);
+        if (c->opt_icp_tile) {
+            HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
+            HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
+            HIPCHK(hipMemsetAsync(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
+        }
         double prev_mse = 1.7976931348623157e308;
         bg::Mat4f Ts = bg::Mat4f::identity();
         while (true) {
@@ -684,9 +690,15 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
             // one launch per iteration; the NN keys land in pinned host memory (no copy)
             const float* s_in = it == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
-            HIPCHK(launch_icp_wave(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt, c->p_best.p,
-                                   c->stream),
-                   "icp iteration");
+            if (c->opt_icp_tile)
+                HIPCHK(launch_icp_tile(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt,
+                                       c->ipart.p, (int)std::min<size_t>(c->ipart.cap, 0x7FFFFFFF), c->icnt.p,
+                                       c->p_best.p, c->stream),
+                       "icp iteration");
+            else
+                HIPCHK(launch_icp_wave(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt,
+                                       c->p_best.p, c->stream),
+                       "icp iteration");
             c->stage_end(sg14);
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
             for (int i = 0; i < ns; ++i) {
@@ -790,7 +802,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->prep = nullptr;
     bsh::velo_free(c->velo);
     c->velo = nullptr;
-    c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->ipart.release(); c->icnt.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
@@ -1042,6 +1054,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
+    else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
     else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;

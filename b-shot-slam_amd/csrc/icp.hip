@@ -138,6 +138,87 @@ __global__ void __launch_bounds__(256) k_icp_wave(const float* __restrict__ src_
     if (lane == 0) best_out[i] = m;
 }
 
+// One ICP iteration, LDS-tiled: a workgroup holds 256 source points (a thread each) and one
+// contiguous span of the targets (blockIdx.y), streamed through LDS in tiles of 512 float4 that
+// every lane reads by broadcast, so each target is fetched once per workgroup instead of once per
+// source point. The span minima meet in `part`; the last workgroup of a source block (agent-scope
+// counter, reset by that workgroup) reduces them and stores the packed (d2 bits << 32 | index)
+// minimum straight into best_out (pinned host memory), as k_icp_wave does.
+#define ICPT_TILE 512
+__global__ void __launch_bounds__(256) k_icp_tile(const float* __restrict__ src_in, float* __restrict__ src_out,
+                                                  Xf16 T, int apply, int ns, const float* __restrict__ tgt, int nt,
+                                                  int span, unsigned long long* __restrict__ part,
+                                                  unsigned int* __restrict__ cnt,
+                                                  unsigned long long* __restrict__ best_out) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
+    __shared__ float4 tt[ICPT_TILE];
+    __shared__ int last;
+    const int t = threadIdx.x, i = blockIdx.x * 256 + t;
+    const int S = gridDim.y, sp = blockIdx.y;
+    float qx = 0.f, qy = 0.f, qz = 0.f;
+    if (i < ns) {
+        const float x = src_in[3 * i], y = src_in[3 * i + 1], z = src_in[3 * i + 2];
+        qx = x; qy = y; qz = z;
+        if (apply) {
+            qx = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
+            qy = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
+            qz = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
+        }
+        if (sp == 0) {
+            src_out[3 * i] = qx; src_out[3 * i + 1] = qy; src_out[3 * i + 2] = qz;
+        }
+    }
+    unsigned long long m = ~0ull;
+    const int r0 = sp * span, r1 = min(nt, r0 + span);
+    for (int b = r0; b < r1; b += ICPT_TILE) {
+        const int nb = min(ICPT_TILE, r1 - b);
+        __syncthreads();
+        for (int u = t; u < nb; u += 256) {
+            const float* p3 = tgt + 3 * (size_t)(b + u);
+            tt[u] = make_float4(p3[0], p3[1], p3[2], 0.f);
+        }
+        __syncthreads();
+        if (i < ns) {
+            int u = 0;
+            for (; u + 4 <= nb; u += 4) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float4 p = tt[u + v];
+                    const float d2 = d2_flann(qx, qy, qz, p.x, p.y, p.z);
+                    const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)(b + u + v);
+                    m = key < m ? key : m;
+                }
+            }
+            for (; u < nb; ++u) {
+                const float4 p = tt[u];
+                const float d2 = d2_flann(qx, qy, qz, p.x, p.y, p.z);
+                const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)(b + u);
+                m = key < m ? key : m;
+            }
+        }
+    }
+    if (S == 1) {
+        if (i < ns) best_out[i] = m;
+        return;
+    }
+    if (i < ns) __hip_atomic_store(&part[(size_t)sp * ns + i], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (t == 0)
+        last = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
+    __syncthreads();
+    if (!last) return;
+    if (i < ns) {
+        unsigned long long r = ~0ull;
+        for (int s2 = 0; s2 < S; ++s2) {
+            const unsigned long long v =
+                __hip_atomic_load(&part[(size_t)s2 * ns + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r = v < r ? v : r;
+        }
+        best_out[i] = r;
+    }
+    if (t == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- device-resident ICP loop: the host enqueues max_iter (NN, update) pairs and syncs once.
 // The update kernel restates ctx_icp's host step exactly (bg::umeyama<float> sequential sums,
 // bm::umeyama_finish, bg::mul, PCL's convergence tests); once converged, later launches return.
@@ -380,6 +461,31 @@ hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16
     for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
     bsk::k_icp_wave<<<(ns + 3) / 4, 256, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, best_out);
     return hipGetLastError();
+}
+
+// spans: about 1024 workgroups in all, each span >= 256 targets; part holds S x ns keys, cnt one
+// counter per 256-source block (zero on entry, left zero)
+hipError_t launch_icp_tile(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
+                           int nt, unsigned long long* part, int part_cap, unsigned int* cnt,
+                           unsigned long long* best_out, hipStream_t s) {
+    if (ns <= 0 || nt <= 0) return hipSuccess;
+    bsk::Xf16 T;
+    for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
+    const int qb = (ns + 255) / 256;
+    int S = icp_tile_splits(ns, nt);
+    if ((long long)S * ns > part_cap) return hipErrorInvalidValue;
+    const int span = (nt + S - 1) / S;
+    S = (nt + span - 1) / span;
+    bsk::k_icp_tile<<<dim3(qb, S), 256, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, span, part, cnt, best_out);
+    return hipGetLastError();
+}
+
+int icp_tile_splits(int ns, int nt) {
+    const int qb = (ns + 255) / 256;
+    int S = (1024 + qb - 1) / qb;
+    const int smax = (nt + 255) / 256;
+    if (S > smax) S = smax;
+    return S < 1 ? 1 : S;
 }
 
 hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int ns, const float4* tgt, int nt,

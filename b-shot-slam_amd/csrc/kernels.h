@@ -45,6 +45,12 @@ hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, in
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
 // wave per source point, results stored straight to best_out (may be pinned host memory)
+// LDS-tiled NN pass over target spans (k_icp_tile); part: icp_tile_splits(ns, nt) x ns keys, cnt:
+// ceil(ns / 256) zeroed counters
+int icp_tile_splits(int ns, int nt);
+hipError_t launch_icp_tile(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
+                           int nt, unsigned long long* part, int part_cap, unsigned int* cnt,
+                           unsigned long long* best_out, hipStream_t s);
 hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
                            int nt, unsigned long long* best_out, hipStream_t s);
 hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,

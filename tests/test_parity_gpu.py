@@ -148,3 +148,27 @@ def test_ransac_dev_matches_host(ctx, seed, frac):
         r2 = ctx.ransac(src, tgt, cq[:ncorr], cm[:ncorr])
         o2 = orc.ransac(src, tgt, cq[:ncorr], cm[:ncorr])
         assert r2[0] == o2[0] and np.array_equal(r2[1], o2[1]) and np.array_equal(r2[2], o2[2])
+
+
+def test_config5_dense_large_radius_describe():
+    """BASELINE config 5: VLP-128-style 256k-point sweep, K=4096 keypoints, SHOT radius 5000 mm
+    (the large-neighbourhood stress case). The GPU describes all 4096 keypoints; the oracle checks
+    a fixed subset of 192 against the same persistent normals array, bit for bit."""
+    pc, _ = bshot_py.synth_sweep(2, sensor=1)
+    prm = bshot_py.default_params(num_keypoints=4096, shot_radius=5000.0)
+    c = bshot_py.Context(0, prm)
+    try:
+        c.set_cloud(pc)
+        idx, rat = c.seg_ratio()
+        kidx, _ = bshot_py.select_topk(idx, rat, 4096)
+        kps = pc[kidx]
+        bits, shot, rf = c.describe(kps)
+    finally:
+        c.close()
+    assert len(pc) > 200000 and len(kps) == 4096
+    rn = orc.normals(pc, kps)
+    sub = np.linspace(0, 4095, 192).astype(np.int64)
+    rs, rrf = orc.shot(pc, rn, kps[sub], radius=5000.0)
+    np.testing.assert_array_equal(shot[sub].view(np.uint32), rs.view(np.uint32))
+    np.testing.assert_array_equal(rf[sub].view(np.uint32), rrf.view(np.uint32))
+    np.testing.assert_array_equal(bits[sub], orc.binarize(rs))
