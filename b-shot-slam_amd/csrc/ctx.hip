@@ -1055,6 +1055,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
+    else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
     else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;

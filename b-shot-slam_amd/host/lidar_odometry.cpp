@@ -19,9 +19,48 @@ namespace myslam {
 static void zero_stats(bshot_frame_stats& s) { std::memset(&s, 0, sizeof(s)); }
 
 // features of one sweep computed ahead of time on a worker thread (prefetchFrameDevice)
+// A2 top-K of a queued sweep (two ahead), computed on its own host thread as soon as the sweep's
+// SR ratios land in pinned memory, so the lookahead worker starts its describe right away. The
+// pinned ratio buffer and SR event it reads belong to the queued cloud state and are not reused
+// before the sweep is described (ctx_queue_dev reuses the other slot).
+struct LidarOdometry::TopkAhead {
+    const float* d_xyz = nullptr;
+    int n = 0;
+    std::thread th;
+    std::string err;
+    int nv = 0;
+    std::vector<int32_t> kidx;
+    std::vector<float> kr;
+};
+
+// SR ratios of a cloud (pinned host copy) -> valid (index, ratio) pairs -> top-K (libstdc++ order)
+static int select_from_ratios(const float* h_ratio, int n, int k_want, std::vector<int32_t>& kidx,
+                              std::vector<float>& kr, int* nv_out) {
+    std::vector<int32_t> idx(n > 0 ? n : 1);
+    std::vector<float> ratio(n > 0 ? n : 1);
+    int nv = 0;
+    for (int i = 0; i < n; ++i) {
+        const float r = h_ratio[i];
+        if (r != r) continue;
+        idx[nv] = i;
+        ratio[nv] = r;
+        ++nv;
+    }
+    *nv_out = nv;
+    kidx.resize(k_want > 0 ? k_want : 1);
+    kr.resize(kidx.size());
+    int k = 0;
+    const int rc = bshot_select_topk(idx.data(), ratio.data(), nv, k_want, kidx.data(), kr.data(), &k);
+    if (rc < 0) return rc;
+    kidx.resize(k);
+    kr.resize(k);
+    return BSHOT_OK;
+}
+
 struct LidarOdometry::Lookahead {
     const float* d_xyz = nullptr;
     int n = 0;
+    std::shared_ptr<TopkAhead> topk;  // precomputed top-K (joined by the worker), or null
     std::thread th;
     std::string err;
     int nv = 0;
@@ -51,7 +90,13 @@ LidarOdometry::LidarOdometry(const bshot_params& p, int device)
 
 LidarOdometry::~LidarOdometry() {
     if (ahead_ && ahead_->th.joinable()) ahead_->th.join();
+    dropTopkAhead();
     bshot_destroy(ctx_);
+}
+
+void LidarOdometry::dropTopkAhead() {
+    if (topk_ahead_ && topk_ahead_->th.joinable()) topk_ahead_->th.join();
+    topk_ahead_.reset();
 }
 
 void LidarOdometry::joinAhead() {
@@ -115,6 +160,10 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
     auto la = std::make_shared<Lookahead>();
     la->d_xyz = d_xyz;
     la->n = n;
+    // the top-K started when this sweep was queued travels with it to the worker
+    if (topk_ahead_ && topk_ahead_->d_xyz == d_xyz && topk_ahead_->n == n) la->topk = std::move(topk_ahead_);
+    else dropTopkAhead();
+    topk_ahead_.reset();
     Lookahead* p = la.get();
     la->th = std::thread([this, p]() {
         try {
@@ -130,8 +179,32 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
 void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
     // on the main thread: issued from the worker (after its describe) it started the sweep after
     // next's SR too late and slowed the describe it then overlapped (measured 260 -> 237 sweeps/s)
+    dropTopkAhead();
     check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
     ctx_->hmark("M_queued");
+    bshot_ctx* c = ctx_;
+    if (!(c->pf2.d_xyz == d_xyz && c->pf2.n == n && c->pf2.sr_state == 1) || c->opt_topk_thread == 0) return;
+    auto tk = std::make_shared<TopkAhead>();
+    tk->d_xyz = d_xyz;
+    tk->n = n;
+    TopkAhead* p = tk.get();
+    const hipEvent_t ev = c->pf2.ev_sr;
+    const float* h_ratio = c->pf2.h_ratio.p;
+    const int* h_err = c->pf2.h_err.p;
+    const int dev = c->device, kwant = prm_.num_keypoints;
+    p->th = std::thread([p, ev, h_ratio, h_err, dev, kwant, n]() {
+        (void)hipSetDevice(dev);
+        if (hipEventSynchronize(ev) != hipSuccess) {
+            p->err = "lookahead sr";
+            return;
+        }
+        if (h_err[0]) {
+            p->err = "seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)";
+            return;
+        }
+        if (select_from_ratios(h_ratio, n, kwant, p->kidx, p->kr, &p->nv) < 0) p->err = "topk";
+    });
+    topk_ahead_ = tk;
 }
 
 // worker thread: the extract + describe half of the frame for the prefetched cloud (ctx->pf) on
@@ -145,26 +218,20 @@ void LidarOdometry::runAhead(Lookahead& la) {
     c->hmark("W_start");
     if (hipEventSynchronize(S.ev_sr) != hipSuccess) fail("lookahead sr");
     c->hmark("W_sr_ready");
-    if (S.h_err.p[0]) throw std::runtime_error("seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)");
-    const int n = S.n;
-    std::vector<int32_t> idx(n > 0 ? n : 1);
-    std::vector<float> ratio(n > 0 ? n : 1);
-    int nv = 0;
-    for (int i = 0; i < n; ++i) {
-        const float r = S.h_ratio.p[i];
-        if (r != r) continue;
-        idx[nv] = i;
-        ratio[nv] = r;
-        ++nv;
+    if (la.topk) {
+        // computed on the top-K thread when this sweep was queued
+        if (la.topk->th.joinable()) la.topk->th.join();
+        if (!la.topk->err.empty()) throw std::runtime_error(la.topk->err);
+        la.nv = la.topk->nv;
+        la.kidx = std::move(la.topk->kidx);
+        la.kr = std::move(la.topk->kr);
+        la.topk.reset();
+    } else {
+        if (S.h_err.p[0])
+            throw std::runtime_error("seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)");
+        if (select_from_ratios(S.h_ratio.p, S.n, prm_.num_keypoints, la.kidx, la.kr, &la.nv) < 0) fail("topk");
     }
-    la.nv = nv;
-    la.kidx.resize(prm_.num_keypoints > 0 ? prm_.num_keypoints : 1);
-    la.kr.resize(la.kidx.size());
-    int k = 0;
-    if (bshot_select_topk(idx.data(), ratio.data(), nv, prm_.num_keypoints, la.kidx.data(), la.kr.data(), &k) < 0)
-        fail("topk");
-    la.kidx.resize(k);
-    la.kr.resize(k);
+    const int k = (int)la.kidx.size();
     la.kps.resize(k);
     // queued without a sync: the describe below follows it on the side stream, and the coordinates
     // are copied out after the side stream's final sync
@@ -182,7 +249,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
         std::vector<int32_t> ii;
         ii.reserve(1024);
         const unsigned char* fl = S.h_flag.p;
-        for (int i = 0; i < n; ++i)
+        for (int i = 0; i < S.n; ++i)
             if (fl[i]) ii.push_back(i);
         la.iss.resize(ii.size());
         if (!ii.empty() &&

@@ -83,8 +83,11 @@ class LidarOdometry {
   private:
     void check(int rc, const char* where);
     struct Lookahead;
+    struct TopkAhead;
     void runAhead(Lookahead& la);
     void joinAhead();
+    void dropTopkAhead();
+    std::shared_ptr<TopkAhead> topk_ahead_;  // sweep after next: top-K on its own thread once its SR lands
     std::shared_ptr<Lookahead> ahead_;  // next sweep, in flight on the worker thread
     std::shared_ptr<Lookahead> ready_;  // adopted for the current sweep
 
