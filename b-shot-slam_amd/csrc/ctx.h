@@ -180,7 +180,8 @@ struct bshot_ctx {
     DBuf<bsh::IcpState> istate;
     PinBuf<bsh::IcpState> p_istate;
     int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
-    int opt_topk_thread = 1;  // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
+    int opt_topk_thread = 1;
+    int opt_queue_thread = 0;  // LidarOdometry: the queued sweep's grids/SR/ISS launches issued from their own host thread  // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
     int opt_icp_tile = 1;  // 1: LDS-tiled NN over target spans (k_icp_tile); 0: wave per source point (k_icp_wave)
     DBuf<unsigned long long> ipart;  // k_icp_tile span minima
     DBuf<unsigned int> icnt;         // k_icp_tile per-block arrival counters
@@ -241,6 +242,8 @@ int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst);
 int ctx_sync_main(bshot_ctx* c);
 // explicit-cloud / explicit-stream variants (the lookahead task runs them on the side stream)
 int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n);
+int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n);
+int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1 = false);
 // after a describe's error word reached the host (err[0..3] as copied from c->errw): true when the
 // describe must be run again -- errw bit 16, a device plan over capacity (the re-run plans on the

@@ -332,7 +332,15 @@ int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
 // the sweep after next: grids + SR on the pre stream, ISS on the iss stream, into the queue slot,
 // running beside the side stream's describe of the next sweep
 int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n) {
-    if (n <= 0 || holds(c->pf, d_xyz, n) || holds(c->pf2, d_xyz, n)) return BSHOT_OK;
+    const int go = ctx_queue_begin(c, d_xyz, n);
+    if (go <= 0) return go;
+    return ctx_queue_rest(c, d_xyz, n);
+}
+
+// main-thread half of ctx_queue_dev: 1 when the cloud must be queued (the pre stream then waits
+// for the work already on the main stream), 0 when it is already held, < 0 on error
+int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n) {
+    if (n <= 0 || holds(c->pf, d_xyz, n) || holds(c->pf2, d_xyz, n)) return 0;
     // the queue slot's buffers may still be read by work queued on the main stream or by ISS
     hipEvent_t e;
     {
@@ -345,6 +353,13 @@ int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n) {
         std::lock_guard<std::mutex> lk(c->evmu);
         c->evpool.push_back(e);
     }
+    return 1;
+}
+
+// the rest of ctx_queue_dev (grids, SR, ISS of the queue slot on the pre / iss streams): touches
+// only c->pf2 and those streams, so it may run on another host thread while the main thread works
+int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n) {
+    (void)hipSetDevice(c->device);
     if (c->pf2.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->pre, c->pf2.ev_iss, 0), "wait old iss");
     int rc = cloud_load(c, c->pf2, d_xyz, n, c->pre);
     if (rc) return rc;
@@ -1056,6 +1071,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
+    else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
     else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;

@@ -57,6 +57,12 @@ static int select_from_ratios(const float* h_ratio, int n, int k_want, std::vect
     return BSHOT_OK;
 }
 
+struct LidarOdometry::QueueAhead {
+    std::thread th;
+    std::string err;
+    std::shared_ptr<TopkAhead> topk;
+};
+
 struct LidarOdometry::Lookahead {
     const float* d_xyz = nullptr;
     int n = 0;
@@ -90,8 +96,24 @@ LidarOdometry::LidarOdometry(const bshot_params& p, int device)
 
 LidarOdometry::~LidarOdometry() {
     if (ahead_ && ahead_->th.joinable()) ahead_->th.join();
+    if (queue_ahead_ && queue_ahead_->th.joinable()) queue_ahead_->th.join();
+    if (queue_ahead_ && queue_ahead_->topk && queue_ahead_->topk->th.joinable()) queue_ahead_->topk->th.join();
     dropTopkAhead();
     bshot_destroy(ctx_);
+}
+
+// the queue thread (launches of the sweep after next) has to be done before the main thread looks
+// at the queue slot again; its top-K thread, if any, becomes topk_ahead_
+void LidarOdometry::joinQueue() {
+    if (!queue_ahead_) return;
+    if (queue_ahead_->th.joinable()) queue_ahead_->th.join();
+    auto q = queue_ahead_;
+    queue_ahead_.reset();
+    if (q->topk) topk_ahead_ = q->topk;
+    if (!q->err.empty()) {
+        err_ = q->err;
+        throw std::runtime_error(err_);
+    }
 }
 
 void LidarOdometry::dropTopkAhead() {
@@ -129,6 +151,7 @@ void LidarOdometry::setRefFrame(Frame::Ptr ref) {
 }
 
 void LidarOdometry::setSrcFrame(Frame::Ptr src) {
+    joinQueue();
     joinAhead();
     ready_.reset();
     src_ = src;
@@ -140,6 +163,7 @@ void LidarOdometry::setSrcFrame(Frame::Ptr src) {
 
 void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n) {
     ctx_->hmark("M_frame");
+    joinQueue();
     joinAhead();
     ctx_->hmark("M_joined");
     if (ready_ && !(ready_->d_xyz == d_xyz && ready_->n == n)) ready_.reset();
@@ -151,6 +175,7 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
 }
 
 void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
+    joinQueue();
     joinAhead();
     ready_.reset();
     // grids + SR + ISS on the side stream (after everything already queued on the main stream,
@@ -177,34 +202,60 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
 }
 
 void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
-    // on the main thread: issued from the worker (after its describe) it started the sweep after
-    // next's SR too late and slowed the describe it then overlapped (measured 260 -> 237 sweeps/s)
+    // issued from the worker (after its describe) it started the sweep after next's SR too late and
+    // slowed the describe it then overlapped (measured 260 -> 237 sweeps/s); the main thread records
+    // the ordering event and a thread of its own issues the launches
+    joinQueue();
     dropTopkAhead();
-    check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
-    ctx_->hmark("M_queued");
     bshot_ctx* c = ctx_;
-    if (!(c->pf2.d_xyz == d_xyz && c->pf2.n == n && c->pf2.sr_state == 1) || c->opt_topk_thread == 0) return;
-    auto tk = std::make_shared<TopkAhead>();
-    tk->d_xyz = d_xyz;
-    tk->n = n;
-    TopkAhead* p = tk.get();
-    const hipEvent_t ev = c->pf2.ev_sr;
-    const float* h_ratio = c->pf2.h_ratio.p;
-    const int* h_err = c->pf2.h_err.p;
-    const int dev = c->device, kwant = prm_.num_keypoints;
-    p->th = std::thread([p, ev, h_ratio, h_err, dev, kwant, n]() {
-        (void)hipSetDevice(dev);
-        if (hipEventSynchronize(ev) != hipSuccess) {
-            p->err = "lookahead sr";
+    const int kwant = prm_.num_keypoints;
+    // top-K of the queued sweep on its own thread once its SR lands (reads only the queue slot's
+    // pinned ratios and SR event, which stay with the sweep until it is described)
+    auto start_topk = [c, d_xyz, n, kwant]() -> std::shared_ptr<TopkAhead> {
+        if (!(c->pf2.d_xyz == d_xyz && c->pf2.n == n && c->pf2.sr_state == 1) || c->opt_topk_thread == 0) return nullptr;
+        auto tk = std::make_shared<TopkAhead>();
+        tk->d_xyz = d_xyz;
+        tk->n = n;
+        TopkAhead* p = tk.get();
+        const hipEvent_t ev = c->pf2.ev_sr;
+        const float* h_ratio = c->pf2.h_ratio.p;
+        const int* h_err = c->pf2.h_err.p;
+        const int dev = c->device;
+        p->th = std::thread([p, ev, h_ratio, h_err, dev, kwant, n]() {
+            (void)hipSetDevice(dev);
+            if (hipEventSynchronize(ev) != hipSuccess) {
+                p->err = "lookahead sr";
+                return;
+            }
+            if (h_err[0]) {
+                p->err = "seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)";
+                return;
+            }
+            if (select_from_ratios(h_ratio, n, kwant, p->kidx, p->kr, &p->nv) < 0) p->err = "topk";
+        });
+        return tk;
+    };
+    if (!c->opt_queue_thread) {
+        check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
+        ctx_->hmark("M_queued");
+        topk_ahead_ = start_topk();
+        return;
+    }
+    const int go = bsh::ctx_queue_begin(c, d_xyz, n);
+    check(go, "queueFrameDevice");
+    if (go == 0) return;
+    auto q = std::make_shared<QueueAhead>();
+    QueueAhead* p = q.get();
+    p->th = std::thread([p, c, d_xyz, n, start_topk]() {
+        if (bsh::ctx_queue_rest(c, d_xyz, n) != BSHOT_OK) {
+            p->err = std::string("queueFrameDevice: ") + c->err;
             return;
         }
-        if (h_err[0]) {
-            p->err = "seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)";
-            return;
-        }
-        if (select_from_ratios(h_ratio, n, kwant, p->kidx, p->kr, &p->nv) < 0) p->err = "topk";
+        c->hmark("Q_queued");
+        p->topk = start_topk();
     });
-    topk_ahead_ = tk;
+    queue_ahead_ = q;
+    ctx_->hmark("M_queued");
 }
 
 // worker thread: the extract + describe half of the frame for the prefetched cloud (ctx->pf) on
