@@ -332,15 +332,15 @@ namespace bsh {
 
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc, int* err,
-                      hipStream_t s) {
+                      hipStream_t s, int ovf_blocks) {
     if (n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn,
                                                                              g21, g32, third, ovf, nml, nmc);
     const size_t lds = sizeof(bsk::IssLds) * ISS_WAVES;
-    // the overflow count is device-side: launch a full grid, idle waves exit at once
-    bsk::k_iss_scatter<<<4096, 64 * ISS_WAVES, lds, s>>>(g.view(), pts4, ovf, salient, min_nn, g21, g32, third, err);
+    // the overflow count is device-side: a fixed grid strides over it, idle waves exit at once
+    bsk::k_iss_scatter<<<ovf_blocks > 0 ? ovf_blocks : 4096, 64 * ISS_WAVES, lds, s>>>(g.view(), pts4, ovf, salient, min_nn, g21, g32, third, err);
     if (nonmax <= salient) {
         // the non-max neighbours are a prefix of the lane kernel's sorted salient neighbours
         bsk::k_iss_nms_list<<<(n + 255) / 256, 256, 0, s>>>(n, min_nn, third, nml, nmc, flag);
