@@ -183,6 +183,7 @@ struct bshot_ctx {
     int opt_topk_thread = 1;   // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
     int opt_queue_thread = 0;  // LidarOdometry: the queued sweep's grids/SR/ISS launches issued from their own host thread
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
+    int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
     int opt_icp_tile = 1;  // 1: LDS-tiled NN over target spans (k_icp_tile); 0: wave per source point (k_icp_wave)
     DBuf<unsigned long long> ipart;  // k_icp_tile span minima
     DBuf<unsigned int> icnt;         // k_icp_tile per-block arrival counters

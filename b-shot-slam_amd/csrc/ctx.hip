@@ -252,7 +252,7 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
                "grid build (ISS)");
         HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
-                          s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks),
+                          s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks),
                "iss launch");
         c->stage_end(sg3, st);
         HIPCHK(hipMemcpyAsync(s.h_flag.p, s.issflag.p, n, hipMemcpyDeviceToHost, st), "D2H iss");
@@ -1073,6 +1073,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
+    else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
     else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;

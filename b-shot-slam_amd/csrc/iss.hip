@@ -332,7 +332,7 @@ namespace bsh {
 
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc, int* err,
-                      hipStream_t s, int ovf_blocks) {
+                      hipStream_t s, int ovf_blocks, int nms_blocks) {
     if (n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
@@ -344,7 +344,8 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
     if (nonmax <= salient) {
         // the non-max neighbours are a prefix of the lane kernel's sorted salient neighbours
         bsk::k_iss_nms_list<<<(n + 255) / 256, 256, 0, s>>>(n, min_nn, third, nml, nmc, flag);
-        bsk::k_iss_nms_wave<<<1024, 256, 0, s>>>(g.view(), pts4, n, ovf, 0, nonmax, min_nn, third, flag);
+        bsk::k_iss_nms_wave<<<nms_blocks > 0 ? nms_blocks : 1024, 256, 0, s>>>(g.view(), pts4, n, ovf, 0, nonmax, min_nn,
+                                                                               third, flag);
     } else {
         bsk::k_iss_nms_wave<<<4096, 256, 0, s>>>(g.view(), pts4, n, ovf, 1, nonmax, min_nn, third, flag);
     }
