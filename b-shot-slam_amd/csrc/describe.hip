@@ -65,8 +65,7 @@ __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __r
 
 // Device-side describe plan (no host round trip): offs = exclusive scan of counts (segment
 // starts, offs[k] = total), cb = exclusive scan of ceil(counts / 64) (chunk bases), perm = keypoints
-// by descending neighbourhood size, ties by index (the apply's LPT launch order; results do not
-// depend on it). When the total or the chunk count exceed the preallocated capacities, err |= 16
+// by descending neighbourhood size (the apply's LPT launch order; results do not depend on it). When the total or the chunk count exceed the preallocated capacities, err |= 16
 // and every segment / chunk range is emptied so no later kernel writes out of bounds; the host
 // then re-plans on its side. One workgroup, k <= DP_MAXK.
 #define DP_MAXK 8192
@@ -75,7 +74,6 @@ __global__ void __launch_bounds__(1024) k_desc_plan(const int* __restrict__ coun
                                                     int* __restrict__ perm, int* __restrict__ err) {
     __shared__ long long ps[1024];
     __shared__ int pc[1024];
-    __shared__ unsigned long long keys[DP_MAXK];
     __shared__ int bad;
     const int t = threadIdx.x;
     const int per = (k + 1023) / 1024;
@@ -110,25 +108,23 @@ __global__ void __launch_bounds__(1024) k_desc_plan(const int* __restrict__ coun
         *reinterpret_cast<long long*>(err + 2) = ps[1023];  // err is 16-byte aligned (errw)
         if (bad) atomicOr(err, 16);
     }
-    // perm: bitonic sort of (~count << 32 | q) ascending = count descending, q ascending
-    int P = 1;
-    while (P < k) P <<= 1;
-    for (int i = t; i < P; i += 1024)
-        keys[i] = i < k ? (((unsigned long long)(~(unsigned int)counts[i])) << 32) | (unsigned int)i : ~0ull;
+    // perm: keypoints by descending neighbourhood size in 16-point buckets (a counting sort; the
+    // order inside a bucket is arbitrary -- it only orders the apply launch, never the results)
     __syncthreads();
-    for (int sz = 2; sz <= P; sz <<= 1)
-        for (int st = sz >> 1; st > 0; st >>= 1) {
-            for (int i = t; i < P; i += 1024) {
-                const int j = i ^ st;
-                if (j > i) {
-                    const unsigned long long x = keys[i], y = keys[j];
-                    const bool up = (i & sz) == 0;
-                    if ((x > y) == up) { keys[i] = y; keys[j] = x; }
-                }
-            }
-            __syncthreads();
-        }
-    for (int i = t; i < k; i += 1024) perm[i] = (int)(keys[i] & 0xFFFFFFFFu);
+    pc[t] = 0;
+    __syncthreads();
+    for (int i = t; i < k; i += 1024) atomicAdd(&pc[1023 - min(1023, counts[i] >> 4)], 1);
+    __syncthreads();
+    const int own = pc[t];
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int w = t >= off ? pc[t - off] : 0;
+        __syncthreads();
+        pc[t] += w;
+        __syncthreads();
+    }
+    pc[t] -= own;  // exclusive bucket starts
+    __syncthreads();
+    for (int i = t; i < k; i += 1024) perm[atomicAdd(&pc[1023 - min(1023, counts[i] >> 4)], 1)] = i;
 }
 
 // exclusive scan of counts[0, k) by one workgroup of 1024 threads; offs[k] = total
