@@ -72,38 +72,47 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
     if (nidx < 3) return fallback();
     const double sample_thresh = sample_threshold(src, indices);
 
-    // ---- phase 1: the hypothesis stream (getSamples for iterations 0..max_iter). `pos` follows
-    // the shuffle of index values with their positions in `indices` (what the GPU scorer reads).
+    // ---- phase 1: the hypothesis stream (getSamples for iterations 0..max_iter), drawn lazily:
+    // draw_until(h) extends it to h hypotheses (fewer if a draw fails: the stream ends there).
+    // `pos` follows the shuffle of index values with their positions in `indices` (what the GPU
+    // scorer reads).
     std::mt19937 rng(12345u);
     std::vector<int> shuffled = indices, pos(nidx);
     for (int i = 0; i < nidx; ++i) pos[i] = i;
     std::vector<int> samples, spos;
     samples.reserve(3 * (size_t)(max_iter + 1));
     spos.reserve(3 * (size_t)(max_iter + 1));
-    for (int it = 0; it <= max_iter; ++it) {
-        bool got = false;
-        for (unsigned chk = 0; chk < 1000 && !got; ++chk) {
-            for (int i = 0; i < 3; ++i) {
-                const unsigned r = rng() >> 1;
-                const int j = i + (int)(r % (unsigned)(nidx - i));
-                std::swap(shuffled[i], shuffled[j]);
-                std::swap(pos[i], pos[j]);
+    bool stream_end = false;
+    auto draw_until = [&](int h) {
+        h = std::min(h, max_iter + 1);
+        while (!stream_end && (int)samples.size() / 3 < h) {
+            bool got = false;
+            for (unsigned chk = 0; chk < 1000 && !got; ++chk) {
+                for (int i = 0; i < 3; ++i) {
+                    const unsigned r = rng() >> 1;
+                    const int j = i + (int)(r % (unsigned)(nidx - i));
+                    std::swap(shuffled[i], shuffled[j]);
+                    std::swap(pos[i], pos[j]);
+                }
+                const Pt &a = src[shuffled[0]], &b = src[shuffled[1]], &c = src[shuffled[2]];
+                const float p10x = b.x - a.x, p10y = b.y - a.y, p10z = b.z - a.z;
+                const float p20x = c.x - a.x, p20y = c.y - a.y, p20z = c.z - a.z;
+                const float p21x = c.x - b.x, p21y = c.y - b.y, p21z = c.z - b.z;
+                got = (double)((p10x * p10x + p10y * p10y) + p10z * p10z) > sample_thresh &&
+                      (double)((p20x * p20x + p20y * p20y) + p20z * p20z) > sample_thresh &&
+                      (double)((p21x * p21x + p21y * p21y) + p21z * p21z) > sample_thresh;
             }
-            const Pt &a = src[shuffled[0]], &b = src[shuffled[1]], &c = src[shuffled[2]];
-            const float p10x = b.x - a.x, p10y = b.y - a.y, p10z = b.z - a.z;
-            const float p20x = c.x - a.x, p20y = c.y - a.y, p20z = c.z - a.z;
-            const float p21x = c.x - b.x, p21y = c.y - b.y, p21z = c.z - b.z;
-            got = (double)((p10x * p10x + p10y * p10y) + p10z * p10z) > sample_thresh &&
-                  (double)((p20x * p20x + p20y * p20y) + p20z * p20z) > sample_thresh &&
-                  (double)((p21x * p21x + p21y * p21y) + p21z * p21z) > sample_thresh;
+            if (!got) {
+                stream_end = true;
+                break;
+            }
+            for (int i = 0; i < 3; ++i) {
+                samples.push_back(shuffled[i]);
+                spos.push_back(pos[i]);
+            }
         }
-        if (!got) break;
-        for (int i = 0; i < 3; ++i) {
-            samples.push_back(shuffled[i]);
-            spos.push_back(pos[i]);
-        }
-    }
-    const int nhyp = (int)samples.size() / 3;
+        return (int)samples.size() / 3;
+    };
 
     // per-correspondence source / target points in index order (countWithinDistance loop order)
     std::vector<Pt> cs(nidx), ct(nidx);
@@ -131,10 +140,17 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
         return bg::umeyama<double>(sd, td, 3);
     };
 
-    // ---- GPU scores of every hypothesis (sample positions index cs/ct)
+    // ---- GPU scores of every hypothesis (sample positions index cs/ct), launched only when PCL's
+    // adaptive loop outlasts the host's share: the host scores the first host_max hypotheses
+    // itself (PCL usually stops within a few dozen), then the rest of the stream is drawn and the
+    // GPU scores it in one launch (identical counts: same float expression,
+    // tests/test_parity_gpu.py::test_ransac_dev_matches_host)
+    const int host_max = ctx ? std::max(8, 24000 / std::max(1, nidx)) : max_iter + 1;
     const int* gcnt = nullptr;
-    if (ctx && nhyp > 0) {
+    auto gpu_scores = [&]() -> int {
         bshot_ctx* c = ctx;
+        const int nhyp = draw_until(max_iter + 1);
+        if (nhyp <= 0) return BSHOT_OK;
         const size_t np = 6 * (size_t)nidx;
         if (c->rpts.ensure(np) || c->rhyp.ensure(3 * (size_t)nhyp) || c->rcnt.ensure(nhyp) || c->p_rpts.ensure(np) ||
             c->p_rhyp.ensure(3 * (size_t)nhyp) || c->p_rcnt.ensure(nhyp))
@@ -152,7 +168,8 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
         c->stage_end(sg);
         if (hipStreamSynchronize(c->stream)) return c->fail("ransac: sync", BSHOT_EHIP);
         gcnt = c->p_rcnt.p;
-    }
+        return BSHOT_OK;
+    };
 
     // ---- phase 2: RandomSampleConsensus::computeModel acceptance scan
     const double log_prob = std::log(1.0 - 0.99);
@@ -161,7 +178,12 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
     int best_cnt = -std::numeric_limits<int>::max();
     bg::Mat4f best_T = bg::Mat4f::identity();
     bool have = false;
-    for (int it = 0; it < nhyp && (double)it < k; ++it) {
+    for (int it = 0; (double)it < k; ++it) {
+        if (it >= host_max && ctx && !gcnt) {
+            const int e = gpu_scores();
+            if (e) return e;
+        }
+        if (draw_until(it + 1) <= it) break;  // the hypothesis stream ended
         int cnt;
         bg::Mat4f T;
         if (gcnt) {
