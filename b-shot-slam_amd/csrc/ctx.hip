@@ -361,15 +361,19 @@ int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n) {
 int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n) {
     (void)hipSetDevice(c->device);
     if (c->pf2.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->pre, c->pf2.ev_iss, 0), "wait old iss");
+    c->hmark("Q_load");
     int rc = cloud_load(c, c->pf2, d_xyz, n, c->pre);
     if (rc) return rc;
+    c->hmark("Q_sr");
     rc = cloud_sr(c, c->pf2, c->pre);
     if (rc) return rc;
+    c->hmark("Q_iss");
     if (c->prm.run_iss) {
         HIPCHK(hipStreamWaitEvent(c->iss, c->pf2.ev_loaded, 0), "wait cloud");
         rc = cloud_iss(c, c->pf2, c->iss);
         if (rc) return rc;
     }
+    c->hmark("Q_done");
     c->pf2.prefetched = true;
     return BSHOT_OK;
 }
