@@ -460,7 +460,9 @@ __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__
 // float-atomic unit of a CU is the limiter (~3 cycles per lane-op), so blocks are launched in
 // descending neighbourhood size (perm, host-sorted) and the LDS reservation caps residency at
 // 4 keypoints per CU: the largest start first and smaller ones fill in as CUs free up.
+#ifndef HA_LDS_PAD
 #define HA_LDS_PAD 8192
+#endif
 #ifndef HA_SKIP
 #define HA_SKIP 0
 #endif
