@@ -96,3 +96,26 @@ def test_odometry_lookahead_device_frames(depth):
             assert np.array_equal(_u(np.array(st.pose, np.float32)), _u(np.array(so.pose, np.float32))), f
     finally:
         od.close()
+
+
+def test_kp_test_config1_kp_evaluation():
+    """BASELINE config 1 / kp_test (test/kp_test.cpp:159-181): ground-free HDL-64 sweeps (N ~ 61k in
+    the synthetic scene, whose returns are half ground; ~120k in the reference's recordings),
+    K=600, kpEvaluation every frame (src/lidar_odometry.cpp:392-445): the SR and ISS 1-NN
+    repeatability rates equal the oracle's bit for bit, on top of the whole-frame parity."""
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=600, run_kp_eval=1))
+    oo = orc.Odometry(orc.params(num_keypoints=600))
+    try:
+        for f in range(3):
+            xyz, _ = bshot_py.synth_sweep(f, no_ground=True)
+            assert 40000 < len(xyz) < 130000
+            st = od.process(xyz)
+            so = oo.process(xyz)
+            assert st.n_keypoints == so.n_keypoints and st.n_iss == so.n_iss and st.n_inliers == so.n_inliers
+            if f > 0:
+                assert 0.0 < so.repeat_sr <= 1.0
+            assert np.float32(st.repeat_sr).view(np.uint32) == np.float32(so.repeat_sr).view(np.uint32), f
+            assert np.float32(st.repeat_iss).view(np.uint32) == np.float32(so.repeat_iss).view(np.uint32), f
+            assert np.array_equal(_u(np.array(st.pose)), _u(np.array(so.pose))), f
+    finally:
+        od.close()
