@@ -51,6 +51,7 @@ struct PreState {
     DBuf<unsigned> val, val2, perm;
     DBuf<int> cstart, colcell, colmin, tot, c_rm, c_sel, c_col, keep, offs, tab, ph0;
     DBuf<double> c_vr, c_dist, col_az, d_vj;
+    DBuf<float4> pts;
     DBuf<unsigned char> selm, tmp;
     DBuf<float> out;
     PinBuf<unsigned char> p_sel;
@@ -66,7 +67,7 @@ void pre_free(PreState* p) {
     p->val.release(); p->val2.release(); p->perm.release();
     p->cstart.release(); p->colcell.release(); p->colmin.release(); p->tot.release(); p->c_rm.release();
     p->c_sel.release(); p->c_col.release(); p->keep.release(); p->offs.release(); p->tab.release(); p->ph0.release();
-    p->c_vr.release(); p->c_dist.release(); p->col_az.release(); p->d_vj.release();
+    p->c_vr.release(); p->c_dist.release(); p->col_az.release(); p->d_vj.release(); p->pts.release();
     p->selm.release(); p->tmp.release(); p->out.release();
     p->p_sel.release(); p->p_vj.release(); p->p_tot.release();
     delete p;
@@ -120,17 +121,15 @@ __global__ void k_pre_flags(const bshot_laser* __restrict__ L, const unsigned* _
     cnt[s] = ((unsigned long long)(cell ? 1u : 0u) << 32) | (col ? 1u : 0u);
 }
 
-// cell / column starts, totals (tot[0] cells, tot[1] columns) and each column's lowest laser
-__global__ void k_pre_starts(const unsigned* __restrict__ perm, const unsigned long long* __restrict__ cnt,
-                             const unsigned long long* __restrict__ scan, int n2, int* __restrict__ cstart,
-                             int* __restrict__ colcell, int* __restrict__ colmin, int* __restrict__ tot) {
+// cell / column starts and totals (tot[0] cells, tot[1] columns)
+__global__ void k_pre_starts(const unsigned long long* __restrict__ cnt, const unsigned long long* __restrict__ scan,
+                             int n2, int* __restrict__ cstart, int* __restrict__ colcell, int* __restrict__ tot) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n2) return;
     const unsigned long long f = cnt[s], sc = scan[s];
     const int m = (int)(sc >> 32) - 1, c = (int)(sc & 0xFFFFFFFFu) - 1;
     if (f >> 32) cstart[m] = s;
     if (f & 0xFFFFFFFFu) colcell[c] = m;
-    atomicMin(&colmin[c], (int)(perm[s] >> 1));
     if (s == n2 - 1) {
         tot[0] = m + 1;
         tot[1] = c + 1;
@@ -140,12 +139,15 @@ __global__ void k_pre_starts(const unsigned* __restrict__ perm, const unsigned l
 }
 
 // one thread per cell: key (first event of the run), surviving value (last event), selection flag
-// of the last real return (-1: selmap has no entry), column
+// of the last real return (-1: selmap has no entry), column. Every laser of a column adds an event
+// to the column's vert_init_ cell and each such run ends with a synthetic event, so the first event
+// of that run belongs to the column's lowest laser: its azimuth is the column's key (colmin).
 __global__ void k_pre_cells(const bshot_laser* __restrict__ L, const unsigned* __restrict__ perm,
                             const unsigned long long* __restrict__ scan, const int* __restrict__ cstart,
                             const unsigned char* __restrict__ selm, const int* __restrict__ tot, double vinit,
                             double syn_dist, int n2, double* __restrict__ c_vr, double* __restrict__ c_dist,
-                            int* __restrict__ c_rm, int* __restrict__ c_sel, int* __restrict__ c_col) {
+                            int* __restrict__ c_rm, int* __restrict__ c_sel, int* __restrict__ c_col,
+                            int* __restrict__ colmin) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n2 || m >= tot[0]) return;
     const int s0 = cstart[m], s1 = cstart[m + 1] - 1;
@@ -167,7 +169,25 @@ __global__ void k_pre_cells(const bshot_laser* __restrict__ L, const unsigned* _
         }
     }
     c_sel[m] = sel;
-    c_col[m] = (int)(scan[s0] & 0xFFFFFFFFu) - 1;
+    const int col = (int)(scan[s0] & 0xFFFFFFFFu) - 1;
+    c_col[m] = col;
+    if (e1 & 1u) colmin[col] = (int)(e0 >> 1);
+}
+
+// per cell: the point the reference builds from it (double geometry, float Vector3f) and its
+// self-car test (src/preprocess.cpp:92-95, :147-152; the same point as writePointCloud's, :206-209)
+__global__ void k_pre_pts(const double* __restrict__ c_vr, const double* __restrict__ c_dist,
+                          const int* __restrict__ c_col, const double* __restrict__ col_az, const int* __restrict__ tot,
+                          int n2, float4* __restrict__ pts) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n2 || m >= tot[0]) return;
+    const double vr = c_vr[m], dist = c_dist[m], az = col_az[c_col[m]];
+    const double cv = cos(vr);
+    const double x = dist * cv * sin(az);
+    const double y = dist * cv * cos(az);
+    const double z = dist * sin(vr);
+    const bool selfcar = x <= 820 && x >= -820 && y <= 1300 && y >= -1800 && z <= 100 && z >= -2000;
+    pts[m] = make_float4((float)x, (float)y, (float)z, selfcar ? 1.f : 0.f);
 }
 
 // column keys: the azimuth of the column's lowest laser
@@ -184,28 +204,25 @@ struct F3 {
 __device__ __forceinline__ float f3norm(F3 a) { return sqrtf((a.x * a.x + a.y * a.y) + a.z * a.z); }
 
 // removeGround (src/preprocess.cpp:72-164): one thread per column, the reference's state machine
-// over the column's cells in vertical order (the first cell is skipped, :87-90)
+// over the column's cells in vertical order (the first cell is skipped, :87-90); the points and
+// self-car tests come precomputed per cell (k_pre_pts)
 __global__ void k_pre_ground(const int* __restrict__ colcell, const int* __restrict__ tot, int n2, PreConsts K,
-                             const double* __restrict__ c_vr, const double* __restrict__ c_dist,
+                             const double* __restrict__ c_dist, const float4* __restrict__ pts,
                              const double* __restrict__ col_az, int* __restrict__ c_rm) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n2 || c >= tot[1]) return;
     const double az = col_az[c];
     bool lost_pt = false, set_th_pt = false, prev_is_ground = true;
-    const double sa = sin(az), ca = cos(az);
-    const double x_0 = K.init_r * sa;  // (-2450/tan(vert_init_)) * sin(col.first)
-    const double y_0 = K.init_r * ca;
+    const double x_0 = K.init_r * sin(az);  // (-2450/tan(vert_init_)) * sin(col.first)
+    const double y_0 = K.init_r * cos(az);
     const double z_0 = -2450;
     F3 p_prev{(float)x_0, (float)y_0, (float)z_0};
     F3 p_th = p_prev;
     const int m1 = colcell[c + 1];
     for (int m = colcell[c] + 1; m < m1; ++m) {
-        const double vr = c_vr[m], dist = c_dist[m];
-        const double cv = cos(vr);
-        const double x = dist * cv * sa;
-        const double y = dist * cv * ca;
-        const double z = dist * sin(vr);
-        const F3 p_curr{(float)x, (float)y, (float)z};
+        const double dist = c_dist[m];
+        const float4 pc = pts[m];
+        const F3 p_curr{pc.x, pc.y, pc.z};
         const F3 d{p_curr.x - p_prev.x, p_curr.y - p_prev.y, p_curr.z - p_prev.z};
         // asin(float) * 180 is float arithmetic; the division by CV_PI promotes to double (:95)
         const double grad = (double)(asinf((p_curr.z - p_prev.z) / f3norm(d)) * 180.0f) / kPi;
@@ -243,7 +260,7 @@ __global__ void k_pre_ground(const int* __restrict__ colcell, const int* __restr
             rm = 1;
             prev_is_ground = true;
         }
-        if (x <= 820 && x >= -820 && y <= 1300 && y >= -1800 && z <= 100 && z >= -2000) rm = 2;
+        if (pc.w != 0.f) rm = 2;  // self-car box (:147-152)
         c_rm[m] = rm;
         p_prev = p_curr;
     }
@@ -323,22 +340,18 @@ __global__ void k_pre_keep(const double* __restrict__ c_vr, const double* __rest
     keep[m] = k;
 }
 
-__global__ void k_pre_write(const double* __restrict__ c_vr, const double* __restrict__ c_dist,
-                            const int* __restrict__ c_col, const double* __restrict__ col_az,
-                            const int* __restrict__ keep, const int* __restrict__ offs, const int* __restrict__ tot,
-                            int n2, int cap, float* __restrict__ xyz, int* __restrict__ n_out) {
+__global__ void k_pre_write(const float4* __restrict__ pts, const int* __restrict__ keep,
+                            const int* __restrict__ offs, const int* __restrict__ tot, int n2, int cap,
+                            float* __restrict__ xyz, int* __restrict__ n_out) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n2 || m >= tot[0]) return;
     const int o = offs[m];
     if (m == tot[0] - 1) *n_out = o + keep[m];
     if (!keep[m] || o >= cap) return;
-    const double vr = c_vr[m], dist = c_dist[m], az = col_az[c_col[m]];
-    const double x = dist * cos(vr) * sin(az);
-    const double y = dist * cos(vr) * cos(az);
-    const double z = dist * sin(vr);
-    xyz[3 * (size_t)o] = (float)x;
-    xyz[3 * (size_t)o + 1] = (float)y;
-    xyz[3 * (size_t)o + 2] = (float)z;
+    const float4 p = pts[m];
+    xyz[3 * (size_t)o] = p.x;
+    xyz[3 * (size_t)o + 1] = p.y;
+    xyz[3 * (size_t)o + 2] = p.z;
 }
 
 }  // namespace bpk
@@ -421,6 +434,7 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
     PCHK(P.c_vr.ensure(n2), "pre alloc"); PCHK(P.c_dist.ensure(n2), "pre alloc");
     PCHK(P.c_rm.ensure(n2), "pre alloc"); PCHK(P.c_sel.ensure(n2), "pre alloc"); PCHK(P.c_col.ensure(n2), "pre alloc");
     PCHK(P.col_az.ensure(n2), "pre alloc"); PCHK(P.keep.ensure(n2), "pre alloc"); PCHK(P.offs.ensure(n2), "pre alloc");
+    PCHK(P.pts.ensure(n2), "pre alloc");
     PCHK(P.ph0.ensure(J > 0 ? J : 1), "pre alloc"); PCHK(P.d_vj.ensure(J > 0 ? J : 1), "pre alloc");
     PCHK(P.p_tot.ensure(4), "pre alloc");
     size_t need = 0, tb = 0;
@@ -464,11 +478,12 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
     tb = P.tmp.cap;
     PCHK(rocprim::inclusive_scan(P.tmp.p, tb, P.cnt.p, P.scan.p, (size_t)n2, rocprim::plus<unsigned long long>(), st),
          "pre scan cells");
-    PCHK(hipMemsetAsync(P.colmin.p, 0x7F, sizeof(int) * (size_t)n2, st), "pre memset");
-    bpk::k_pre_starts<<<G, B, 0, st>>>(P.perm.p, P.cnt.p, P.scan.p, n2, P.cstart.p, P.colcell.p, P.colmin.p, P.tot.p);
+    bpk::k_pre_starts<<<G, B, 0, st>>>(P.cnt.p, P.scan.p, n2, P.cstart.p, P.colcell.p, P.tot.p);
     bpk::k_pre_cells<<<G, B, 0, st>>>(d_lasers, P.perm.p, P.scan.p, P.cstart.p, selm, P.tot.p, pp.vert_init,
-                                      P.syn_dist, n2, P.c_vr.p, P.c_dist.p, P.c_rm.p, P.c_sel.p, P.c_col.p);
+                                      P.syn_dist, n2, P.c_vr.p, P.c_dist.p, P.c_rm.p, P.c_sel.p, P.c_col.p,
+                                      P.colmin.p);
     bpk::k_pre_colaz<<<G, B, 0, st>>>(d_lasers, P.colmin.p, P.tot.p, n2, P.col_az.p);
+    bpk::k_pre_pts<<<G, B, 0, st>>>(P.c_vr.p, P.c_dist.p, P.c_col.p, P.col_az.p, P.tot.p, n2, P.pts.p);
     if (J > 0) PCHK(hipMemsetAsync(P.ph0.p, 0, sizeof(int) * J, st), "pre memset");
     c->stage_end(sg, st);
     PCHK(hipGetLastError(), "pre read launch");
@@ -481,7 +496,7 @@ int pre_ground(bshot_ctx* c) {
     if (P.n <= 0) return BSHOT_OK;
     const int n2 = 2 * P.n, B = 256, G = (n2 + B - 1) / B;
     const int sg = c->stage_begin(BSHOT_STAGE_PRE, c->stream);
-    bpk::k_pre_ground<<<G, B, 0, c->stream>>>(P.colcell.p, P.tot.p, n2, P.K, P.c_vr.p, P.c_dist.p, P.col_az.p,
+    bpk::k_pre_ground<<<G, B, 0, c->stream>>>(P.colcell.p, P.tot.p, n2, P.K, P.c_dist.p, P.pts.p, P.col_az.p,
                                               P.c_rm.p);
     c->stage_end(sg, c->stream);
     PCHK(hipGetLastError(), "pre ground launch");
@@ -523,8 +538,7 @@ int pre_write(bshot_ctx* c, float* d_xyz, int cap, int* n_out) {
     size_t tb = P.tmp.cap;
     PCHK(rocprim::exclusive_scan(P.tmp.p, tb, P.keep.p, P.offs.p, 0, (size_t)n2, rocprim::plus<int>(), st),
          "pre scan keep");
-    bpk::k_pre_write<<<G, B, 0, st>>>(P.c_vr.p, P.c_dist.p, P.c_col.p, P.col_az.p, P.keep.p, P.offs.p, P.tot.p, n2,
-                                      cap, d_xyz, P.tot.p + 2);
+    bpk::k_pre_write<<<G, B, 0, st>>>(P.pts.p, P.keep.p, P.offs.p, P.tot.p, n2, cap, d_xyz, P.tot.p + 2);
     c->stage_end(sg, st);
     PCHK(hipGetLastError(), "pre write launch");
     PCHK(hipMemcpyAsync(P.p_tot.p, P.tot.p, sizeof(int) * 4, hipMemcpyDeviceToHost, st), "pre D2H count");
