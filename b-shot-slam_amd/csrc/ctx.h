@@ -182,6 +182,7 @@ struct bshot_ctx {
     int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
     int opt_topk_thread = 1;   // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
     int opt_queue_thread = 0;  // LidarOdometry: the queued sweep's grids/SR/ISS launches issued from their own host thread
+    int opt_pre_fast = 1;  // preprocessor: one 32-bit sort for azimuth-ordered lasers with tabled verticals
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
     int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
     int opt_icp_tile = 1;  // 1: LDS-tiled NN over target spans (k_icp_tile); 0: wave per source point (k_icp_wave)

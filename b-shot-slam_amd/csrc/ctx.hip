@@ -1077,6 +1077,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
+    else if (k == "pre_fast") c->opt_pre_fast = value ? 1 : 0;
     else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;

@@ -43,7 +43,8 @@ struct PreState {
     double syn_dist = 0;
     int n = 0, cells = 0, cols = 0;
     bool counts_ok = false;  // cells / cols copied back since the last read
-    std::vector<double> vdeg, vj;
+    std::vector<double> vdeg, vj, rtab;
+    int vinit_rank = 0;
     std::vector<unsigned char> h_sel;
     DBuf<bshot_laser> lasers;
     PinBuf<bshot_laser> p_lasers;
@@ -52,6 +53,12 @@ struct PreState {
     DBuf<int> cstart, colcell, colmin, tot, c_rm, c_sel, c_col, keep, offs, tab, ph0;
     DBuf<double> c_vr, c_dist, col_az, d_vj;
     DBuf<float4> pts;
+    DBuf<int> colflag, colid, vrank, fbad;  // fast path
+    DBuf<unsigned> fkey, fkey2;
+    DBuf<double> d_rtab;
+    PinBuf<double> p_rtab;
+    PinBuf<int> p_fbad;
+    int fast_runs = 0, general_runs = 0;
     DBuf<unsigned char> selm, tmp;
     DBuf<float> out;
     PinBuf<unsigned char> p_sel;
@@ -68,6 +75,8 @@ void pre_free(PreState* p) {
     p->cstart.release(); p->colcell.release(); p->colmin.release(); p->tot.release(); p->c_rm.release();
     p->c_sel.release(); p->c_col.release(); p->keep.release(); p->offs.release(); p->tab.release(); p->ph0.release();
     p->c_vr.release(); p->c_dist.release(); p->col_az.release(); p->d_vj.release(); p->pts.release();
+    p->colflag.release(); p->colid.release(); p->vrank.release(); p->fbad.release(); p->fkey.release();
+    p->fkey2.release(); p->d_rtab.release(); p->p_rtab.release(); p->p_fbad.release();
     p->selm.release(); p->tmp.release(); p->out.release();
     p->p_sel.release(); p->p_vj.release(); p->p_tot.release();
     delete p;
@@ -108,17 +117,57 @@ __global__ void k_pre_akeys(const bshot_laser* __restrict__ L, const unsigned* _
 }
 
 // run starts: high word counts cells (equal azimuth and vertical), low word columns (equal azimuth)
-__global__ void k_pre_flags(const bshot_laser* __restrict__ L, const unsigned* __restrict__ perm,
-                            const unsigned long long* __restrict__ akey, int n2, double vinit,
-                            unsigned long long* __restrict__ cnt) {
+__global__ void k_pre_flags(const bshot_laser* __restrict__ L, const unsigned* __restrict__ perm, int n2,
+                            double vinit, unsigned long long* __restrict__ cnt) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n2) return;
     bool col = s == 0, cell = s == 0;
     if (s > 0) {
-        col = akey[s] != akey[s - 1];
-        cell = col || ordkey(ev_vertical(L, perm[s], vinit)) != ordkey(ev_vertical(L, perm[s - 1], vinit));
+        const unsigned e = perm[s], ep = perm[s - 1];
+        col = ordkey(L[e >> 1].azimuth * kPi / 180.0) != ordkey(L[ep >> 1].azimuth * kPi / 180.0);
+        cell = col || ordkey(ev_vertical(L, e, vinit)) != ordkey(ev_vertical(L, ep, vinit));
     }
     cnt[s] = ((unsigned long long)(cell ? 1u : 0u) << 32) | (col ? 1u : 0u);
+}
+
+// fast-path test: lasers already in nondecreasing azimuth order (every rotation the capture
+// pushes is, include/VelodyneCapture.h:474-489) and every vertical angle found in the rank table
+// (the vertical table plus vert_init_, sorted, distinct). bad[0] = 1 when either fails.
+// colflag[l] = 1 where a new azimuth starts; vrank[l] = rank of the laser's vertical.
+__global__ void k_pre_check(const bshot_laser* __restrict__ L, int n, const double* __restrict__ rtab, int nr,
+                            int* __restrict__ colflag, int* __restrict__ vrank, int* __restrict__ bad) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n) return;
+    const double az = L[l].azimuth * kPi / 180.0;
+    bool b = !(az == az);
+    int cf = 1;
+    if (l > 0) {
+        const unsigned long long k0 = ordkey(L[l - 1].azimuth * kPi / 180.0), k1 = ordkey(az);
+        if (k1 < k0) b = true;
+        cf = k1 != k0;
+    }
+    const double vr = L[l].vertical * kPi / 180.0;
+    int lo = 0, hi = nr;  // first rank with rtab >= vr
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rtab[mid] < vr) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= nr || !(rtab[lo] == vr)) b = true;
+    colflag[l] = cf;
+    vrank[l] = lo;
+    if (b) atomicOr(bad, 1);
+}
+
+// fast-path keys: (column << 9 | vertical rank) per event; one stable 32-bit sort then orders the
+// events by (azimuth, vertical, e) exactly as the two 64-bit sorts do
+__global__ void k_pre_fkeys(const int* __restrict__ colid, const int* __restrict__ vrank, int vinit_rank, int n2,
+                            unsigned* __restrict__ key, unsigned* __restrict__ val) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n2) return;
+    const int l = e >> 1;
+    key[e] = ((unsigned)(colid[l] - 1) << 9) | (unsigned)((e & 1) ? vinit_rank : vrank[l]);
+    val[e] = (unsigned)e;
 }
 
 // cell / column starts and totals (tot[0] cells, tot[1] columns)
@@ -413,6 +462,12 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
     const int J = (int)P.vdeg.size();
     P.vj.resize(J);
     for (int j = 0; j < J; ++j) P.vj[j] = P.vdeg[j] * bpk::kPi / 180.0;
+    // fast-path rank table: the table's angles and vert_init_, sorted, equal values merged (+-0 too)
+    P.rtab = P.vj;
+    P.rtab.push_back(pp.vert_init);
+    std::sort(P.rtab.begin(), P.rtab.end());
+    P.rtab.erase(std::unique(P.rtab.begin(), P.rtab.end(), [](double a, double b) { return a == b; }), P.rtab.end());
+    P.vinit_rank = (int)(std::lower_bound(P.rtab.begin(), P.rtab.end(), pp.vert_init) - P.rtab.begin());
     P.K.grad_th = 45;
     P.K.lowpt_th = pp.lowpt_th;
     P.K.height_th = 500;
@@ -449,6 +504,15 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
     PCHK(rocprim::exclusive_scan(nullptr, tb, P.keep.p, P.offs.p, 0, (size_t)n2, rocprim::plus<int>(), st),
          "pre scan size");
     need = std::max(need, tb);
+    tb = 0;
+    PCHK(rocprim::radix_sort_pairs(nullptr, tb, (unsigned*)nullptr, (unsigned*)nullptr, P.val.p, P.perm.p, (unsigned)n2, 0,
+                                   32, st),
+         "pre sort size");
+    need = std::max(need, tb);
+    tb = 0;
+    PCHK(rocprim::inclusive_scan(nullptr, tb, (int*)nullptr, (int*)nullptr, (size_t)n, rocprim::plus<int>(), st),
+         "pre scan size");
+    need = std::max(need, tb);
     PCHK(P.tmp.ensure(need), "pre alloc tmp");
     const unsigned char* selm = nullptr;
     if (pp.have_sel_list) {
@@ -466,15 +530,46 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
     }
     const int sg = c->stage_begin(BSHOT_STAGE_PRE, st);
     const int B = 256, G = (n2 + B - 1) / B;
-    bpk::k_pre_vkeys<<<G, B, 0, st>>>(d_lasers, n2, pp.vert_init, P.vkey.p, P.val.p);
-    tb = P.tmp.cap;
-    PCHK(rocprim::radix_sort_pairs(P.tmp.p, tb, P.vkey.p, P.vkey2.p, P.val.p, P.val2.p, (unsigned)n2, 0, 64, st),
-         "pre sort vertical");
-    bpk::k_pre_akeys<<<G, B, 0, st>>>(d_lasers, P.val2.p, n2, P.akey.p);
-    tb = P.tmp.cap;
-    PCHK(rocprim::radix_sort_pairs(P.tmp.p, tb, P.akey.p, P.akey2.p, P.val2.p, P.perm.p, (unsigned)n2, 0, 64, st),
-         "pre sort azimuth");
-    bpk::k_pre_flags<<<G, B, 0, st>>>(d_lasers, P.perm.p, P.akey2.p, n2, pp.vert_init, P.cnt.p);
+    // fast path (azimuth-ordered lasers whose verticals are all in the table): one 32-bit sort of
+    // (column, vertical rank); otherwise two stable 64-bit sorts (vertical, then azimuth)
+    bool fast = false;
+    if (c->opt_pre_fast && !P.rtab.empty() && P.rtab.size() <= 512 && n < (1 << 22)) {
+        const int nr = (int)P.rtab.size();
+        PCHK(P.colflag.ensure(n), "pre alloc"); PCHK(P.colid.ensure(n), "pre alloc"); PCHK(P.vrank.ensure(n), "pre alloc");
+        PCHK(P.fbad.ensure(1), "pre alloc"); PCHK(P.p_fbad.ensure(1), "pre alloc");
+        PCHK(P.d_rtab.ensure(nr), "pre alloc"); PCHK(P.p_rtab.ensure(nr), "pre alloc");
+        std::memcpy(P.p_rtab.p, P.rtab.data(), sizeof(double) * nr);
+        PCHK(hipMemcpyAsync(P.d_rtab.p, P.p_rtab.p, sizeof(double) * nr, hipMemcpyHostToDevice, st), "pre H2D ranks");
+        PCHK(hipMemsetAsync(P.fbad.p, 0, sizeof(int), st), "pre memset");
+        bpk::k_pre_check<<<(n + B - 1) / B, B, 0, st>>>(d_lasers, n, P.d_rtab.p, nr, P.colflag.p, P.vrank.p, P.fbad.p);
+        PCHK(hipMemcpyAsync(P.p_fbad.p, P.fbad.p, sizeof(int), hipMemcpyDeviceToHost, st), "pre D2H check");
+        PCHK(hipStreamSynchronize(st), "pre sync check");
+        fast = P.p_fbad.p[0] == 0;
+    }
+    if (fast) {
+        P.fast_runs++;
+        PCHK(P.fkey.ensure(n2), "pre alloc"); PCHK(P.fkey2.ensure(n2), "pre alloc");
+        tb = P.tmp.cap;
+        PCHK(rocprim::inclusive_scan(P.tmp.p, tb, P.colflag.p, P.colid.p, (size_t)n, rocprim::plus<int>(), st),
+             "pre scan columns");
+        bpk::k_pre_fkeys<<<G, B, 0, st>>>(P.colid.p, P.vrank.p, P.vinit_rank, n2, P.fkey.p, P.val.p);
+        const int bits = 9 + (32 - __builtin_clz((unsigned)n));  // column ids < n
+        tb = P.tmp.cap;
+        PCHK(rocprim::radix_sort_pairs(P.tmp.p, tb, P.fkey.p, P.fkey2.p, P.val.p, P.perm.p, (unsigned)n2, 0,
+                                       std::min(bits, 32), st),
+             "pre sort (column, vertical)");
+    } else {
+        P.general_runs++;
+        bpk::k_pre_vkeys<<<G, B, 0, st>>>(d_lasers, n2, pp.vert_init, P.vkey.p, P.val.p);
+        tb = P.tmp.cap;
+        PCHK(rocprim::radix_sort_pairs(P.tmp.p, tb, P.vkey.p, P.vkey2.p, P.val.p, P.val2.p, (unsigned)n2, 0, 64, st),
+             "pre sort vertical");
+        bpk::k_pre_akeys<<<G, B, 0, st>>>(d_lasers, P.val2.p, n2, P.akey.p);
+        tb = P.tmp.cap;
+        PCHK(rocprim::radix_sort_pairs(P.tmp.p, tb, P.akey.p, P.akey2.p, P.val2.p, P.perm.p, (unsigned)n2, 0, 64, st),
+             "pre sort azimuth");
+    }
+    bpk::k_pre_flags<<<G, B, 0, st>>>(d_lasers, P.perm.p, n2, pp.vert_init, P.cnt.p);
     tb = P.tmp.cap;
     PCHK(rocprim::inclusive_scan(P.tmp.p, tb, P.cnt.p, P.scan.p, (size_t)n2, rocprim::plus<unsigned long long>(), st),
          "pre scan cells");

@@ -47,11 +47,12 @@ def main(tag):
         durs = collections.defaultdict(list)
         for r in csv.DictReader(open(tr)):
             durs[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-        with open(os.path.join(dst, f"{tag}_kernel_median.csv"), "w") as f:
-            f.write("kernel,launches,median_us,mean_us,min_us,max_us\n")
+        with open(os.path.join(dst, f"{tag}_kernel_median.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "launches", "median_us", "mean_us", "min_us", "max_us"])
             for k, v in sorted(durs.items(), key=lambda kv: -sum(kv[1])):
                 v.sort()
-                f.write(f"{k},{len(v)},{v[len(v) // 2]:.1f},{sum(v) / len(v):.1f},{v[0]:.1f},{v[-1]:.1f}\n")
+                w.writerow([k, len(v), f"{v[len(v) // 2]:.1f}", f"{sum(v) / len(v):.1f}", f"{v[0]:.1f}", f"{v[-1]:.1f}"])
     for f in (f"prof_bench_{tag}.json", f"bench_{tag}.json", f"bench_{tag}.err", f"pytest_gpu_{tag}.log", f"smoke_{tag}.log"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f"{tag}_{f.replace('_' + tag, '')}"))

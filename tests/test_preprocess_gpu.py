@@ -36,11 +36,16 @@ def _check(ctx, L, vlist, vert_init=-0.6, lowpt=-1950.0, sel=None, save=True):
     return g
 
 
+@pytest.mark.parametrize("fast", [1, 0])
 @pytest.mark.parametrize("sensor,frame", [(2, 0), (2, 7), (0, 0), (1, 3)])
-def test_synthetic_rotation_exact(ctx, sensor, frame):
+def test_synthetic_rotation_exact(ctx, sensor, frame, fast):
+    """Azimuth-ordered rotations with tabled verticals take the one-sort fast path (fast=1); the
+    general two-sort path (knob pre_fast=0) must give the same bits."""
+    ctx.set_option("pre_fast", fast)
     L = bshot_py.synth_lasers(frame, sensor=sensor)
     g = _check(ctx, L, bshot_py.sensor_vertical_angles(sensor))
     assert len(g) > 10000
+    ctx.set_option("pre_fast", 1)
 
 
 def test_shuffled_with_duplicates_and_selection(ctx):
