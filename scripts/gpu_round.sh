@@ -27,4 +27,9 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o fetch --out
 echo "[gpu_round] $(date +%T) pmc WRITE_SIZE" &&
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$TAG -o write --output-format csv -- \
     python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_write_$TAG.log 2>&1 &&
+echo "[gpu_round] $(date +%T) preprocessor + capture kernels" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pre_$TAG -o t --output-format csv -- \
+    python3 $R/b-shot-slam_amd/tools/pre_bench.py 30 > $O/pre_bench_$TAG.log 2>&1 &&
+grep "^{" $O/pre_bench_$TAG.log > $O/pre_bench_$TAG.json &&
+cat $O/pre_bench_$TAG.json &&
 echo "[gpu_round] $(date +%T) done"

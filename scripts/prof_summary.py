@@ -53,7 +53,10 @@ def main(tag):
             for k, v in sorted(durs.items(), key=lambda kv: -sum(kv[1])):
                 v.sort()
                 w.writerow([k, len(v), f"{v[len(v) // 2]:.1f}", f"{sum(v) / len(v):.1f}", f"{v[0]:.1f}", f"{v[-1]:.1f}"])
-    for f in (f"prof_bench_{tag}.json", f"bench_{tag}.json", f"bench_{tag}.err", f"pytest_gpu_{tag}.log", f"smoke_{tag}.log"):
+    pre = os.path.join(src, f"prof_pre_{tag}", "t_kernel_stats.csv")
+    if os.path.exists(pre):
+        shutil.copy(pre, os.path.join(dst, f"{tag}_preprocess_kernel_stats.csv"))
+    for f in (f"pre_bench_{tag}.json", f"prof_bench_{tag}.json", f"bench_{tag}.json", f"bench_{tag}.err", f"pytest_gpu_{tag}.log", f"smoke_{tag}.log"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f"{tag}_{f.replace('_' + tag, '')}"))
     print(json.dumps({k: v for k, v in out["kernels"].items() if "k_seg_ratio" in k or "k_shot_hist" in k}))
