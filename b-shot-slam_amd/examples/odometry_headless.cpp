@@ -5,11 +5,15 @@
 // Output: one line per frame, "frame <id> <n_points> <n_inliers> <pose row-major, 16 x %a>".
 //
 //   bin/odometry_headless [frames=5] [keypoints=600] [sensor=0] [sr_type=CV] [pre=0] [pcap=<file>]
+//                         [trajectory=<file>]
+// The trajectory file is odometry_test's "Save trajectories" output (:348-361): the translation of
+// every frame's pose, "x y z" per line (default stream formatting), then an empty line.
 // With a pcap file (HDL-32E packets) the loop is odometry_test's whole chain: HDL32ECapture ->
 // Preprocessor -> LidarOdometry (:60-61, :111-194).
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <fstream>
 #include <cstdlib>
 #include <memory>
 #include <string>
@@ -31,6 +35,8 @@ int main(int argc, char** argv) {
     const std::string sr = argc > 4 ? argv[4] : "CV";
     const std::string pcap = argc > 6 ? argv[6] : "";
     const bool pre = (argc > 5 && std::atoi(argv[5]) != 0) || !pcap.empty();
+    const std::string traj_file = argc > 7 ? argv[7] : "";
+    std::vector<myslam::Vector3f> trajectory;
     bshot_params p;
     bshot_default_params(&p);
     p.num_keypoints = k;
@@ -101,6 +107,7 @@ int main(int argc, char** argv) {
             lo.updateMap();
             lo.updateCorrespondence();
             const myslam::Matrix4f P = fptr->getPose();
+            trajectory.push_back(P.topRightCorner());  // odometry_test.cpp:195-198
             std::printf("frame %d %d %d", f, n, (int)lo.inlierCorrespondences().size());
             for (int j = 0; j < 16; ++j) std::printf(" %a", P.m[j]);
             std::printf("\n");
@@ -108,6 +115,11 @@ int main(int argc, char** argv) {
     } catch (const std::exception& e) {
         std::fprintf(stderr, "odometry_headless: %s\n", e.what());
         return 1;
+    }
+    if (!traj_file.empty()) {
+        std::ofstream ofs(traj_file);
+        for (const myslam::Vector3f& p : trajectory) ofs << p[0] << " " << p[1] << " " << p[2] << std::endl;
+        ofs << std::endl;
     }
     return 0;
 }

@@ -80,8 +80,9 @@ def test_pcap_capture_preprocess_odometry_chain(tmp_path):
     path = tmp_path / "hdl32.pcap"
     write_pcap(path, pk, [(1_600_000_000 + i // 100, (i * 553) % 1_000_000) for i in range(len(pk))])
     frames, k = 3, 600
-    out = subprocess.run([EXE, str(frames), str(k), "2", "CV", "1", str(path)], capture_output=True, text=True,
-                         timeout=300)
+    traj = tmp_path / "traj.txt"
+    out = subprocess.run([EXE, str(frames), str(k), "2", "CV", "1", str(path), str(traj)], capture_output=True,
+                         text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     lines = [ln.split() for ln in out.stdout.splitlines() if ln.startswith("frame ")]
     assert len(lines) == frames
@@ -96,3 +97,10 @@ def test_pcap_capture_preprocess_odometry_chain(tmp_path):
         assert int(ln[2]) == len(xyz) and int(ln[3]) == st.n_inliers, (f, ln[:4], st.n_inliers)
         pose = np.array([float.fromhex(x) for x in ln[4:20]], np.float32)
         assert np.array_equal(pose.view(np.uint32), np.array(st.pose, np.float32).view(np.uint32)), f
+    # odometry_test's trajectory file: "x y z" of every pose (default 6-significant-digit output), then ""
+    rows = traj.read_text().split("\n")
+    assert rows[frames] == "" and len([r for r in rows if r]) == frames
+    for f, ln in enumerate(lines):
+        pose = np.array([float.fromhex(x) for x in ln[4:20]], np.float32).reshape(4, 4)
+        got = np.array([float(v) for v in rows[f].split()])
+        assert np.allclose(got, pose[:3, 3], rtol=1e-5, atol=1e-3), (f, got, pose[:3, 3])
