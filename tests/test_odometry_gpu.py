@@ -70,17 +70,21 @@ def test_odometry_no_icp_no_iss():
     _run_pair(range(3), run_icp=0, run_iss=0)
 
 
-@pytest.mark.parametrize("depth", [1, 2])
-def test_odometry_lookahead_device_frames(depth):
+@pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"queue_thread": 1}), (2, {"topk_thread": 0}),
+                                        (2, {"icp_tile": 0, "ransac_dev": 0})])
+def test_odometry_lookahead_device_frames(depth, opts):
     """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
     stream during the current one (bshot_odom_set_next_device; depth 2 also queues the sweep after
-    next, bshot_odom_set_next2_device) -- results must not change."""
+    next, bshot_odom_set_next2_device) -- results must not change, whichever host threading
+    (queue thread, top-K thread) and ICP / RANSAC variant the knobs select."""
     import torch
 
     frames = [bshot_py.synth_sweep(f)[0] for f in range(20, 25)]
     dev = [torch.from_numpy(x).to("cuda:0") for x in frames]
     torch.cuda.synchronize()
     od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=1024))
+    for name, val in opts.items():
+        od.set_option(name, val)
     oo = orc.Odometry(orc.params(num_keypoints=1024))
     try:
         for f, (xyz, d) in enumerate(zip(frames, dev)):
