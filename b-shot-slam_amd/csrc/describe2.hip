@@ -466,90 +466,35 @@ __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__
 #ifndef HA_SKIP
 #define HA_SKIP 0
 #endif
-__global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps, int k, const int* __restrict__ perm,
-                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                   const int* __restrict__ ok_in,
-                                                   const unsigned short* __restrict__ recS,
-                                                   const float* __restrict__ recV, float* __restrict__ shot_out,
-                                                   unsigned int* __restrict__ bits_out) {
-    __shared__ float hist[384];
-    __shared__ unsigned int gcode[88];
-    __shared__ float pad_[HA_LDS_PAD];  // residency cap (see above)
-    const int lane = lane_id();
-    const int q = perm[blockIdx.x];
-    if (lane == 0 && q < 0) pad_[0] = 0.f;
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const long long o = offs[q];
-    const int n = (int)(offs[q + 1] - o);
-    const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
-    const bool good = fin && ok_in[q] && n >= 5;
-    for (int j = lane; j < 384; j += 64) hist[j] = 0.0f;
-    __builtin_amdgcn_wave_barrier();
-    if (good && lane < 5) {
-        // lane j applies record slot j of every rank, in rank order: one ds_add_f32 per rank with
-        // lanes 0..4 (distinct bins within a rank), so every bin sees its adds in PCL's order. A
-        // lane reads its slot's chunk rows straight from memory (64 bins as 32 dwords, 64 values),
-        // the next chunk's rows in flight while this one is applied.
-        const int c_end = cb[q + 1];
-        auto load = [&](int c, uint4* bw, float4* vw) {
-            const uint4* b4 = reinterpret_cast<const uint4*>(recS + (size_t)c * 320 + 64 * lane);
-            const float4* v4 = reinterpret_cast<const float4*>(recV + (size_t)c * 320 + 64 * lane);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) bw[u] = b4[u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) vw[u] = v4[u];
-        };
-        uint4 bw[8], nbw[8];
-        float4 vw[16], nvw[16];
-        int c = cb[q];
-        load(c, bw, vw);
-        for (; c < c_end; ++c) {
-            if (c + 1 < c_end) load(c + 1, nbw, nvw);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const unsigned int w[4] = {bw[u].x, bw[u].y, bw[u].z, bw[u].w};
-#pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    const int r = 8 * u + 2 * h;  // ranks r, r + 1 of the chunk
-                    const float4 va = vw[r >> 2];
-                    const float v0 = (r & 3) == 0 ? va.x : va.z;
-                    const float v1 = (r & 3) == 0 ? va.y : va.w;
-#if HA_SKIP
-                    // no-op records (bin 360, +0) issue no LDS atomic
-                    if ((w[h] & 0xFFFFu) < 352u) atomicAdd(&hist[w[h] & 0xFFFFu], v0);
-                    if ((w[h] >> 16) < 352u) atomicAdd(&hist[w[h] >> 16], v1);
-#else
-                    atomicAdd(&hist[w[h] & 0xFFFFu], v0);
-                    atomicAdd(&hist[w[h] >> 16], v1);
+// keypoints per wave: group g owns lanes 5g..5g+4 and its own LDS histogram, so one in-order
+// ds_add_f32 carries the records of HA_G keypoints (their adds never share an address). HA_G > 1
+// measured slower (the atomic unit, not instruction issue, is the limit)
+#ifndef HA_G
+#define HA_G 1
 #endif
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) bw[u] = nbw[u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) vw[u] = nvw[u];
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_wave_barrier();
+static_assert(5 * HA_G <= 64, "HA_G groups of 5 lanes must fit a wave");
+
+// normalizeHistogram + B-SHOT of one keypoint's histogram h (wave-uniform q, good)
+__device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q, bool good, int lane,
+                                            float* __restrict__ shot_out, unsigned int* __restrict__ bits_out) {
     // normalizeHistogram: double accumulation of float squares in bin order
     float sv[6];
     if (good) {
         double acc = 0.0;
         if (lane == 0)
             for (int j = 0; j < 352; j += 8) {
-                float h[8];
+                float hv[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) h[u] = hist[j + u];
+                for (int u = 0; u < 8; ++u) hv[u] = h[j + u];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) acc = acc + (double)(h[u] * h[u]);
+                for (int u = 0; u < 8; ++u) acc = acc + (double)(hv[u] * hv[u]);
             }
         acc = __shfl(acc, 0, 64);
         const float fa = (float)sqrt(acc);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             const int b = lane + 64 * j;
-            sv[j] = b < 352 ? hist[b] / fa : 0.f;
+            sv[j] = b < 352 ? h[b] / fa : 0.f;
         }
     } else {
 #pragma unroll
@@ -560,7 +505,7 @@ __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps
     for (int j = 0; j < 6; ++j) {
         const int b = lane + 64 * j;
         if (b < 352) {
-            hist[b] = sv[j];
+            h[b] = sv[j];
             if (shot_out) shot_out[352 * (size_t)q + b] = sv[j];
         }
     }
@@ -568,10 +513,10 @@ __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps
     // B-SHOT: 88 groups of 4 (include/bshot_bits.h:144-278)
     unsigned int code[2] = {0u, 0u};
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int gidx = lane + 64 * h;
+    for (int hh = 0; hh < 2; ++hh) {
+        const int gidx = lane + 64 * hh;
         if (gidx < 88) {
-            const float v0 = hist[4 * gidx], v1 = hist[4 * gidx + 1], v2 = hist[4 * gidx + 2], v3 = hist[4 * gidx + 3];
+            const float v0 = h[4 * gidx], v1 = h[4 * gidx + 1], v2 = h[4 * gidx + 2], v3 = h[4 * gidx + 3];
             const float sum = ((v0 + v1) + v2) + v3;
             const double th = 0.9 * (double)sum;
             unsigned b;
@@ -591,7 +536,7 @@ __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps
             else if ((double)((v0 + v2) + v3) > th) b = 13;
             else if ((double)((v0 + v1) + v3) > th) b = 11;
             else b = 15;
-            code[h] = b;
+            code[hh] = b;
         }
     }
     if (lane < 88) gcode[lane] = code[0];
@@ -602,6 +547,98 @@ __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps
 #pragma unroll
         for (int j = 0; j < 8; ++j) w |= gcode[8 * lane + j] << (4 * j);
         bits_out[11 * (size_t)q + lane] = w;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ bool apply_good(const float* __restrict__ kps, const long long* __restrict__ offs,
+                                           const int* __restrict__ ok_in, int q) {
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const int n = (int)(offs[q + 1] - offs[q]);
+    const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
+    return fin && ok_in[q] && n >= 5;
+}
+
+// HA_G keypoints per wave (perm[HA_G * blockIdx.x + g]); launched with ceil(k / HA_G) blocks
+__global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps, int k, const int* __restrict__ perm,
+                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
+                                                   const int* __restrict__ ok_in,
+                                                   const unsigned short* __restrict__ recS,
+                                                   const float* __restrict__ recV, float* __restrict__ shot_out,
+                                                   unsigned int* __restrict__ bits_out) {
+    __shared__ float hist[HA_G * 384];
+    __shared__ unsigned int gcode[88];
+    __shared__ float pad_[HA_LDS_PAD];  // residency cap (see above)
+    const int lane = lane_id();
+    const int g = lane / 5, slot = lane - 5 * g;
+    const int p0 = HA_G * blockIdx.x;
+    if (lane == 0 && perm[p0] < 0) pad_[0] = 0.f;
+    for (int j = lane; j < HA_G * 384; j += 64) hist[j] = 0.0f;
+    __builtin_amdgcn_wave_barrier();
+    // lane (g, slot) applies record slot `slot` of every rank of keypoint g, in rank order: one
+    // ds_add_f32 per rank with the 5 lanes of each group (distinct bins within a rank), so every
+    // bin sees its adds in PCL's order. A lane reads its slot's chunk rows straight from memory
+    // (64 bins as 32 dwords, 64 values), the next chunk's rows in flight while this one is applied.
+    int c0 = 0, nch = 0;
+    if (g < HA_G && p0 + g < k) {
+        const int q = perm[p0 + g];
+        if (apply_good(kps, offs, ok_in, q)) {
+            c0 = cb[q];
+            nch = cb[q + 1] - c0;
+        }
+    }
+    int tmax = nch;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) tmax = max(tmax, __shfl_xor(tmax, m, 64));
+    if (tmax > 0) {
+        float* hg = hist + 384 * (g < HA_G ? g : 0);
+        auto load = [&](int c, uint4* bw, float4* vw) {
+            const uint4* b4 = reinterpret_cast<const uint4*>(recS + (size_t)c * 320 + 64 * slot);
+            const float4* v4 = reinterpret_cast<const float4*>(recV + (size_t)c * 320 + 64 * slot);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bw[u] = b4[u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) vw[u] = v4[u];
+        };
+        uint4 bw[8], nbw[8];
+        float4 vw[16], nvw[16];
+        if (nch > 0) load(c0, bw, vw);
+        for (int t = 0; t < tmax; ++t) {
+            const bool act = t < nch;
+            if (t + 1 < nch) load(c0 + t + 1, nbw, nvw);
+            if (act) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const unsigned int w[4] = {bw[u].x, bw[u].y, bw[u].z, bw[u].w};
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        const int r = 8 * u + 2 * h;  // ranks r, r + 1 of the chunk
+                        const float4 va = vw[r >> 2];
+                        const float v0 = (r & 3) == 0 ? va.x : va.z;
+                        const float v1 = (r & 3) == 0 ? va.y : va.w;
+#if HA_SKIP
+                        // no-op records (bin 360, +0) issue no LDS atomic
+                        if ((w[h] & 0xFFFFu) < 352u) atomicAdd(&hg[w[h] & 0xFFFFu], v0);
+                        if ((w[h] >> 16) < 352u) atomicAdd(&hg[w[h] >> 16], v1);
+#else
+                        atomicAdd(&hg[w[h] & 0xFFFFu], v0);
+                        atomicAdd(&hg[w[h] >> 16], v1);
+#endif
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bw[u] = nbw[u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) vw[u] = nvw[u];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();
+    for (int gg = 0; gg < HA_G; ++gg) {
+        if (p0 + gg >= k) break;
+        const int q = perm[p0 + gg];
+        hist_finish(hist + 384 * gg, gcode, q, apply_good(kps, offs, ok_in, q), lane, shot_out, bits_out);
     }
 }
 
@@ -645,7 +682,7 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.n_chunks > 0)
         bsk::k_hist_contrib<<<cblocks, 256, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.offs, A.cb, A.owner,
                                                      A.sorted, A.rf, A.ok, A.recS, A.recV);
-    bsk::k_hist_apply<<<A.k, 64, 0, s>>>(A.kps, A.k, A.perm, A.offs, A.cb, A.ok, A.recS, A.recV, A.shot, A.bits);
+    bsk::k_hist_apply<<<(A.k + HA_G - 1) / HA_G, 64, 0, s>>>(A.kps, A.k, A.perm, A.offs, A.cb, A.ok, A.recS, A.recV, A.shot, A.bits);
     return hipGetLastError();
 }
 

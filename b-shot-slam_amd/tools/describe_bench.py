@@ -1,5 +1,6 @@
 """Diagnostic: standalone (uncontended) describe timing per stage for describe2 knob settings.
 usage: python describe_bench.py [knob values, default 2 1]"""
+import hashlib
 import json
 import os
 import sys
@@ -32,5 +33,6 @@ for arg in sys.argv[1:] or ["2", "1"]:
     same = ref is None or np.array_equal(bits, ref)
     ref = bits if ref is None else ref
     ms = {k: round(v[0] / 10, 4) for k, v in st.items() if v[1]}
-    print(json.dumps({"describe2": d2, "identical_bits": bool(same), "total_ms": round(sum(ms.values()), 4), **ms}))
+    print(json.dumps({"describe2": d2, "identical_bits": bool(same), "bits_sha": hashlib.sha1(bits.tobytes()).hexdigest()[:12],
+                      "shot_sha": hashlib.sha1(shot.tobytes()).hexdigest()[:12], "total_ms": round(sum(ms.values()), 4), **ms}))
 c.close()
