@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
                         bool p = false, m = false;
                         if (r < need) {
                             const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
-                            const float dot = (tx * vx + ty * vy) + tz * vz;
+                            const float dot = tx * vx + (ty * vy + tz * vz);
                             p = dot > 0.f;
                             m = dot < 0.f;
                         }
@@ -496,7 +496,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
                     out = 1.0f - fminf(fp, fm) / fmaxf(fp, fm);
                 } else {
                     // CVS / CVSN: per-neighbour terms in parallel, sequential float sum in rank order
-                    const float ctn = sqrtf((tx * tx + ty * ty) + tz * tz);
+                    const float ctn = sqrtf(tx * tx + (ty * ty + tz * tz));
                     // a skipped neighbour stores +0: sum + (+0) == sum, as sum starts at +0 and so
                     // is never -0 (the only value +0 changes)
                     float* term = fl + 1536;
@@ -504,8 +504,8 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
                         const int r = r0 + lane;
                         if (r < need) {
                             const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
-                            const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
-                            const float dot = (tx * vx + ty * vy) + tz * vz;
+                            const float vn = sqrtf(vx * vx + (vy * vy + vz * vz));
+                            const float dot = tx * vx + (ty * vy + tz * vz);
                             const bool use = !(ctn == 0.f || vn == 0.f);
                             term[r] = !use ? 0.f : (sr_type == 1 ? dot : dot / (ctn * vn));
                         }

@@ -21,10 +21,12 @@ struct Vector3f {
     Vector3f operator-(const Vector3f& o) const { return Vector3f(v[0] - o.v[0], v[1] - o.v[1], v[2] - o.v[2]); }
     Vector3f operator*(float s) const { return Vector3f(v[0] * s, v[1] * s, v[2] * s); }
     bool operator==(const Vector3f& o) const { return v[0] == o.v[0] && v[1] == o.v[1] && v[2] == o.v[2]; }
-    float dot(const Vector3f& o) const { return (v[0] * o.v[0] + v[1] * o.v[1]) + v[2] * o.v[2]; }
-    float squaredNorm() const { return (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]; }
+    // Eigen 3.2 reductions of a 3-vector (no packet access: DefaultTraversal, CompleteUnrolling)
+    // go through redux_novec_unroller, which halves the range: a0 + (a1 + a2).
+    float dot(const Vector3f& o) const { return v[0] * o.v[0] + (v[1] * o.v[1] + v[2] * o.v[2]); }
+    float squaredNorm() const { return v[0] * v[0] + (v[1] * v[1] + v[2] * v[2]); }
     float norm() const { return std::sqrt(squaredNorm()); }
-    float sum() const { return (v[0] + v[1]) + v[2]; }
+    float sum() const { return v[0] + (v[1] + v[2]); }
     static Vector3f Zero() { return Vector3f(); }
 };
 

@@ -101,20 +101,20 @@ static float seg_ratio_one(const P3* pts, const P3& sp, const std::vector<std::p
         for (const auto& e : nn) {
             const P3& p = pts[e.second];
             const float vx = p.x - sp.x, vy = p.y - sp.y, vz = p.z - sp.z;
-            const float dot = (tx * vx + ty * vy) + tz * vz;
+            const float dot = tx * vx + (ty * vy + tz * vz);  // Vector3f::dot: Eigen redux a0 + (a1 + a2)
             if (dot > 0) pos += 1.0f;
             else if (dot < 0) neg += 1.0f;
         }
         return 1.0f - std::min(pos, neg) / std::max(pos, neg);
     }
-    const float ctn = std::sqrt((tx * tx + ty * ty) + tz * tz);
+    const float ctn = std::sqrt(tx * tx + (ty * ty + tz * tz));
     float sum = 0.f;
     for (const auto& e : nn) {
         const P3& p = pts[e.second];
         const float vx = p.x - sp.x, vy = p.y - sp.y, vz = p.z - sp.z;
-        const float vn = std::sqrt((vx * vx + vy * vy) + vz * vz);
+        const float vn = std::sqrt(vx * vx + (vy * vy + vz * vz));
         if (ctn == 0.f || vn == 0.f) continue;
-        const float dot = (tx * vx + ty * vy) + tz * vz;
+        const float dot = tx * vx + (ty * vy + tz * vz);
         if (sr_type == 1) sum += dot;
         else sum += dot / (ctn * vn);
     }

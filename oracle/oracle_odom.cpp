@@ -31,7 +31,7 @@ struct Kp {
 // Map::MapHasher (include/mymap.h:12-25): abs(round(p.sum())) on the float sum
 struct MapHasher {
     unsigned long operator()(const V3& p) const {
-        const float s = (p.v[0] + p.v[1]) + p.v[2];
+        const float s = p.v[0] + (p.v[1] + p.v[2]);  // Eigen redux order a0 + (a1 + a2)
         return (unsigned long)std::fabs(std::round(s));
     }
 };
@@ -64,7 +64,7 @@ class OMap {
         for (auto& e : blocks[id]) {
             const float dx = kp->pos.v[0] - e.first.v[0], dy = kp->pos.v[1] - e.first.v[1],
                         dz = kp->pos.v[2] - e.first.v[2];
-            if (std::sqrt((dx * dx + dy * dy) + dz * dz) < 800 && kp->ratio <= e.second->ratio) cand = false;
+            if (std::sqrt(dx * dx + (dy * dy + dz * dz)) < 800 && kp->ratio <= e.second->ratio) cand = false;
         }
         if (cand) blocks[id][kp->pos] = kp;
     }
@@ -249,7 +249,7 @@ class OOdom {
         inv44(ref->pose, Ti_inv);
         mul44(Ti_inv, ransac_T, Tij);
         const float h_diff = std::acos(Tij[5]);
-        const float t_diff = std::sqrt((Tij[3] * Tij[3] + Tij[7] * Tij[7]) + Tij[11] * Tij[11]);
+        const float t_diff = std::sqrt(Tij[3] * Tij[3] + (Tij[7] * Tij[7] + Tij[11] * Tij[11]));
         st->h_diff = h_diff;
         st->t_diff = t_diff;
         float T_est[16];

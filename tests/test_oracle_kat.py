@@ -130,21 +130,21 @@ def _sr_ref(xyz, i, nn, sr_type):
         pos = neg = f(0)
         for j in nn:
             v = (xyz[j] - sp).astype(np.float32)
-            dot = f(f(t[0] * v[0] + t[1] * v[1]) + t[2] * v[2])
+            dot = f(t[0] * v[0] + f(t[1] * v[1] + t[2] * v[2]))  # Eigen redux: a0 + (a1 + a2)
             if dot > 0:
                 pos = f(pos + f(1))
             elif dot < 0:
                 neg = f(neg + f(1))
         with np.errstate(invalid="ignore", divide="ignore"):
             return f(f(1) - f(min(pos, neg) / max(pos, neg)))
-    ctn = f(np.sqrt(f(f(t[0] * t[0] + t[1] * t[1]) + t[2] * t[2])))
+    ctn = f(np.sqrt(f(t[0] * t[0] + f(t[1] * t[1] + t[2] * t[2]))))
     s = f(0)
     for j in nn:
         v = (xyz[j] - sp).astype(np.float32)
-        vn = f(np.sqrt(f(f(v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])))
+        vn = f(np.sqrt(f(v[0] * v[0] + f(v[1] * v[1] + v[2] * v[2]))))
         if ctn == 0 or vn == 0:
             continue
-        dot = f(f(t[0] * v[0] + t[1] * v[1]) + t[2] * v[2])
+        dot = f(t[0] * v[0] + f(t[1] * v[1] + t[2] * v[2]))  # Eigen redux: a0 + (a1 + a2)
         s = f(s + (dot if sr_type == 1 else f(dot / f(ctn * vn))))
     return f(abs(s) / f(len(nn)))
 
