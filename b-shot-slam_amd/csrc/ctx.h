@@ -131,6 +131,11 @@ struct bshot_ctx {
     // persistent normals (include/bshot_bits.h:59): logical size + grow-only storage
     DBuf<float4> normals;
     int normals_size = 0;
+    // the state a lookahead describe started from (ctx_normals_snapshot), put back if its result
+    // is dropped instead of adopted (ctx_normals_restore): slots [0, snap_n) and the logical size
+    DBuf<float4> normals_snap;
+    int normals_snap_size = -1;  // -1: no snapshot held
+    int normals_snap_n = 0;
 
     // describe
     DBuf<float> kps;
@@ -248,6 +253,13 @@ int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1 = false);
+// persistent-normals state around a lookahead describe of k keypoints on stream st: a describe
+// writes slots [0, k) and zero-fills past the logical size, so slots [0, min(k, size)) and the size
+// are all it can change. snapshot: queued on st before the describe; restore: after the describe
+// finished (the worker synchronised st), when its result is dropped; discard: when it is adopted.
+int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k);
+int ctx_normals_restore(bshot_ctx* c);
+void ctx_normals_discard(bshot_ctx* c);
 // after a describe's error word reached the host (err[0..3] as copied from c->errw): true when the
 // describe must be run again -- errw bit 16, a device plan over capacity (the re-run plans on the
 // host; the capacity hint grows to the total the device counted)

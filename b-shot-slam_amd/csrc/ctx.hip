@@ -391,6 +391,31 @@ int ctx_iss_launch(bshot_ctx* c) {
     return cloud_iss(c, c->cs, c->iss);
 }
 
+int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k) {
+    const int m = std::min(std::max(k, 0), c->normals_size);
+    c->normals_snap_size = c->normals_size;
+    c->normals_snap_n = m;
+    if (m > 0) {
+        HIPCHK(c->normals_snap.ensure(m), "alloc normals snapshot");
+        HIPCHK(hipMemcpyAsync(c->normals_snap.p, c->normals.p, sizeof(float4) * m, hipMemcpyDeviceToDevice, st),
+               "snapshot normals");
+    }
+    return BSHOT_OK;
+}
+
+int ctx_normals_restore(bshot_ctx* c) {
+    if (c->normals_snap_size < 0) return BSHOT_OK;
+    if (c->normals_snap_n > 0)
+        HIPCHK(hipMemcpyAsync(c->normals.p, c->normals_snap.p, sizeof(float4) * c->normals_snap_n,
+                              hipMemcpyDeviceToDevice, c->stream),
+               "restore normals");
+    c->normals_size = c->normals_snap_size;
+    c->normals_snap_size = -1;
+    return BSHOT_OK;
+}
+
+void ctx_normals_discard(bshot_ctx* c) { c->normals_snap_size = -1; }
+
 // keypoints already in c->kps (device, k x 3)
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1) {
     if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > 512)

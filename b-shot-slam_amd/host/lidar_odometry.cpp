@@ -133,6 +133,14 @@ void LidarOdometry::joinAhead() {
     ready_ = la;
 }
 
+// a lookahead result that is not adopted: its describe already advanced the persistent normals
+// (include/bshot_bits.h:59) past the state the sweep actually described next must start from
+void LidarOdometry::dropReady() {
+    if (!ready_) return;
+    ready_.reset();
+    check(bsh::ctx_normals_restore(ctx_), "restore normals");
+}
+
 void LidarOdometry::check(int rc, const char* where) {
     if (rc >= 0) return;
     err_ = std::string(where) + ": " + (ctx_ ? bshot_last_error(ctx_) : "no context");
@@ -140,6 +148,14 @@ void LidarOdometry::check(int rc, const char* where) {
 }
 
 void LidarOdometry::setSRType(std::string sr_type) {
+    // a type change takes effect at the next extractKeypoints (as in the reference): sweeps already
+    // prefetched or queued with the old type are dropped, after their threads are done
+    joinQueue();
+    joinAhead();
+    dropReady();
+    dropTopkAhead();
+    ctx_->pf.prefetched = false;
+    ctx_->pf2.prefetched = false;
     sr_type_ = sr_type;
     prm_.sr_type = sr_type == "CVS" ? 1 : (sr_type == "CVSN" ? 2 : 0);
     ctx_->prm.sr_type = prm_.sr_type;
@@ -153,7 +169,7 @@ void LidarOdometry::setRefFrame(Frame::Ptr ref) {
 void LidarOdometry::setSrcFrame(Frame::Ptr src) {
     joinQueue();
     joinAhead();
-    ready_.reset();
+    dropReady();
     src_ = src;
     src_pc_ = *src_->getPointCloud();
     src_dev_ = nullptr;
@@ -166,7 +182,7 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
     joinQueue();
     joinAhead();
     ctx_->hmark("M_joined");
-    if (ready_ && !(ready_->d_xyz == d_xyz && ready_->n == n)) ready_.reset();
+    if (ready_ && !(ready_->d_xyz == d_xyz && ready_->n == n)) dropReady();
     src_ = src;
     src_pc_.clear();
     src_dev_ = d_xyz;
@@ -177,7 +193,7 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
 void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
     joinQueue();
     joinAhead();
-    ready_.reset();
+    dropReady();
     // grids + SR + ISS on the side stream (after everything already queued on the main stream,
     // i.e. after this sweep's describe, whose normals the next describe continues from)
     ctx_->hmark("M_prefetch");
@@ -291,6 +307,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
     TicToc t_d;
     // describe is queued on the side stream; while it runs, ISS (own stream) is collected
     c->hmark("W_topk_done");
+    if (bsh::ctx_normals_snapshot(c, c->side, k) != BSHOT_OK) fail("lookahead normals snapshot");
     if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
     c->hmark("W_describe_queued");
     TicToc t_iss;
@@ -424,6 +441,7 @@ void LidarOdometry::computeDescriptors() {
         }
         src_->setDescriptors(desc);
         ready_.reset();
+        bsh::ctx_normals_discard(ctx_);  // adopted: its normals are the state to continue from
         stats_.host_ms[2] = (float)t_d.toc();
         return;
     }
@@ -611,7 +629,10 @@ void LidarOdometry::kpEvaluation() {
 }
 
 PointCloudXYZ LidarOdometry::issKpDetection(const PointCloudXYZ& kps) {
-    // standalone ISS over an arbitrary cloud (src/lidar_odometry.cpp:447-461)
+    // standalone ISS over an arbitrary cloud (src/lidar_odometry.cpp:447-461); the lookahead threads
+    // finish first (they issue on the context's streams), their prefetched results stay valid
+    joinQueue();
+    joinAhead();
     const int n = (int)kps.size();
     check(bshot_set_cloud(ctx_, n ? kps.data()->v : nullptr, n), "iss set cloud");
     std::vector<int32_t> iss(n > 0 ? n : 1);

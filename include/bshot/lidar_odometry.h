@@ -87,6 +87,7 @@ class LidarOdometry {
     void runAhead(Lookahead& la);
     void joinAhead();
     void dropTopkAhead();
+    void dropReady();
     struct QueueAhead;
     void joinQueue();
     std::shared_ptr<QueueAhead> queue_ahead_;  // sweep after next: its launches issued on their own thread

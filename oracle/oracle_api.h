@@ -95,6 +95,8 @@ void oracle_umeyama(const double* src, const double* dst, int n, int use_float, 
 /* OpenMP threads for the stages the reference runs with OpenMP (normals, SHOT) */
 void oracle_set_threads(int n);
 int oracle_get_threads(void);
+/* threads for the per-point SR and ISS loops (default 1, as the reference); results do not depend on it */
+void oracle_set_point_threads(int n);
 
 void oracle_default_params(oracle_params* p);
 void* oracle_odom_create(const oracle_params* p);

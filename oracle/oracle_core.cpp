@@ -127,23 +127,36 @@ using namespace orc;
 
 extern "C" {
 
+// Threads for the per-point SR / ISS loops. 1 by default: the reference runs them single-threaded
+// (src/lidar_odometry.cpp:61, :457), and bench.py's cpu_baseline keeps that. The golden-fixture
+// generator raises it; every point is independent and the output is compacted in index order, so
+// the results do not depend on the thread count.
+static int g_point_threads = 1;
+
 int oracle_seg_ratio(const float* xyz, int n, float radius, int max_nn, int sr_type, int32_t* idx_out,
                      float* ratio_out, int* n_out) {
     const P3* pts = reinterpret_cast<const P3*>(xyz);
     Grid g(pts, n, radius * 0.25f);
-    std::vector<std::pair<float, int>> nn;
-    int m = 0;
-    for (int i = 0; i < n; ++i) {
-        const P3& sp = pts[i];
-        if (sp.x == 0 && sp.y == 0 && sp.z == 0) continue;  // :63-64
-        g.radius_knn(sp, radius, max_nn, nn);
-        if (nn.empty()) continue;  // radiusSearch(...) > 0 (:70)
-        const float r = seg_ratio_one(pts, sp, nn, sr_type);
-        if (std::isnan(r)) continue;  // :121-122
-        idx_out[m] = i;
-        ratio_out[m] = r;
-        ++m;
+    std::vector<float> r_all(n > 0 ? n : 1);
+    std::vector<uint8_t> ok(n > 0 ? n : 1, 0);
+#pragma omp parallel num_threads(g_point_threads)
+    {
+        std::vector<std::pair<float, int>> nn;
+#pragma omp for schedule(dynamic, 256)
+        for (int i = 0; i < n; ++i) {
+            const P3& sp = pts[i];
+            if (sp.x == 0 && sp.y == 0 && sp.z == 0) continue;  // :63-64
+            g.radius_knn(sp, radius, max_nn, nn);
+            if (nn.empty()) continue;  // radiusSearch(...) > 0 (:70)
+            const float r = seg_ratio_one(pts, sp, nn, sr_type);
+            if (std::isnan(r)) continue;  // :121-122
+            r_all[i] = r;
+            ok[i] = 1;
+        }
     }
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        if (ok[i]) { idx_out[m] = i; ratio_out[m] = r_all[i]; ++m; }
     *n_out = m;
     return 0;
 }
@@ -171,45 +184,56 @@ int oracle_iss(const float* xyz, int n, float salient, float nonmax, double g21,
     {
         Grid g(pts, n, salient);
         const float r2 = (float)((double)salient * (double)salient);
-        std::vector<std::pair<float, int>> nn;
-        for (int i = 0; i < n; ++i) {
-            const P3& c = pts[i];
-            if (!finite3(c)) continue;
-            g.radius_all(c, r2, nn);
-            if ((int)nn.size() < min_nn) continue;  // zero scatter -> NaN ratios -> rejected
-            const double cx = c.x, cy = c.y, cz = c.z;
-            double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            for (const auto& e : nn) {
-                const double d[3] = {(double)pts[e.second].x - cx, (double)pts[e.second].y - cy,
-                                     (double)pts[e.second].z - cz};
-                for (int a = 0; a < 3; ++a)
-                    for (int b = 0; b < 3; ++b) cov[a * 3 + b] += d[a] * d[b];
+#pragma omp parallel num_threads(g_point_threads)
+        {
+            std::vector<std::pair<float, int>> nn;
+#pragma omp for schedule(dynamic, 256)
+            for (int i = 0; i < n; ++i) {
+                const P3& c = pts[i];
+                if (!finite3(c)) continue;
+                g.radius_all(c, r2, nn);
+                if ((int)nn.size() < min_nn) continue;  // zero scatter -> NaN ratios -> rejected
+                const double cx = c.x, cy = c.y, cz = c.z;
+                double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                for (const auto& e : nn) {
+                    const double d[3] = {(double)pts[e.second].x - cx, (double)pts[e.second].y - cy,
+                                         (double)pts[e.second].z - cz};
+                    for (int a = 0; a < 3; ++a)
+                        for (int b = 0; b < 3; ++b) cov[a * 3 + b] += d[a] * d[b];
+                }
+                double w[3], v[9];
+                o_jacobi3(cov, w, v);
+                const double e1c = w[2], e2c = w[1], e3c = w[0];
+                if (!std::isfinite(e1c) || !std::isfinite(e2c) || !std::isfinite(e3c)) continue;
+                if (e3c < 0) continue;
+                if ((e2c / e1c) < g21 && (e3c / e2c) < g32) third[i] = e3c;
             }
-            double w[3], v[9];
-            o_jacobi3(cov, w, v);
-            const double e1c = w[2], e2c = w[1], e3c = w[0];
-            if (!std::isfinite(e1c) || !std::isfinite(e2c) || !std::isfinite(e3c)) continue;
-            if (e3c < 0) continue;
-            if ((e2c / e1c) < g21 && (e3c / e2c) < g32) third[i] = e3c;
         }
     }
     int m = 0;
     {
         Grid g(pts, n, nonmax);
         const float r2 = (float)((double)nonmax * (double)nonmax);
-        std::vector<std::pair<float, int>> nn;
-        for (int i = 0; i < n; ++i) {
-            if (!(third[i] > 0.0) || !finite3(pts[i])) continue;
-            g.radius_all(pts[i], r2, nn);
-            if ((int)nn.size() < min_nn) continue;
-            bool is_max = true;
-            for (const auto& e : nn)
-                if (third[i] < third[e.second]) { is_max = false; break; }
-            if (is_max) {
+        std::vector<uint8_t> keep(n > 0 ? n : 1, 0);
+#pragma omp parallel num_threads(g_point_threads)
+        {
+            std::vector<std::pair<float, int>> nn;
+#pragma omp for schedule(dynamic, 256)
+            for (int i = 0; i < n; ++i) {
+                if (!(third[i] > 0.0) || !finite3(pts[i])) continue;
+                g.radius_all(pts[i], r2, nn);
+                if ((int)nn.size() < min_nn) continue;
+                bool is_max = true;
+                for (const auto& e : nn)
+                    if (third[i] < third[e.second]) { is_max = false; break; }
+                keep[i] = is_max;
+            }
+        }
+        for (int i = 0; i < n; ++i)
+            if (keep[i]) {
                 if (m < cap) out_idx[m] = i;
                 ++m;
             }
-        }
     }
     if (third_eig)
         for (int i = 0; i < n; ++i) third_eig[i] = third[i];
@@ -774,6 +798,8 @@ void oracle_set_threads(int n) {
     (void)n;
 #endif
 }
+
+void oracle_set_point_threads(int n) { g_point_threads = n > 0 ? n : 1; }
 
 int oracle_get_threads(void) {
 #ifdef _OPENMP

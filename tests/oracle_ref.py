@@ -249,6 +249,12 @@ def set_threads(n):
     return lib().oracle_get_threads()
 
 
+def set_point_threads(n):
+    """Threads for the oracle's per-point SR/ISS loops (default 1, as the reference). Used by the
+    golden generator only; results do not depend on it."""
+    lib().oracle_set_point_threads(int(n))
+
+
 # ---- preprocessor (oracle/oracle_pre.cpp; reference src/preprocess.cpp) ----------------------------
 class OPreParams(ctypes.Structure):
     _fields_ = [("vert_init", ctypes.c_double), ("lowpt_th", ctypes.c_double), ("have_sel_list", ctypes.c_int),
