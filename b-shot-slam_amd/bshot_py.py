@@ -63,7 +63,7 @@ ABI_SYMBOLS = [
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
     "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
-    "bshot_odom_set_option", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
+    "bshot_odom_set_option", "bshot_odom_drain", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
     "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
     "bshot_pcap_load", "bshot_velodyne_decode", "bshot_velodyne_decode_device",
 ]
@@ -410,6 +410,10 @@ class Odometry:
     def set_next2_device(self, dptr, n):
         """Lookahead depth 2: the device cloud of the process_device call after next."""
         self._chk(self.L.bshot_odom_set_next2_device(self.h, P(dptr), n), "odom_set_next2_device")
+
+    def drain(self):
+        """Wait for the lookahead work in flight (bshot_odom_drain); prefetched results stay ready."""
+        self._chk(self.L.bshot_odom_drain(self.h), "odom_drain")
 
     def process_device(self, dptr, n):
         st = FrameStats()

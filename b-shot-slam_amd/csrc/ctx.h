@@ -112,6 +112,7 @@ struct bshot_ctx {
     bshot_params prm;
     std::string err;
     bool timing = false;
+    unsigned timing_mask = ~0u;  // stages timed while timing is on (bit = BSHOT_STAGE_*)
 
     CloudState cs;  // current cloud
     CloudState pf;  // prefetch slot (next sweep: the lookahead worker describes it)

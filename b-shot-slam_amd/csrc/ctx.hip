@@ -68,7 +68,7 @@ void bshot_ctx::hmark(const char* name) {
 }
 
 int bshot_ctx::stage_begin(int st, hipStream_t s) {
-    if (!timing) return -1;
+    if (!timing || !((timing_mask >> st) & 1u)) return -1;
     std::lock_guard<std::mutex> lk(evmu);
     StageEv e{st, get_ev(), get_ev(), ++stage_seq, false};
     (void)hipEventRecord(e.a, s ? s : stream);
@@ -1107,6 +1107,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
     else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;
+    else if (k == "timing_mask") c->timing_mask = (unsigned)value;
     else if (k == "dev_plan_hint") c->seg_hint = value < 0 ? 0 : value;  // tests: force / avoid a re-plan
     else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;

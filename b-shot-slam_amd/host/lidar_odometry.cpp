@@ -116,6 +116,12 @@ void LidarOdometry::joinQueue() {
     }
 }
 
+void LidarOdometry::drainLookahead() {
+    joinQueue();
+    joinAhead();
+    if (topk_ahead_ && topk_ahead_->th.joinable()) topk_ahead_->th.join();
+}
+
 void LidarOdometry::dropTopkAhead() {
     if (topk_ahead_ && topk_ahead_->th.joinable()) topk_ahead_->th.join();
     topk_ahead_.reset();

@@ -149,6 +149,11 @@ int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2
     return BSHOT_OK;
 }
 
+int bshot_odom_drain(bshot_odom* o) {
+    if (!o) return BSHOT_EINVAL;
+    return guard(o, [&]() { o->lo->drainLookahead(); });
+}
+
 int bshot_odom_process(bshot_odom* o, const float* xyz, int n, bshot_frame_stats* st) {
     if (!o || n < 0 || (n > 0 && !xyz)) return BSHOT_EINVAL;
     return guard(o, [&]() { run_frame(o, xyz, nullptr, n, st); });

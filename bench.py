@@ -31,20 +31,20 @@ import bshot_py  # noqa: E402
 from dist_map import exchange_map_delta  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+L2_PEAK_GBPS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md "L2 (per XCD)")
 
 
-def pmc_traffic(stage):
-    """HBM bytes per launch of the stage's kernel from the newest committed PMC summary
-    (profiles/rNN_pmc.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE, separate passes)."""
+def pmc_kernel(stage):
+    """Counters of the stage's kernel from the newest committed PMC summary (profiles/rNN_pmc.json,
+    scripts/pmc_summary.py): HBM bytes per launch (rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE,
+    separate passes) and, where collected, the SQ / TCC / TCP derived metrics."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
     if not files:
         return None, None
     try:
         k = json.load(open(files[-1]))["kernels"].get(f"bsk::k_{stage}")
-        if not k:
-            return None, None
-        return round(k.get("hbm_read_bytes", 0.0) + k.get("hbm_write_bytes", 0.0)), os.path.relpath(files[-1], ROOT)
+        return (k or None), os.path.relpath(files[-1], ROOT)
     except (OSError, ValueError, KeyError):
         return None, None
 
@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
+    ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage HIP events in the timed region")
     ap.add_argument("--depth", type=int, default=2, help="lookahead depth (1: next sweep only, 2: two sweeps)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="process sweeps strictly one after another (no lookahead of the next sweep's SR/ISS)")
@@ -89,7 +90,12 @@ def main():
 
     dev = torch.device("cuda", local)
     params = bshot_py.default_params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
-    nframes = a.warmup + a.steps
+    # steady state at both edges of the timed region: the last warm-up sweep starts the first timed
+    # sweep's lookahead, and the last timed sweep starts the lookahead of `extra` sweeps past the
+    # region, which finishes inside it (bshot_odom_drain) -- the region holds exactly K sweeps' work
+    extra = 0 if a.no_prefetch else max(1, min(2, a.depth))
+    nframes = a.warmup + a.steps + extra
+    nwork = a.warmup + a.steps
     seed = 42 + rank
     # synthetic sequence for this rank, uploaded to HBM before timing
     t0 = time.time()
@@ -130,17 +136,13 @@ def main():
     tot_pts = 0
 
     def step(i):
-        # sweeps are preprocessed when first needed (this one or a lookahead), timed sweeps inside
-        # the timed region only
+        # sweeps are preprocessed when first needed (this one or a lookahead)
         for j in (i, i + 1, i + 2):
-            if j < a.warmup or i >= a.warmup:
-                prep(j)
-        # lookahead inside each region only: the last warm-up sweep does not start the first timed
-        # sweep, so the timed region holds exactly K sweeps' work
-        if not a.no_prefetch and i + 1 < nframes and i + 1 != a.warmup:
+            prep(j)
+        if not a.no_prefetch and i + 1 < nframes:
             odo.set_next_device(frames[i + 1].data_ptr(), npts[i + 1])
             # depth 2: the sweep after next gets its grids/SR/ISS queued beside the next describe
-            if a.depth >= 2 and i + 2 < nframes and i + 2 != a.warmup:
+            if a.depth >= 2 and i + 2 < nframes:
                 odo.set_next2_device(frames[i + 2].data_ptr(), npts[i + 2])
         st = odo.process_device(frames[i].data_ptr(), npts[i])
         if a.map_bcast and world > 1:
@@ -150,7 +152,10 @@ def main():
 
     for i in range(a.warmup):
         step(i)
-    odo.set_timing(True)
+    # HIP events cost host time on every launch they bracket: in the default run only the stage of
+    # the roofline kernel (SR) is timed; --profile-stages times them all
+    odo.set_option("timing_mask", -1 if a.profile_stages else 1 << 1)
+    odo.set_timing(not a.no_stage_timing)
     odo.stage_reset()
     if pre_ctx is not None:
         pre_ctx.set_timing(True)
@@ -161,10 +166,11 @@ def main():
     t0 = time.perf_counter()
     stats = []
     marks = []
-    for i in range(a.warmup, nframes):
+    for i in range(a.warmup, nwork):
         stats.append(step(i))
         marks.append(time.perf_counter())
         tot_pts += npts[i]
+    odo.drain()  # the lookahead started by the last timed sweep finishes inside the region
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -191,7 +197,7 @@ def main():
     k_eff = float(np.mean([s.n_keypoints for s in stats]))
     m_eff = float(np.mean([s.n_target for s in stats]))
     icp_it = float(np.mean([s.icp_iters for s in stats]))
-    n_eff = float(np.mean(npts[a.warmup:]))
+    n_eff = float(np.mean(npts[a.warmup:nwork]))
     ctx.close()
     # the dominant kernel among those with an algorithmic-bytes figure (k_seg_ratio in every
     # configuration measured so far, profiles/*_kernel_stats.csv)
@@ -206,21 +212,36 @@ def main():
     dname = dom[0]
     roof = None
     if dname in alg and per_launch_ms[dname] > 0:
-        ach = alg[dname] / (per_launch_ms[dname] * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic(dname)
-        roof = {"kernel": dname, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": tsrc, "alg_bytes_per_launch": alg[dname],
-                "ms_per_launch": round(per_launch_ms[dname], 4),
-                "convention": "SURVEY.md 8(d) pair-gather bytes; DESIGN.md section 4"}
+        t_launch = per_launch_ms[dname] * 1e-3
+        pmc, psrc = pmc_kernel(dname)
+        traffic = round(pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]) if pmc and "hbm_read_bytes" in pmc else None
+        roof = {"kernel": dname, "ms_per_launch": round(per_launch_ms[dname], 4), "traffic": traffic,
+                "traffic_unit": "HBM bytes/launch (PMC)", "pmc_source": psrc}
         if dname == "seg_ratio":
-            # the same launch on the candidate-gather convention: the float4 candidates the radius
-            # ladder actually streams (64 per chunk) + query read + ratio write
+            # the bytes the launch actually moves: the float4 candidates the radius ladder streams
+            # (64 per chunk) + query read + ratio write. The per-sweep footprint (2 MB cloud + grids)
+            # sits in L2, so those bytes are L2-served: the memory level this kernel touches is L2.
             g = 16.0 * 64.0 * kst[5] + 20.0 * n_eff
-            roof["gather_bytes_per_launch"] = g
-            roof["achieved_gather"] = round(g / (per_launch_ms[dname] * 1e-3) / 1e9, 1)
-            roof["frac_gather"] = round(roof["achieved_gather"] / HBM_PEAK_GBPS, 4)
-            roof["candidates_per_query"] = round(64.0 * kst[5] / max(1, kst[0]), 1)
+            ach = g / t_launch / 1e9
+            roof.update({"bound": "l2", "achieved": round(ach, 1), "peak": L2_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / L2_PEAK_GBPS, 4), "bytes_per_launch": g,
+                         "candidates_per_query": round(64.0 * kst[5] / max(1, kst[0]), 1)})
+        else:
+            ach = alg[dname] / t_launch / 1e9
+            roof.update({"bound": "l2", "achieved": round(ach, 1), "peak": L2_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / L2_PEAK_GBPS, 4), "bytes_per_launch": alg[dname]})
+        if traffic is not None:
+            roof["hbm_achieved"] = round(traffic / t_launch / 1e9, 1)
+            roof["hbm_frac"] = round(traffic / t_launch / 1e9 / HBM_PEAK_GBPS, 5)
+        if pmc:
+            # what limits the kernel, from the SQ/TCC counters of the committed PMC passes
+            roof["limiter"] = {k: pmc[k] for k in ("limiter", "valu_issue_frac", "lds_busy_frac", "lds_bank_conflict_frac",
+                                                    "waves_per_cu", "wave_wait_frac", "wave_issue_stall_frac",
+                                                    "l2_hit_rate") if k in pmc}
+        # SURVEY.md 8(d) pair-gather convention (every in-radius pair counted as read): informational
+        # only -- the radius ladder never reads most of those pairs, so it is no roofline fraction
+        roof["alg_pair_gather_bytes"] = alg[dname]
+        roof["alg_pair_gather_GBps"] = round(alg[dname] / t_launch / 1e9, 1)
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference algorithm), rank 0 only
     cpu = None
@@ -232,19 +253,25 @@ def main():
         op = oracle_ref.params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
         od = oracle_ref.Odometry(op)
         nf = a.cpu_frames
-        t1 = time.perf_counter()
-        for f in range(nf):
+
+        def cpu_frame(o, f):
             if a.from_lasers:
                 # the oracle preprocessor (std::map restatement) runs inside the timed CPU sample too
                 L = lasers[f][0].cpu().numpy().view(bshot_py.LASER_DTYPE)
                 xyz, _ = oracle_ref.preprocess(L, vert, -0.6, -1950.0)
-                od.process(xyz)
+                o.process(xyz)
             else:
-                od.process(frames[f].cpu().numpy())
+                o.process(frames[f].cpu().numpy())
+
+        # sweep 0 (the initial self-match) untimed: the sample is steady-state sweeps 1..nf
+        cpu_frame(od, 0)
+        t1 = time.perf_counter()
+        for f in range(1, nf + 1):
+            cpu_frame(od, f)
         ct = time.perf_counter() - t1
         cpu = {"value": round(nf / ct, 4), "unit": "sweeps/s", "cores": nthr, "kind": "port",
                "sample": ("preprocessor + " if a.from_lasers else "") +
-                         f"first {nf} sweeps of the same synthetic sequence (N~{int(n_eff)}, K={a.keypoints}), full "
+                         f"sweeps 1..{nf} (after the untimed initial sweep 0) of the same synthetic sequence (N~{int(n_eff)}, K={a.keypoints}), full "
                          f"path, oracle/ C++ restatement (PCL unavailable); {ct:.1f} s; SR/ISS/Hamming/RANSAC/ICP "
                          f"1 thread, normals/SHOT {nthr} OpenMP threads as in the reference",
                "cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()}
@@ -258,9 +285,10 @@ def main():
         if n_all > nthr and not a.from_lasers:
             oracle_ref.set_threads(n_all)
             od2 = oracle_ref.Odometry(op)
+            cpu_frame(od2, 0)
             t1 = time.perf_counter()
-            for f in range(nf):
-                od2.process(frames[f].cpu().numpy())
+            for f in range(1, nf + 1):
+                cpu_frame(od2, f)
             ct2 = time.perf_counter() - t1
             cpu["all_cores"] = {"value": round(nf / ct2, 4), "cores": n_all}
 
@@ -295,7 +323,11 @@ def main():
                        (" + RCCL map bcast" if a.map_bcast else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "stage_ms_per_sweep": {k: round(v[0] / a.steps, 4) for k, v in stages.items()},
+            "stage_ms_per_sweep": {k: round(v[0] / a.steps, 4) for k, v in stages.items() if v[1]},
+            # main-thread host wall time per phase (mean over the timed sweeps; a prefetched sweep's
+            # extract/describe ran on the worker thread, so those phases are near zero here)
+            "host_ms_per_sweep": dict(zip(bshot_py.FrameStats.HOST_PHASES,
+                                          np.round(np.mean([list(s.host_ms) for s in stats], axis=0), 3).tolist())),
         }
         print(json.dumps(line))
     if dist is not None:

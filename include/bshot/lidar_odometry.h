@@ -41,6 +41,9 @@ class LidarOdometry {
     // the sweep after the prefetched one: grids, SR and ISS queued now (no worker), promoted by
     // the next prefetchFrameDevice() with the same pointer
     void queueFrameDevice(const float* d_xyz, int n);
+    // wait until the lookahead work in flight (worker, queue and top-K threads) has been issued and
+    // finished on the host; the prefetched results stay ready for adoption
+    void drainLookahead();
     void extractKeypoints();
     void computeDescriptors();
     void featureMatching();

@@ -200,6 +200,10 @@ int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next);
 int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2);
 /* odometry knobs: forwarded to bshot_set_option on the odometry's context */
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value);
+/* wait for the lookahead work started by the last process call (the prefetched sweep's describe on
+ * its worker thread, the queued sweep's launches and top-K) to be issued and finished; the results
+ * stay ready for the next process call. Extension (no reference counterpart). */
+int bshot_odom_drain(bshot_odom* o);
 int bshot_odom_get_keypoints(bshot_odom* o, float* xyz, int cap);
 int bshot_odom_get_ratios(bshot_odom* o, float* r, int cap);
 int bshot_odom_get_bits(bshot_odom* o, uint32_t* bits, int cap);

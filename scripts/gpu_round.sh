@@ -17,16 +17,31 @@ cat $O/smoke_$TAG.log &&
 echo "[gpu_round] $(date +%T) bench" &&
 timeout -k 10 600 python bench.py --profile-stages > $O/bench_$TAG.json 2> $O/bench_$TAG.err &&
 cat $O/bench_$TAG.json &&
+echo "[gpu_round] $(date +%T) bench, driver-sized (20 steps, 5 warm-up)" &&
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_$TAG.json 2> $O/bench_driver_$TAG.err &&
+cat $O/bench_driver_$TAG.json &&
 cd /tmp && export TMPDIR=/tmp &&
 echo "[gpu_round] $(date +%T) rocprofv3 kernel trace" &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o trace --output-format csv -- \
     python3 $R/bench.py --no-cpu-baseline > $O/prof_bench_$TAG.json 2> $O/prof_bench_$TAG.err &&
 echo "[gpu_round] $(date +%T) pmc FETCH_SIZE" &&
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o fetch --output-format csv -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_fetch_$TAG.log 2>&1 &&
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/pmc_fetch_$TAG.log 2>&1 &&
 echo "[gpu_round] $(date +%T) pmc WRITE_SIZE" &&
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$TAG -o write --output-format csv -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_write_$TAG.log 2>&1 &&
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/pmc_write_$TAG.log 2>&1 &&
+echo "[gpu_round] $(date +%T) pmc SQ pass 1" &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU \
+    -d $O/pmc_sq1_$TAG -o sq1 --output-format csv -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/pmc_sq1_$TAG.log 2>&1 &&
+echo "[gpu_round] $(date +%T) pmc SQ pass 2" &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR \
+    -d $O/pmc_sq2_$TAG -o sq2 --output-format csv -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/pmc_sq2_$TAG.log 2>&1 &&
+echo "[gpu_round] $(date +%T) pmc TCC/TCP/GRBM pass" &&
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE GRBM_COUNT \
+    -d $O/pmc_tcc_$TAG -o tcc --output-format csv -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/pmc_tcc_$TAG.log 2>&1 &&
 echo "[gpu_round] $(date +%T) preprocessor + capture kernels" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pre_$TAG -o t --output-format csv -- \
     python3 $R/b-shot-slam_amd/tools/pre_bench.py 30 > $O/pre_bench_$TAG.log 2>&1 &&
