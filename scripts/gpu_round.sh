@@ -20,6 +20,10 @@ cat $O/bench_$TAG.json &&
 echo "[gpu_round] $(date +%T) bench, driver-sized (20 steps, 5 warm-up)" &&
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_$TAG.json 2> $O/bench_driver_$TAG.err &&
 cat $O/bench_driver_$TAG.json &&
+echo "[gpu_round] $(date +%T) host timeline (no profiler)" &&
+BSHOT_HOST_TRACE=$O/host_$TAG.csv timeout -k 10 300 python bench.py --no-cpu-baseline --steps 100 --warmup 10 > $O/bench_host_$TAG.json 2>&1 &&
+python b-shot-slam_amd/tools/host_phases.py $O/host_$TAG.csv > $O/host_phases_$TAG.txt &&
+cat $O/host_phases_$TAG.txt &&
 cd /tmp && export TMPDIR=/tmp &&
 echo "[gpu_round] $(date +%T) rocprofv3 kernel trace" &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o trace --output-format csv -- \
