@@ -194,6 +194,8 @@ struct bshot_ctx {
     int opt_icp_tile = 1;  // 1: LDS-tiled NN over target spans (k_icp_tile); 0: wave per source point (k_icp_wave)
     DBuf<unsigned long long> ipart;  // k_icp_tile span minima
     DBuf<unsigned int> icnt;         // k_icp_tile per-block arrival counters
+    int opt_icp_grid = 1;  // 1: exact 1-NN on hashed grids of the targets (k_icp_grid); 0: brute-force passes
+    bsh::DevGrid icp_g1, icp_g2;  // ICP target grids (cells 1000 / 5000 mm), built once per ICP call
     int opt_icp_dev = 0;  // 1: ICP loop resident on the device (one sync); 0: host Umeyama per iteration (faster under load)
     DBuf<float> isrc, itgt3;
     DBuf<float4> itgt;

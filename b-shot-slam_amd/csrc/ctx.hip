@@ -722,7 +722,13 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
         const unsigned long long* best = c->p_best.p;
         const int splits = icp_tile_splits(ns, nt);
-        if (c->opt_icp_tile) {
+        const bool use_grid = c->opt_icp_grid != 0;
+        if (use_grid) {
+            // the targets are fixed for the whole ICP call: two hashed grids of them, built once
+            HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
+            HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true), "icp grid");
+            HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false), "icp grid 2");
+        } else if (c->opt_icp_tile) {
             HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
             HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
             HIPCHK(hipMemsetAsync(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
@@ -734,7 +740,11 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
             // one launch per iteration; the NN keys land in pinned host memory (no copy)
             const float* s_in = it == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
-            if (c->opt_icp_tile)
+            if (use_grid)
+                HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->icp_g1, c->icp_g2,
+                                       c->itgt.p, nt, c->p_best.p, c->stream),
+                       "icp iteration");
+            else if (c->opt_icp_tile)
                 HIPCHK(launch_icp_tile(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt,
                                        c->ipart.p, (int)std::min<size_t>(c->ipart.cap, 0x7FFFFFFF), c->icnt.p,
                                        c->p_best.p, c->stream),
@@ -835,6 +845,8 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 4\n");
     c->pf.release();
     c->pf2.release();
+    bsh::grid_free(c->icp_g1);
+    bsh::grid_free(c->icp_g2);
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
     c->seg.release(); c->segtmp.release(); c->rf.release(); c->shot.release(); c->ok.release(); c->bits.release();
     c->ma.release(); c->lbest.release(); c->left.release();
@@ -1099,6 +1111,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
+    else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;

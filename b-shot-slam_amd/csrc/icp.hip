@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bshot_math.h"
+#include "dev_cand.h"
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -217,6 +218,62 @@ __global__ void __launch_bounds__(256) k_icp_tile(const float* __restrict__ src_
         best_out[i] = r;
     }
     if (t == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One ICP iteration on hashed grids of the targets (built once per ICP call): a wave per source
+// point searches balls of growing radius (g1: r1, 2 r1; g2: r2, 2 r2). Every target with d2 < rs^2
+// is visited (for_candidates), so the smallest (d2 bits << 32 | index) key found inside the first
+// non-empty ball is the global one, ties included: a target outside the ball has d2 >= rs^2 > the
+// key's d2. A source with no target inside the largest ball (or non-finite) scans every target,
+// exactly as k_icp_tile. The step transform is applied with k_icp_tile's float expressions.
+#define ICPG_WAVES 4
+__global__ void __launch_bounds__(64 * ICPG_WAVES) k_icp_grid(const float* __restrict__ src_in, float* __restrict__ src_out,
+                                                              Xf16 T, int apply, int ns, GridView g1, GridView g2,
+                                                              float r1, float r2, const float4* __restrict__ tgt4, int nt,
+                                                              unsigned long long* __restrict__ best_out) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
+    __shared__ CandLds cl[ICPG_WAVES];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    CandLds* cs = &cl[wave];
+    cand_init(cs);
+    for (int i = blockIdx.x * ICPG_WAVES + wave; i < ns; i += gridDim.x * ICPG_WAVES) {
+        const float x = src_in[3 * i], y = src_in[3 * i + 1], z = src_in[3 * i + 2];
+        float qx = x, qy = y, qz = z;
+        if (apply) {
+            qx = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
+            qy = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
+            qz = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
+        }
+        if (lane == 0) { src_out[3 * i] = qx; src_out[3 * i + 1] = qy; src_out[3 * i + 2] = qz; }
+        unsigned long long m = ~0ull;
+        const bool fin = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
+        if (fin) {
+#pragma unroll 1
+            for (int step = 0; step < 4; ++step) {
+                const float rs = (step & 1) ? 2.f * ((step < 2) ? r1 : r2) : ((step < 2) ? r1 : r2);
+                const float rs2 = (float)((double)rs * (double)rs);
+                for_candidates((step < 2) ? g1 : g2, cs, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+                    if (v) {
+                        const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+                        m = key < m ? key : m;
+                    }
+                });
+                m = wave_min_u64(m);
+                if (m != ~0ull) break;
+            }
+        }
+        if (m == ~0ull) {
+            for (int j = lane; j < nt; j += 64) {
+                const float4 p = tgt4[j];
+                const float d2 = d2_flann(qx, qy, qz, p.x, p.y, p.z);
+                const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)j;
+                m = key < m ? key : m;
+            }
+            m = wave_min_u64(m);
+        }
+        if (lane == 0) best_out[i] = m;
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ---- device-resident ICP loop: the host enqueues max_iter (NN, update) pairs and syncs once.
@@ -460,6 +517,17 @@ hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16
     bsk::Xf16 T;
     for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
     bsk::k_icp_wave<<<(ns + 3) / 4, 256, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, best_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_icp_grid(const float* src_in, float* src_out, const float* T16, int apply, int ns, const DevGrid& g1,
+                           const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best_out, hipStream_t s) {
+    if (ns <= 0 || nt <= 0) return hipSuccess;
+    bsk::Xf16 T;
+    for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
+    const int blocks = (ns + ICPG_WAVES - 1) / ICPG_WAVES;
+    bsk::k_icp_grid<<<blocks, 64 * ICPG_WAVES, 0, s>>>(src_in, src_out, T, apply, ns, g1.view(), g2.view(), g1.cell,
+                                                        g2.cell, tgt4, nt, best_out);
     return hipGetLastError();
 }
 

@@ -51,6 +51,9 @@ int icp_tile_splits(int ns, int nt);
 hipError_t launch_icp_tile(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
                            int nt, unsigned long long* part, int part_cap, unsigned int* cnt,
                            unsigned long long* best_out, hipStream_t s);
+// exact 1-NN on two hashed grids of the targets (cells r1 < r2; k_icp_grid), brute force past them
+hipError_t launch_icp_grid(const float* src_in, float* src_out, const float* T16, int apply, int ns, const DevGrid& g1,
+                           const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best_out, hipStream_t s);
 hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
                            int nt, unsigned long long* best_out, hipStream_t s);
 hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,

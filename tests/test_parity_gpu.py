@@ -132,6 +132,40 @@ def test_icp_exact(ctx, cloud, sr_ref):
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
 
 
+@pytest.mark.parametrize("icp_grid", [1, 0])
+def test_icp_grid_edge_cases(icp_grid):
+    """A11 1-NN on the target grids (k_icp_grid) vs the oracle's brute force: sources far beyond
+    every ball (brute-force fallback), exact-duplicate targets (index tie), targets exactly on a
+    ball radius (d2 == rs^2 is outside the ball), a non-finite source, sparse and dense targets."""
+    rng = np.random.default_rng(11)
+    tgt = (rng.random((5000, 3)) * [80000, 80000, 4000] - [40000, 40000, 2000]).astype(np.float32)
+    tgt[100:110] = tgt[90]  # duplicates
+    tgt[200] = [0, 0, 0]
+    tgt[201] = [1000, 0, 0]
+    src = np.concatenate([tgt[:1500] + rng.normal(0, 300, (1500, 3)), tgt[1500:1600] + 7000.0,
+                          [[0, 0, 0], [1000, 0, 0], [500, 0, 0], [2e6, 2e6, 0], [-9e5, 0, 3e5]],
+                          tgt[90:91] + 1.0]).astype(np.float32)
+    c = bshot_py.Context(0)
+    try:
+        c.set_option("icp_grid", icp_grid)
+        for s2 in (src, src[:64]):
+            T, it = c.icp(s2, tgt)
+            Tr, itr = orc.icp(s2, tgt)
+            assert it == itr
+            np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+        bad = src.copy()
+        bad[5] = np.nan
+        T, it = c.icp(bad, tgt)
+        Tr, itr = orc.icp(bad, tgt)
+        assert it == itr
+        # a NaN source spreads NaN through the host Umeyama: same NaN pattern (payloads may differ)
+        assert np.array_equal(np.isnan(T), np.isnan(Tr))
+        ok = ~np.isnan(T)
+        np.testing.assert_array_equal(T[ok].view(np.uint32), Tr[ok].view(np.uint32))
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("seed,frac", [(1, 0.6), (2, 0.3), (3, 0.9), (4, 0.05), (6, 0.15)])
 def test_ransac_dev_matches_host(ctx, seed, frac):
     """A10 with the hypotheses scored on the GPU (bshot_ransac_dev) == host RANSAC == oracle, bit for bit."""
