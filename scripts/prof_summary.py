@@ -24,7 +24,9 @@ def short(name):
 N_CU, N_SIMD = 256, 1024
 DERIVED_DOC = {
     "time": "median launch duration of the kernel in the same round's kernel trace (prof_<tag>)",
-    "clock_ghz": "GRBM_GUI_ACTIVE / duration (GPU-busy cycles of the dispatch)",
+    "cycles": "GRBM_GUI_ACTIVE / 8: rocprofv3 sums the counter over the 8 XCDs (GRBM / 8 / the PMC run's own "
+              "dispatch duration = 2.4 GHz, checked on k_seg_ratio r02c)",
+    "clock_ghz": "cycles / the PMC run's mean dispatch duration (Start/End timestamps of the counter CSV)",
     "valu_issue_frac": "SQ_INSTS_VALU x 2 cycles (wave64 fp32 issue on a 32-lane SIMD, MI355X_MICROARCH.md "
                        "per-instruction table) / (cycles x 1024 SIMDs): VALU issue share of the chip",
     "lds_busy_frac": "SQ_LDS_IDX_ACTIVE / (cycles x 256 CUs): LDS-array busy share",
@@ -39,14 +41,15 @@ DERIVED_DOC = {
 }
 
 
-def derive(e, c, dur):
+def derive(e, c, dur, pmc_dur=None):
     g = lambda n: c.get(n)
     if dur:
         e["time_ms"] = round(dur * 1e3, 4)
     cyc = None
-    if dur and g("GRBM_GUI_ACTIVE"):
-        cyc = g("GRBM_GUI_ACTIVE")
-        e["clock_ghz"] = round(cyc / dur / 1e9, 3)
+    if g("GRBM_GUI_ACTIVE"):
+        cyc = g("GRBM_GUI_ACTIVE") / 8.0
+        if pmc_dur:
+            e["clock_ghz"] = round(cyc / pmc_dur / 1e9, 3)
     if cyc is None and dur:
         cyc = dur * 2.4e9
     if cyc:
@@ -92,12 +95,15 @@ def main(tag):
             e["hbm_read_bytes" if sub == "fetch" else "hbm_write_bytes"] = sum(v) / len(v) * scale
     # SQ / TCC / TCP / GRBM passes (scripts/gpu_round.sh): per-dispatch means, then derived metrics
     raw = collections.defaultdict(lambda: collections.defaultdict(list))
+    pdur = collections.defaultdict(list)
     for sub in ("sq1", "sq2", "tcc"):
         f = os.path.join(src, f"pmc_{sub}_{tag}", f"{sub}_counter_collection.csv")
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
             raw[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if sub == "tcc" and r["Counter_Name"] == "GRBM_GUI_ACTIVE" and "End_Timestamp" in r:
+                pdur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     med = {}
     tr = os.path.join(src, f"prof_{tag}", "trace_kernel_trace.csv")
     if os.path.exists(tr):
@@ -109,7 +115,8 @@ def main(tag):
         e = out["kernels"].setdefault(k, {})
         c = {n: sum(v) / len(v) for n, v in ctrs.items()}
         e["counters"] = {n: round(v, 1) for n, v in c.items()}
-        derive(e, c, med.get(k))
+        pd = pdur.get(k)
+        derive(e, c, med.get(k), sum(pd) / len(pd) if pd else None)
     out["derived"] = DERIVED_DOC
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
     # per-kernel median launch duration from the same kernel trace (the rocprofv3 mean is skewed by
