@@ -20,7 +20,9 @@ struct DBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t c = n + n / 4 + 64;
+        // doubling with a 64 Ki-element floor: a sequence's sizes (targets M, neighbourhood totals)
+        // grow for many sweeps, and every regrowth is a free + malloc that stalls the device
+        size_t c = n * 2 > (size_t)65536 ? n * 2 : (size_t)65536;
         hipError_t e = hipMalloc(&p, sizeof(T) * c);
         if (e == hipSuccess) cap = c;
         return e;
@@ -42,7 +44,9 @@ struct PinBuf {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        size_t c = n + n / 4 + 64;
+        // doubling with a 64 Ki-element floor: a sequence's sizes (targets M, neighbourhood totals)
+        // grow for many sweeps, and every regrowth is a free + malloc that stalls the device
+        size_t c = n * 2 > (size_t)65536 ? n * 2 : (size_t)65536;
         hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * c, hipHostMallocDefault);
         if (e == hipSuccess) cap = c;
         return e;

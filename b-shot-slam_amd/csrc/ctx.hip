@@ -455,7 +455,9 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
         // bases, LPT order) is computed on the device against capacities sized from the largest
         // neighbourhood total seen so far (+25%); an overflow (errw bit 16) makes the caller
         // re-run this describe with the host-side plan
-        const long long seg_cap = c->seg_hint + c->seg_hint / 4 + 65536;
+        // +50%: a sequence's neighbourhood totals drift by tens of percent, and an overflow costs a
+        // second describe (re-planned on the host)
+        const long long seg_cap = c->seg_hint + c->seg_hint / 2 + 262144;
         const int chunk_cap = (int)(seg_cap / 64) + k + 1;
         HIPCHK(c->seg.ensure((size_t)seg_cap), "alloc seg");
         HIPCHK(c->segtmp.ensure((size_t)seg_cap), "alloc segtmp");
@@ -596,6 +598,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
 
 bool ctx_describe_replan(bshot_ctx* c, const int* err) {
     if (!(err[0] & 16)) return false;
+    c->work[1]++;  // re-planned describes (bshot_work_counters)
     long long total = 0;
     std::memcpy(&total, err + 2, sizeof(total));
     if (total > c->seg_hint) c->seg_hint = total;
@@ -726,8 +729,9 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         if (use_grid) {
             // the targets are fixed for the whole ICP call: two hashed grids of them, built once
             HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
-            HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true), "icp grid");
-            HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false), "icp grid 2");
+            const int mc = std::max(65536, 2 * nt);
+            HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true, mc), "icp grid");
+            HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false, mc), "icp grid 2");
         } else if (c->opt_icp_tile) {
             HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
             HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");

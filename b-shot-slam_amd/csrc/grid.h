@@ -32,9 +32,11 @@ struct DevGrid {
 
 // Builds the grid of d_xyz (N x 3 floats, device) with edge `cell`; writes float4 copies of the
 // points in index order to d_pts4 (N entries).
-// write_pts4 = false: d_pts4 already holds the cloud (another grid built it) and is only read
+// write_pts4 = false: d_pts4 already holds the cloud (another grid built it) and is only read.
+// min_cap: capacity floor when the buffers (re)grow -- for clouds whose size keeps growing (the ICP
+// targets), so that regrowth, a device-wide stall (hipFree), is rare
 hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s,
-                      bool write_pts4 = true);
+                      bool write_pts4 = true, int min_cap = 0);
 void grid_free(DevGrid& g);
 // four nested grids (cells c0, 2c0, 4c0, 8c0) from one sort; g[1..3].spts alias g[0].spts
 hipError_t grid_build_ladder(DevGrid* const* g, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s);

@@ -5,6 +5,8 @@
 //
 // Build: keys -> rocprim radix sort of (cell key, idx) -> cell-start detection (binary search for
 // the run end) + hash insert -> scatter float4 points into cell order. All O(N), no host sync.
+#include <algorithm>
+
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -193,11 +195,11 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
 }
 
 hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s,
-                      bool write_pts4) {
+                      bool write_pts4, int min_cap) {
     hipError_t e;
     if (n > g.cap || g.alias || !g.keys) {
         grid_free(g);
-        g.cap = n + n / 4 + 1024;
+        g.cap = std::max(n + n / 4 + 1024, min_cap);
         if ((e = hipMalloc(&g.keys, sizeof(unsigned long long) * g.cap))) return e;
         if ((e = hipMalloc(&g.keys2, sizeof(unsigned long long) * g.cap))) return e;
         if ((e = hipMalloc(&g.vals, sizeof(unsigned int) * g.cap))) return e;

@@ -293,6 +293,12 @@ def main():
             cpu["all_cores"] = {"value": round(nf / ct2, 4), "cores": n_all}
 
     if rank == 0:
+        if os.environ.get("BENCH_INTERVALS"):
+            iv = np.diff([t0] + marks) * 1e3
+            import ctypes
+            wc = (ctypes.c_int64 * 8)()
+            bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 8)
+            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": list(wc)}), file=sys.stderr)
         if a.profile_stages:
             print(json.dumps({k: [round(v[0], 3), v[1]] for k, v in stages.items()}), file=sys.stderr)
             hm = np.mean([list(s.host_ms) for s in stats], axis=0)

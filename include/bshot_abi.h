@@ -260,7 +260,8 @@ enum {
 int bshot_stage_times(bshot_ctx* c, double* ms, int64_t* launches, int n);
 void bshot_stage_reset(bshot_ctx* c);
 void bshot_set_timing(bshot_ctx* c, int enabled);
-/* algorithmic work counters of the last describe/SR calls (pair counts), see DESIGN.md §roofline */
+/* work counters: [0] neighbourhood total of the last describe (SHOT pairs), [1] describes re-run with a
+ * host plan after the device plan ran out of capacity (cumulative) */
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
 /* instrumentation (outside timed regions): sum over all points of the current cloud of
  * |B(p, R)| (strict d2 < R^2, self included) -> the P_sr / P_iss work figures of SURVEY.md §8(d). */

@@ -1,17 +1,14 @@
 #!/bin/bash
-# Fast iteration on the GPU box: stage parity + golden fixtures, then a bench line with stage ms.
-# usage: bash scripts/gpu_quick.sh [tag] [extra pytest selection]
+# quick GPU check: selected tests (-k expression) then a bench line at the default and driver sizes
+# usage (via gpurun): bash scripts/gpu_quick.sh "<pytest -k expr>" [tag] [extra bench args]
 set -u
-TAG=${1:-q}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -m pytest tests/test_parity_gpu.py tests/test_golden.py -m gpu -x -q > $O/quick_pytest_$TAG.log 2>&1
-rc=$?
-tail -5 $O/quick_pytest_$TAG.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --no-cpu-baseline --profile-stages > $O/quick_bench_$TAG.json 2> $O/quick_bench_$TAG.err
-rc=$?
-cat $O/quick_bench_$TAG.json; tail -2 $O/quick_bench_$TAG.err
-exit $rc
+K=${1:-icp}
+TAG=${2:-quick}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > $O/pytest_$TAG.log 2>&1
+rc=$?; tail -3 $O/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline ${@:3} > $O/bench_$TAG.json 2> $O/bench_$TAG.err && cat $O/bench_$TAG.json &&
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 ${@:3} > $O/bench_driver_$TAG.json 2>> $O/bench_$TAG.err && cat $O/bench_driver_$TAG.json
