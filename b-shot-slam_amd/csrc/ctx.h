@@ -103,6 +103,7 @@ struct CloudState {
 };
 
 namespace bsh {
+struct GMap;       // csrc/gmap.hip
 struct PreState;   // csrc/preprocess.hip
 struct VeloState;  // csrc/velodyne.hip
 }
@@ -173,6 +174,12 @@ struct bshot_ctx {
     bool plan_on_host = false;  // next describe: plan on the host (after a device-plan overflow)
     long long seg_hint = 0;     // largest neighbourhood total seen (device-plan capacities)
     int ladder_mode(const CloudState& s) const { return s.fine_ladder ? (opt_ladder_front ? 2 : 1) : 0; }
+
+    // GPU keypoint map (csrc/gmap.hip): mode 0 host Map, 1 GPU map in the reference's libstdc++
+    // block order (default), 2 GPU map in insertion order (canonical; not the reference's order)
+    int opt_gpu_map = 1;
+    bsh::GMap* gmap = nullptr;
+    DBuf<float> gtgt;  // matching targets assembled on the device (float3)
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag
     DBuf<unsigned int> ma;
@@ -277,5 +284,7 @@ int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h
 // device gather of cloud points -> host (pinned staging), synchronous
 int ctx_gather_host(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst, float* out);
 int ctx_gather_kps_async(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k);
-int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters);
+// d_tgt (nullable): the same targets already on the device (gmap), copied D2D instead of uploaded
+int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
+            const float* d_tgt = nullptr);
 }  // namespace bsh

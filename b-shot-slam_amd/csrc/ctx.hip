@@ -16,6 +16,7 @@
 
 #include "../host/geom.h"
 #include "ctx.h"
+#include "gmap.h"
 #include "kernels.h"
 #include "preprocess.h"
 #include "velodyne.h"
@@ -668,7 +669,8 @@ int ctx_sync_main(bshot_ctx* c) {
     return BSHOT_OK;
 }
 
-int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters) {
+int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
+            const float* d_tgt) {
     bg::Mat4f fin = bg::Mat4f::identity();
     int it = 0;
     if (ns >= 3 && nt > 0) {
@@ -678,11 +680,20 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         HIPCHK(c->itgt3.ensure(3 * ((size_t)nt + ns)), "alloc icp staging");
         HIPCHK(c->p_tgt.ensure(3 * ((size_t)nt + ns)), "alloc pinned tgt");
         HIPCHK(c->p_best.ensure(ns), "alloc pinned best");
-        std::memcpy(c->p_tgt.p, tgt, sizeof(float) * 3 * nt);
-        std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
-        HIPCHK(hipMemcpyAsync(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * ((size_t)nt + ns), hipMemcpyHostToDevice,
-                              c->stream),
-               "H2D icp points");
+        if (d_tgt) {
+            std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
+            HIPCHK(hipMemcpyAsync(c->itgt3.p, d_tgt, sizeof(float) * 3 * (size_t)nt, hipMemcpyDeviceToDevice, c->stream),
+                   "icp targets");
+            HIPCHK(hipMemcpyAsync(c->itgt3.p + 3 * (size_t)nt, c->p_tgt.p + 3 * (size_t)nt, sizeof(float) * 3 * ns,
+                                  hipMemcpyHostToDevice, c->stream),
+                   "H2D icp source");
+        } else {
+            std::memcpy(c->p_tgt.p, tgt, sizeof(float) * 3 * nt);
+            std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
+            HIPCHK(hipMemcpyAsync(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * ((size_t)nt + ns), hipMemcpyHostToDevice,
+                                  c->stream),
+                   "H2D icp points");
+        }
         const float* d_src0 = c->itgt3.p + 3 * (size_t)nt;
         if (c->opt_icp_dev) {
             HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
@@ -849,6 +860,8 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 4\n");
     c->pf.release();
     c->pf2.release();
+    bsh::gmap_free(c);
+    c->gtgt.release();
     bsh::grid_free(c->icp_g1);
     bsh::grid_free(c->icp_g2);
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
@@ -1116,6 +1129,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
     else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
+    else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;

@@ -1,0 +1,628 @@
+// gmap.hip -- the keypoint map on the GPU: Map::addKeypoint with the 800 mm
+// suppression (src/mymap.cpp:4-26), Keypoint::createKeypoint's 10 mm grid (src/keypoint.cpp:23-32),
+// getBlockID (src/mymap.cpp:95-105), and Map::getKeypoints' 21^3 block loop (src/mymap.cpp:28-74)
+// with the ref keypoints appended (src/lidar_odometry.cpp:195-207) -- the matching targets are
+// assembled in HBM, where the Hamming matcher and ICP read them.
+//
+// Order. A block's entries come out in the iteration order of the reference's
+// std::unordered_map<Vector3f, Keypoint::Ptr, MapHasher> (include/mymap.h:11-25), restated by
+// umap_order.h (checked against libstdc++ itself); that order decides first-index ties in the
+// Hamming match, so this mode is bit-exact with the host map. Mode 2 ("canonical") emits a block's
+// entries in insertion order instead (not the reference's order; the oracle has the same mode).
+//
+// Layout (device, grow-only):
+//   slots      kpos[s] = (x, y, z, ratio) on the 10 mm grid, kdesc[s] = 11 words; every keypoint a
+//              sweep offers gets a slot (slot_base + i), rejected ones are never referenced
+//   blocks     open-addressed table block id -> block index; GBlock headers
+//   members    per block, in insertion order: mslot (current slot of the key: a replaced value
+//              points at the newer slot), hash code; plus ord[n] (iteration order), pos (inverse)
+//              and the bucket array of the restated libstdc++ table -- all in two bump pools
+// Insert: one wave per block touched by the sweep, its keypoints in sweep order (the reference's
+// loop order); the block's arrays are staged in LDS, the suppression scan and the list shifts are
+// wave-parallel, the libstdc++ bookkeeping runs on lane 0.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+#include "dev_common.h"
+#include "gmap.h"
+#include "umap_order.h"
+
+namespace bsk {
+
+using bsh::GBlock;
+using bsh::GM_CTOP;
+using bsh::GM_ERR;
+using bsh::GM_ITOP;
+using bsh::GM_LDS_BK;
+using bsh::GM_LDS_N;
+using bsh::GM_MEMBERS;
+using bsh::GM_NBLOCKS;
+using bsh::GM_NSEG;
+
+struct GMapDev {
+    float4* kpos;
+    unsigned int* kdesc;
+    unsigned long long* tkey;
+    int* tval;
+    unsigned int tmask;
+    GBlock* blk;
+    int blk_cap;
+    int* ctr;  // GM_* counters
+    int* ipool;
+    long long ipool_cap;
+    unsigned long long* cpool;
+    long long cpool_cap;
+};
+
+__device__ __forceinline__ unsigned long long block_id_of(float gx, float gy, float gz) {
+    // Map::getBlockID: low 21 bits of each coordinate of the 10 m grid position
+    const int prec = 10000;
+    const int bx = (int)(float)((int)roundf(gx / (float)prec) * prec);
+    const int by = (int)(float)((int)roundf(gy / (float)prec) * prec);
+    const int bz = (int)(float)((int)roundf(gz / (float)prec) * prec);
+    const unsigned long long i = ((unsigned long long)(long long)bx << 42) & (0x1FFFFFull << 42);
+    const unsigned long long j = ((unsigned long long)(long long)by << 21) & (0x1FFFFFull << 21);
+    const unsigned long long k = ((unsigned long long)(long long)bz) & 0x1FFFFFull;
+    return i | j | k;
+}
+
+__device__ __forceinline__ unsigned long long map_hash(float x, float y, float z) {
+    // MapHasher: abs(round(p.sum())) on the float sum, Eigen's redux order x + (y + z)
+    return (unsigned long long)fabsf(roundf(x + (y + z)));
+}
+
+__device__ __forceinline__ int find_block(const GMapDev& m, unsigned long long id) {
+    unsigned int h = hash_key(id) & m.tmask;
+    for (unsigned int probe = 0; probe <= m.tmask; ++probe) {
+        const unsigned long long k = m.tkey[h];
+        if (k == id) return m.tval[h];
+        if (k == BS_EMPTY_KEY) return -1;
+        h = (h + 1) & m.tmask;
+    }
+    return -1;
+}
+
+// the sweep's keypoints -> world position on the 10 mm grid (updateMap: R * p + T, then
+// createKeypoint), their slots, block ids (sort keys) and hash codes
+__global__ void k_gmap_prep(const float* __restrict__ kps, const float* __restrict__ ratio,
+                            const unsigned int* __restrict__ bits, int k, Xf16g T, int slot_base, GMapDev m,
+                            unsigned long long* __restrict__ keys, unsigned int* __restrict__ vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const float x = kps[3 * i], y = kps[3 * i + 1], z = kps[3 * i + 2];
+    // Matrix3f * Vector3f (Eigen 3.2 coefficient order) + T
+    const float wx = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
+    const float wy = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
+    const float wz = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
+    const float gx = (float)((int)truncf(wx / 10.f) * 10);
+    const float gy = (float)((int)truncf(wy / 10.f) * 10);
+    const float gz = (float)((int)truncf(wz / 10.f) * 10);
+    const int s = slot_base + i;
+    m.kpos[s] = make_float4(gx, gy, gz, ratio[i]);
+#pragma unroll
+    for (int w = 0; w < 11; ++w) m.kdesc[11 * (size_t)s + w] = bits[11 * (size_t)i + w];
+    keys[i] = block_id_of(gx, gy, gz);
+    vals[i] = (unsigned int)i;
+}
+
+// one thread per run of equal block ids in the sorted keys: find or create the block, record the run
+__global__ void k_gmap_segments(const unsigned long long* __restrict__ keys, int k, GMapDev m, int* __restrict__ seg) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    const unsigned long long id = keys[j];
+    if (j > 0 && keys[j - 1] == id) return;
+    int lo = j + 1, hi = k;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] == id) lo = mid + 1;
+        else hi = mid;
+    }
+    int b = find_block(m, id);
+    if (b < 0) {
+        b = atomicAdd(&m.ctr[GM_NBLOCKS], 1);
+        if (b >= m.blk_cap) {
+            atomicOr(&m.ctr[GM_ERR], 1);
+            return;
+        }
+        GBlock B;
+        B.id = id;
+        B.n = 0; B.bkt = 1; B.next_resize = 0; B.cap = 0;  // um::initial(): one bucket, nothing allocated
+        B.mslot = B.ord = B.pos = B.code = -1;
+        B.bk = -1; B.bk_cap = 0;
+        m.blk[b] = B;
+        unsigned int h = hash_key(id) & m.tmask;
+        while (atomicCAS(&m.tkey[h], BS_EMPTY_KEY, id) != BS_EMPTY_KEY) h = (h + 1) & m.tmask;
+        m.tval[h] = b;
+    }
+    const int s = atomicAdd(&m.ctr[GM_NSEG], 1);
+    seg[3 * s] = j;
+    seg[3 * s + 1] = lo - j;
+    seg[3 * s + 2] = b;
+}
+
+// bump allocation from a pool (lane 0); false when the pool is exhausted (error bit 2)
+__device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long long need, int* err, long long* off) {
+    const long long o = (long long)atomicAdd(ctr_top, (int)need);
+    if (o + need > cap) {
+        atomicOr(err, 2);
+        return false;
+    }
+    *off = o;
+    return true;
+}
+
+// one wave per touched block (grid-strides over the device-side segment count)
+__global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
+                                                    const int* __restrict__ seg, int slot_base) {
+    // 116 KiB of static LDS (one workgroup per CU; the sweep touches ~100 blocks)
+    __shared__ int s_ord[GM_LDS_N], s_pos[GM_LDS_N], s_slot[GM_LDS_N], s_nxt[GM_LDS_N], s_bk[GM_LDS_BK];
+    __shared__ uint64_t s_code[GM_LDS_N];
+    const int lane = lane_id();
+    const int nseg = m.ctr[GM_NSEG];
+    for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const int j0 = seg[3 * sg], cnt = seg[3 * sg + 1], b = seg[3 * sg + 2];
+        GBlock B = m.blk[b];
+        if (B.n + cnt > GM_LDS_N) {
+            if (lane == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
+            continue;
+        }
+        // stage the block's arrays
+        for (int i = lane; i < B.n; i += 64) {
+            s_ord[i] = m.ipool[B.ord + i];
+            s_pos[i] = m.ipool[B.pos + i];
+            s_slot[i] = m.ipool[B.mslot + i];
+            s_code[i] = m.cpool[B.code + i];
+        }
+        if (B.bk >= 0)
+            for (int i = lane; i < B.bkt; i += 64) s_bk[i] = m.ipool[B.bk + i];
+        __syncthreads();
+        um::State S{B.n, B.bkt, B.next_resize};
+        int added = 0;
+        for (int t = 0; t < cnt; ++t) {
+            const int slot = slot_base + (int)vals[j0 + t];
+            const float4 p = m.kpos[slot];
+            // src/mymap.cpp:14-22: rejected when a keypoint of the block within 800 mm has a
+            // segmentation ratio >= this one's; an exact key hit is the entry operator[] replaces
+            bool rej = false;
+            int hit = -1;
+            for (int i = lane; i < S.n; i += 64) {
+                const float4 e = m.kpos[s_slot[i]];
+                const float dx = p.x - e.x, dy = p.y - e.y, dz = p.z - e.z;
+                if (sqrtf(dx * dx + (dy * dy + dz * dz)) < 800.f && p.w <= e.w) rej = true;
+                if (e.x == p.x && e.y == p.y && e.z == p.z) hit = i;
+            }
+            if (__ballot(rej)) continue;
+            const unsigned long long hm = __ballot(hit >= 0);
+            if (hm) {
+                const int owner = (int)__ffsll((long long)hm) - 1;
+                const int mi = __shfl(hit, owner, 64);
+                if (lane == 0) s_slot[mi] = slot;
+                __syncthreads();
+                continue;
+            }
+            const int x = S.n;
+            int at = 0;
+            if (lane == 0) {
+                s_slot[x] = slot;
+                s_code[x] = map_hash(p.x, p.y, p.z);
+                int nb;
+                if (um::need_rehash(S, &nb)) um::rehash(S, nb, s_ord, s_pos, s_code, s_bk, s_nxt);
+                at = um::insert_position(S, x, s_ord, s_pos, s_code, s_bk);
+            }
+            at = __shfl(at, 0, 64);
+            S.bkt = __shfl(S.bkt, 0, 64);
+            S.next_resize = __shfl(S.next_resize, 0, 64);
+            __syncthreads();
+            // shift ord[at, n) one place up, top chunk first (reads of a chunk never overlap the
+            // writes of the chunks before it)
+            for (int hi = S.n; hi > at; hi -= 64) {
+                const int i = hi - lane;
+                int v = 0;
+                if (i > at) v = s_ord[i - 1];
+                __syncthreads();
+                if (i > at) { s_ord[i] = v; s_pos[v] = i; }
+                __syncthreads();
+            }
+            if (lane == 0) { s_ord[at] = x; s_pos[x] = at; }
+            __syncthreads();
+            S.n += 1;
+            ++added;
+        }
+        // write the block back (arrays regrow by doubling)
+        long long off = 0;
+        bool ok = true;
+        if (lane == 0) {
+            if (S.n > B.cap) {
+                const int nc = std::max(16, std::max(S.n, 2 * B.cap));
+                long long io = 0, co = 0;
+                ok = pool_alloc(&m.ctr[GM_ITOP], m.ipool_cap, 3LL * nc, &m.ctr[GM_ERR], &io) &&
+                     pool_alloc(&m.ctr[GM_CTOP], m.cpool_cap, nc, &m.ctr[GM_ERR], &co);
+                if (ok) {
+                    B.cap = nc;
+                    B.ord = (int)io; B.pos = (int)(io + nc); B.mslot = (int)(io + 2 * nc);
+                    B.code = (int)co;
+                }
+            }
+            if (ok && S.bkt > B.bk_cap) {
+                ok = pool_alloc(&m.ctr[GM_ITOP], m.ipool_cap, S.bkt, &m.ctr[GM_ERR], &off);
+                if (ok) { B.bk = (int)off; B.bk_cap = S.bkt; }
+            }
+        }
+        ok = __shfl((int)ok, 0, 64) != 0;
+        B.cap = __shfl(B.cap, 0, 64);
+        B.ord = __shfl(B.ord, 0, 64); B.pos = __shfl(B.pos, 0, 64); B.mslot = __shfl(B.mslot, 0, 64);
+        B.code = __shfl(B.code, 0, 64); B.bk = __shfl(B.bk, 0, 64); B.bk_cap = __shfl(B.bk_cap, 0, 64);
+        if (!ok) continue;
+        for (int i = lane; i < S.n; i += 64) {
+            m.ipool[B.ord + i] = s_ord[i];
+            m.ipool[B.pos + i] = s_pos[i];
+            m.ipool[B.mslot + i] = s_slot[i];
+            m.cpool[B.code + i] = s_code[i];
+        }
+        for (int i = lane; i < S.bkt; i += 64) m.ipool[B.bk + i] = s_bk[i];
+        if (lane == 0) {
+            B.n = S.n; B.bkt = S.bkt; B.next_resize = S.next_resize;
+            m.blk[b] = B;
+            if (added) atomicAdd(&m.ctr[GM_MEMBERS], added);
+        }
+        __syncthreads();
+    }
+}
+
+// Map::getKeypoints: one thread per position of the x/y/z loop -> its block's entry count
+__global__ void k_gmap_qcount(GMapDev m, int x0, int y0, int z0, int ny, int nz, int npos, int* __restrict__ cnt,
+                              int* __restrict__ bidx) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= npos) return;
+    const int iz = t % nz, r = t / nz, iy = r % ny, ix = r / ny;
+    const int prec = 10000;
+    const int x = x0 + ix * prec, y = y0 + iy * prec, z = z0 + iz * prec;
+    const int b = find_block(m, block_id_of((float)x, (float)y, (float)z));
+    bidx[t] = b;
+    cnt[t] = b >= 0 ? m.blk[b].n : 0;
+}
+
+// exclusive scan of cnt[0, npos) in one workgroup of 1024 threads; total -> *tot
+__global__ void __launch_bounds__(1024) k_gmap_scan(const int* __restrict__ cnt, int npos, int* __restrict__ off,
+                                                    int* __restrict__ tot) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int per = (npos + 1023) / 1024;
+    const int a = t * per, e = min(npos, a + per);
+    int s = 0;
+    for (int i = a; i < e; ++i) s += cnt[i];
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = t > 0 ? part[t - 1] : 0;
+    for (int i = a; i < e; ++i) { off[i] = run; run += cnt[i]; }
+    if (t == 1023) *tot = part[1023];
+}
+
+// one wave per loop position: the block's entries in iteration order (mode 1) or insertion order
+// (mode 2) -> target positions (float3) and descriptors (11 words at dst_desc)
+__global__ void __launch_bounds__(256) k_gmap_qfill(GMapDev m, const int* __restrict__ cnt, const int* __restrict__ bidx,
+                                                    const int* __restrict__ off, int npos, int canonical,
+                                                    float* __restrict__ dst_pos, unsigned int* __restrict__ dst_desc) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = lane_id();
+    const int nw = (gridDim.x * blockDim.x) >> 6;
+    for (int t = wave; t < npos; t += nw) {
+        const int n = cnt[t];
+        if (n == 0) continue;
+        const GBlock B = m.blk[bidx[t]];
+        const int o = off[t];
+        for (int r = lane; r < n; r += 64) {
+            const int mi = canonical ? r : m.ipool[B.ord + r];
+            const int s = m.ipool[B.mslot + mi];
+            const float4 p = m.kpos[s];
+            dst_pos[3 * (size_t)(o + r)] = p.x;
+            dst_pos[3 * (size_t)(o + r) + 1] = p.y;
+            dst_pos[3 * (size_t)(o + r) + 2] = p.z;
+#pragma unroll
+            for (int w = 0; w < 11; ++w) dst_desc[11 * (size_t)(o + r) + w] = m.kdesc[11 * (size_t)s + w];
+        }
+    }
+}
+
+// the ref keypoints after the map's: transformPointCloud with the ref pose (src/lidar_odometry.cpp:202)
+__global__ void k_gmap_ref(const float* __restrict__ kps, const unsigned int* __restrict__ bits, int k, Xf16g T,
+                           float* __restrict__ dst_pos, unsigned int* __restrict__ dst_desc) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const float x = kps[3 * i], y = kps[3 * i + 1], z = kps[3 * i + 2];
+    dst_pos[3 * i] = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
+    dst_pos[3 * i + 1] = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
+    dst_pos[3 * i + 2] = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
+#pragma unroll
+    for (int w = 0; w < 11; ++w) dst_desc[11 * (size_t)i + w] = bits[11 * (size_t)i + w];
+}
+
+}  // namespace bsk
+
+namespace bsh {
+
+#define HIPCHK(call, what)                              \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return c->fail(what, e_); \
+    } while (0)
+
+static bsk::GMapDev dev_view(GMap& g) {
+    bsk::GMapDev v;
+    v.kpos = g.kpos.p;
+    v.kdesc = g.kdesc.p;
+    v.tkey = g.tkey.p;
+    v.tval = g.tval.p;
+    v.tmask = g.tsize - 1;
+    v.blk = g.blk.p;
+    v.blk_cap = (int)g.blk_cap;
+    v.ctr = g.ctr.p;
+    v.ipool = g.ipool.p;
+    v.ipool_cap = (long long)g.ipool_cap;
+    v.cpool = g.cpool.p;
+    v.cpool_cap = (long long)g.cpool_cap;
+    return v;
+}
+
+static bsk::Xf16g xf(const float* T16) {
+    bsk::Xf16g T;
+    for (int i = 0; i < 16; ++i) T.m[i] = T16[i];
+    return T;
+}
+
+// device copy (keeps contents) when a buffer must grow; the map's pools and tables carry state
+template <typename T>
+static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s) {
+    if (need <= b.cap) return hipSuccess;
+    size_t c = std::max(need, 2 * b.cap);
+    T* p = nullptr;
+    hipError_t e = hipMalloc(&p, sizeof(T) * c);
+    if (e != hipSuccess) return e;
+    if (used) {
+        e = hipMemcpyAsync(p, b.p, sizeof(T) * used, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+    }
+    if (b.p) (void)hipFree(b.p);
+    b.p = p;
+    b.cap = c;
+    return hipSuccess;
+}
+
+static int gmap_init(bshot_ctx* c) {
+    GMap& g = *c->gmap;
+    if (g.ready) return BSHOT_OK;
+    g.tsize = 1u << 16;
+    HIPCHK(g.tkey.ensure(g.tsize), "gmap table");
+    HIPCHK(g.tval.ensure(g.tsize), "gmap table");
+    HIPCHK(hipMemsetAsync(g.tkey.p, 0xFF, sizeof(unsigned long long) * g.tsize, c->stream), "gmap table clear");
+    g.blk_cap = 1 << 14;
+    HIPCHK(g.blk.ensure(g.blk_cap), "gmap blocks");
+    g.ipool_cap = (size_t)1 << 24;
+    g.cpool_cap = (size_t)1 << 22;
+    HIPCHK(g.ipool.ensure(g.ipool_cap), "gmap pool");
+    HIPCHK(g.cpool.ensure(g.cpool_cap), "gmap pool");
+    g.ipool_cap = g.ipool.cap;
+    g.cpool_cap = g.cpool.cap;
+    HIPCHK(g.ctr.ensure(GM_NCTR), "gmap counters");
+    HIPCHK(hipMemsetAsync(g.ctr.p, 0, sizeof(int) * GM_NCTR, c->stream), "gmap counters");
+    HIPCHK(g.p_ctr.ensure(GM_NCTR), "gmap pinned counters");
+    std::memset(g.p_ctr.p, 0, sizeof(int) * GM_NCTR);
+    g.slots = 0;
+    g.ready = true;
+    return BSHOT_OK;
+}
+
+// room for one more sweep of k keypoints (host-side counters from the last sync): slots, blocks,
+// table load <= 1/2, pools at most half full (a sweep can at most double what its blocks hold)
+static int gmap_reserve(bshot_ctx* c, int k) {
+    GMap& g = *c->gmap;
+    const int* h = g.p_ctr.p;
+    HIPCHK(grow_keep(g.kpos, (size_t)g.slots, (size_t)g.slots + k + 1, c->stream), "gmap slots");
+    HIPCHK(grow_keep(g.kdesc, 11 * (size_t)g.slots, 11 * ((size_t)g.slots + k + 1), c->stream), "gmap slots");
+    const size_t nb = (size_t)h[GM_NBLOCKS];
+    HIPCHK(grow_keep(g.blk, nb, nb + k + 1, c->stream), "gmap blocks");
+    g.blk_cap = g.blk.cap;
+    if (2 * (nb + k) > g.tsize) {
+        // rehash the block table on the host side of a sync: rebuilt from the headers
+        unsigned int ts = g.tsize;
+        while (2 * (nb + k) > ts) ts <<= 1;
+        std::vector<GBlock> hb(nb);
+        if (nb) HIPCHK(hipMemcpy(hb.data(), g.blk.p, sizeof(GBlock) * nb, hipMemcpyDeviceToHost), "gmap headers");
+        std::vector<unsigned long long> key(ts, BS_EMPTY_KEY);
+        std::vector<int> val(ts, -1);
+        for (size_t b = 0; b < nb; ++b) {
+            unsigned long long kk = hb[b].id;
+            kk ^= kk >> 29;
+            kk *= 0xBF58476D1CE4E5B9ull;
+            kk ^= kk >> 32;
+            unsigned int x = (unsigned int)kk & (ts - 1);
+            while (key[x] != BS_EMPTY_KEY) x = (x + 1) & (ts - 1);
+            key[x] = hb[b].id;
+            val[x] = (int)b;
+        }
+        HIPCHK(g.tkey.ensure(ts), "gmap table");
+        HIPCHK(g.tval.ensure(ts), "gmap table");
+        HIPCHK(hipMemcpy(g.tkey.p, key.data(), sizeof(unsigned long long) * ts, hipMemcpyHostToDevice), "gmap table");
+        HIPCHK(hipMemcpy(g.tval.p, val.data(), sizeof(int) * ts, hipMemcpyHostToDevice), "gmap table");
+        g.tsize = ts;
+    }
+    const size_t itop = (size_t)(unsigned)h[GM_ITOP], ctop = (size_t)(unsigned)h[GM_CTOP];
+    HIPCHK(grow_keep(g.ipool, itop, 2 * itop + 64 * (size_t)k + 4096, c->stream), "gmap pool");
+    HIPCHK(grow_keep(g.cpool, ctop, 2 * ctop + 16 * (size_t)k + 1024, c->stream), "gmap pool");
+    g.ipool_cap = g.ipool.cap;
+    g.cpool_cap = g.cpool.cap;
+    return BSHOT_OK;
+}
+
+int gmap_insert(bshot_ctx* c, const float* kps_host, const float* ratio_host, const unsigned int* d_bits, int k,
+                const float T[16], int* map_size) {
+    if (!c->gmap) c->gmap = new GMap();
+    GMap& g = *c->gmap;
+    int rc = gmap_init(c);
+    if (rc) return rc;
+    if (k > 0) {
+        rc = gmap_reserve(c, k);
+        if (rc) return rc;
+        HIPCHK(g.kin.ensure(4 * (size_t)k), "gmap in");
+        HIPCHK(g.p_kin.ensure(4 * (size_t)k), "gmap pinned in");
+        std::memcpy(g.p_kin.p, kps_host, sizeof(float) * 3 * k);
+        std::memcpy(g.p_kin.p + 3 * (size_t)k, ratio_host, sizeof(float) * k);
+        HIPCHK(hipMemcpyAsync(g.kin.p, g.p_kin.p, sizeof(float) * 4 * k, hipMemcpyHostToDevice, c->stream), "H2D map in");
+        HIPCHK(g.keys.ensure(2 * (size_t)k), "gmap keys");
+        HIPCHK(g.vals.ensure(2 * (size_t)k), "gmap vals");
+        HIPCHK(g.seg.ensure(3 * (size_t)k), "gmap segments");
+        const int B = 256;
+        bsk::k_gmap_prep<<<(k + B - 1) / B, B, 0, c->stream>>>(g.kin.p, g.kin.p + 3 * (size_t)k, d_bits, k, xf(T),
+                                                               g.slots, dev_view(g), g.keys.p, g.vals.p);
+        size_t tb = 0;
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
+                                         c->stream), "gmap sort size");
+        HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
+        HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
+                                         c->stream), "gmap sort");
+        HIPCHK(hipMemsetAsync(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
+        bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, c->stream>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
+        bsk::k_gmap_insert<<<std::min(k, 1024), 64, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
+        HIPCHK(hipGetLastError(), "gmap insert launch");
+        g.slots += k;
+    }
+    HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync map");
+    if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > LDS image or pool)", BSHOT_ECAP);
+    *map_size = g.p_ctr.p[GM_MEMBERS];
+    return BSHOT_OK;
+}
+
+int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_kps, const unsigned int* ref_bits,
+               int kref, const float ref_pose[16], int na, int canonical, int* nb_out) {
+    if (!c->gmap) c->gmap = new GMap();
+    GMap& g = *c->gmap;
+    int rc = gmap_init(c);
+    if (rc) return rc;
+    const int prec = 10000;
+    // the reference's loop bounds (src/mymap.cpp:30-36), as Map::getKeypoints computes them
+    const int x_min = (int)std::round((pos[0] - range) / (float)prec) * prec;
+    const int x_max = (int)std::round((pos[0] + range) / (float)prec) * prec;
+    const int y_min = (int)std::round((pos[1] - range) / (float)prec) * prec;
+    const int y_max = (int)std::round((pos[1] + range) / (float)prec) * prec;
+    const int z_min = (int)std::round((pos[2] - range) / (float)prec) * prec;
+    const int z_max = (int)std::round((pos[2] + range) / (float)prec) * prec;
+    int npos = 0, nx = 0, ny = 0, nz = 0;
+    if (x_max >= x_min && y_max >= y_min && z_max >= z_min) {
+        nx = (x_max - x_min) / prec + 1;
+        ny = (y_max - y_min) / prec + 1;
+        nz = (z_max - z_min) / prec + 1;
+        npos = nx * ny * nz;
+    }
+    int mmap = 0;
+    if (npos > 0 && g.p_ctr.p[GM_NBLOCKS] > 0) {
+        HIPCHK(g.qcnt.ensure((size_t)3 * npos + 1), "gmap query");
+        int* cnt = g.qcnt.p;
+        int* bidx = cnt + npos;
+        int* off = bidx + npos;
+        int* tot = off + npos;
+        bsk::k_gmap_qcount<<<(npos + 255) / 256, 256, 0, c->stream>>>(dev_view(g), x_min, y_min, z_min, ny, nz, npos, cnt,
+                                                                      bidx);
+        bsk::k_gmap_scan<<<1, 1024, 0, c->stream>>>(cnt, npos, off, tot);
+        HIPCHK(hipMemcpyAsync(g.p_ctr.p + GM_QTOT, tot, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H map total");
+        HIPCHK(hipStreamSynchronize(c->stream), "sync map query");
+        mmap = g.p_ctr.p[GM_QTOT];
+    }
+    const int nb = mmap + kref;
+    // targets: positions in c->gtgt (float3), descriptors in c->ma after the na source rows
+    HIPCHK(c->gtgt.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc targets");
+    if (c->ma.cap < 11 * ((size_t)na + nb)) {
+        // keep the source rows already staged at the front
+        HIPCHK(grow_keep(c->ma, 11 * (size_t)na, 11 * ((size_t)na + nb), c->stream), "alloc descriptors");
+    }
+    if (mmap > 0) {
+        int* cnt = g.qcnt.p;
+        bsk::k_gmap_qfill<<<std::min((npos + 3) / 4, 2048), 256, 0, c->stream>>>(
+            dev_view(g), cnt, cnt + npos, cnt + 2 * npos, npos, canonical, c->gtgt.p, c->ma.p + 11 * (size_t)na);
+    }
+    if (kref > 0) {
+        HIPCHK(g.refin.ensure(14 * (size_t)kref), "gmap ref");
+        HIPCHK(g.p_refin.ensure(14 * (size_t)kref), "gmap pinned ref");
+        std::memcpy(g.p_refin.p, ref_kps, sizeof(float) * 3 * kref);
+        std::memcpy(g.p_refin.p + 3 * (size_t)kref, ref_bits, sizeof(unsigned int) * 11 * kref);
+        HIPCHK(hipMemcpyAsync(g.refin.p, g.p_refin.p, sizeof(float) * 14 * kref, hipMemcpyHostToDevice, c->stream),
+               "H2D ref");
+        bsk::k_gmap_ref<<<(kref + 255) / 256, 256, 0, c->stream>>>(
+            g.refin.p, reinterpret_cast<const unsigned int*>(g.refin.p + 3 * (size_t)kref), kref, xf(ref_pose),
+            c->gtgt.p + 3 * (size_t)mmap, c->ma.p + 11 * ((size_t)na + mmap));
+    }
+    HIPCHK(hipGetLastError(), "gmap query launch");
+    *nb_out = nb;
+    return BSHOT_OK;
+}
+
+int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], float range, const float* ref_kps,
+               const unsigned int* ref_bits, int kref, const float ref_pose[16], int canonical, int* nb_out,
+               std::vector<float>& tgt, int32_t* left_nn, std::vector<int32_t>& right_nn, int32_t* corr_q,
+               int32_t* corr_m, int* n_corr) {
+    *n_corr = 0;
+    HIPCHK(grow_keep(c->ma, 0, 11 * (size_t)(na > 0 ? na : 1), c->stream), "alloc descriptors");
+    if (na > 0) {
+        HIPCHK(c->p_a.ensure(11 * (size_t)na), "alloc pinned descriptors");
+        std::memcpy(c->p_a.p, a, sizeof(uint32_t) * 11 * na);
+        HIPCHK(hipMemcpyAsync(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * na, hipMemcpyHostToDevice, c->stream),
+               "H2D descriptors");
+    }
+    int nb = 0;
+    int rc = gmap_query(c, pos, range, ref_kps, ref_bits, kref, ref_pose, na, canonical, &nb);
+    if (rc) return rc;
+    *nb_out = nb;
+    tgt.resize(3 * (size_t)nb);
+    right_nn.assign(nb > 0 ? nb : 1, 0);
+    HIPCHK(c->p_g3.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc pinned targets");
+    if (nb > 0)
+        HIPCHK(hipMemcpyAsync(c->p_g3.p, c->gtgt.p, sizeof(float) * 3 * nb, hipMemcpyDeviceToHost, c->stream),
+               "D2H targets");
+    const bool run = na > 0 && nb > 0;
+    if (run) {
+        HIPCHK(c->p_left.ensure(2 * (size_t)na + nb), "alloc pinned match out");
+        rc = ctx_match_dev(c, na, nb);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb), hipMemcpyDeviceToHost,
+                              c->stream),
+               "D2H match");
+    }
+    HIPCHK(hipStreamSynchronize(c->stream), "sync match");
+    c->resolve_events();
+    if (nb > 0) std::memcpy(tgt.data(), c->p_g3.p, sizeof(float) * 3 * nb);
+    if (!run) return BSHOT_OK;
+    std::memcpy(left_nn, c->p_left.p, sizeof(int) * na);
+    std::memcpy(right_nn.data(), c->p_left.p + na, sizeof(int) * nb);
+    const int* flag = c->p_left.p + na + nb;
+    int m = 0;
+    for (int i = 0; i < na; ++i)
+        if (flag[i]) { corr_q[m] = i; corr_m[m] = left_nn[i]; ++m; }
+    *n_corr = m;
+    return BSHOT_OK;
+}
+
+int gmap_target_descriptors(bshot_ctx* c, int na, int nb, unsigned int* out) {
+    if (nb > 0)
+        HIPCHK(hipMemcpy(out, c->ma.p + 11 * (size_t)na, sizeof(unsigned int) * 11 * nb, hipMemcpyDeviceToHost),
+               "D2H target descriptors");
+    return BSHOT_OK;
+}
+
+void gmap_free(bshot_ctx* c) {
+    delete c->gmap;
+    c->gmap = nullptr;
+}
+
+}  // namespace bsh

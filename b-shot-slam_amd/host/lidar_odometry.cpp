@@ -11,6 +11,7 @@
 #include <thread>
 
 #include "../csrc/ctx.h"
+#include "../csrc/gmap.h"
 #include "geom.h"
 #include "../../include/bshot/tic_toc.h"
 
@@ -487,9 +488,74 @@ void LidarOdometry::computeDescriptors() {
     stats_.host_ms[2] = (float)t_d.toc();
 }
 
+bool LidarOdometry::gpuMap() const { return ctx_->opt_gpu_map != 0; }
+
+void LidarOdometry::syncHostMap() {
+    // replay updateMap's offers into the host Map (same keypoints, ratios, descriptors, poses, order)
+    for (; map_log_done_ < map_log_.size(); ++map_log_done_) {
+        MapLogEntry& e = map_log_[map_log_done_];
+        const Matrix3f R = e.T.block33();
+        const Vector3f T = e.T.topRightCorner();
+        for (size_t i = 0; i < e.ratios.size(); ++i) {
+            Vector3f kp_pos = R * e.kps->at(i) + T;
+            bshot_descriptor d;
+            d.bits = e.desc->at(i);
+            globalMap_.addKeypoint(Keypoint::createKeypoint(kp_pos, e.ratios[i], d));
+        }
+        e.kps.reset();
+        e.desc.reset();
+        e.ratios.clear();
+    }
+}
+
+const std::vector<bshot_descriptor>& LidarOdometry::targetDescriptors() {
+    if (targets_on_device_) {
+        const int nb = (int)cloud2_kps_.size();
+        std::vector<uint32_t> w(11 * (size_t)(nb > 0 ? nb : 1));
+        check(bsh::gmap_target_descriptors(ctx_, last_na_, nb, w.data()), "target descriptors");
+        cloud2_bshot_.resize(nb);
+        for (int i = 0; i < nb; ++i) cloud2_bshot_[i].bits = words_to_bits(&w[11 * (size_t)i]);
+        targets_on_device_ = false;
+    }
+    return cloud2_bshot_;
+}
+
 void LidarOdometry::featureMatching() {
     // src/lidar_odometry.cpp:186-265
     TicToc t_m;
+    targets_on_device_ = false;
+    if (!isInitial() && gpuMap()) {
+        // the targets are assembled in HBM (csrc/gmap.hip): map blocks around the ref position in
+        // the reference's loop and libstdc++ order, then the ref keypoints in the world frame
+        const Matrix4f rp = ref_->getPose();
+        const Vector3f pos = rp.topRightCorner();
+        Frame::PCPtr rk = ref_->getKeypoints();
+        Frame::DCPPtr rd = ref_->getDescriptors();
+        const int kref = rk && rd ? (int)std::min(rk->size(), rd->size()) : 0;
+        std::vector<uint32_t> refw(11 * (size_t)(kref > 0 ? kref : 1));
+        for (int i = 0; i < kref; ++i) bits_to_words((*rd)[i], &refw[11 * (size_t)i]);
+        const int na = (int)cloud1_bshot_.size();
+        std::vector<uint32_t> a(11 * (size_t)(na > 0 ? na : 1));
+        for (int i = 0; i < na; ++i) bits_to_words(cloud1_bshot_[i].bits, &a[11 * (size_t)i]);
+        std::vector<int32_t> left(na > 0 ? na : 1), right, cq(na > 0 ? na : 1), cm(na > 0 ? na : 1);
+        std::vector<float> tgt;
+        int nb = 0, nc = 0;
+        ctx_->hmark("M_match_prep");
+        check(bsh::gmap_match(ctx_, a.data(), na, pos.v, prm_.map_range, kref ? &(*rk)[0][0] : nullptr, refw.data(), kref,
+                              rp.m, ctx_->opt_gpu_map == 2, &nb, tgt, left.data(), right, cq.data(), cm.data(), &nc),
+              "match");
+        ctx_->hmark("M_matched");
+        cloud2_kps_.resize(nb);
+        if (nb > 0) std::memcpy(&cloud2_kps_[0][0], tgt.data(), sizeof(float) * 3 * nb);
+        cloud2_bshot_.clear();
+        targets_on_device_ = true;
+        last_na_ = na;
+        stats_.n_target = nb;
+        stats_.n_mutual = nc;
+        stats_.host_ms[3] = (float)t_m.toc();
+        ransacStep(na, nb, cq, cm, nc);
+        return;
+    }
     if (isInitial()) {
         passSrc2Ref();
         ref_->setKeypoints(src_->getKeypoints());
@@ -515,6 +581,10 @@ void LidarOdometry::featureMatching() {
     ctx_->hmark("M_matched");
     stats_.n_mutual = nc;
     stats_.host_ms[3] = (float)t_m.toc();
+    ransacStep(na, nb, cq, cm, nc);
+}
+
+void LidarOdometry::ransacStep(int na, int nb, const std::vector<int32_t>& cq, const std::vector<int32_t>& cm, int nc) {
     TicToc t_r;
     // RANSAC rejection (maxIter 2000, threshold 1500 mm)
     std::vector<int32_t> iq(nc > 0 ? nc : 1), im(nc > 0 ? nc : 1);
@@ -567,7 +637,16 @@ void LidarOdometry::evaluateEstimation() {
     }
     float Ticp[16];
     int iters = 0;
-    check(bshot_icp(ctx_, src.data(), k, m ? &cloud2_kps_[0][0] : nullptr, m, prm_.icp_max_iter, Ticp, &iters), "icp");
+    if (targets_on_device_) {
+        // the targets are already in HBM (gmap_match)
+        check(bsh::ctx_icp(ctx_, src.data(), k, m ? &cloud2_kps_[0][0] : nullptr, m, prm_.icp_max_iter, Ticp, &iters,
+                           ctx_->gtgt.p),
+              "icp");
+        ctx_->resolve_events();
+    } else {
+        check(bshot_icp(ctx_, src.data(), k, m ? &cloud2_kps_[0][0] : nullptr, m, prm_.icp_max_iter, Ticp, &iters),
+              "icp");
+    }
     stats_.icp_iters = iters;
     ctx_->hmark("M_icp");
     stats_.host_ms[5] = (float)t_icp.toc();
@@ -588,18 +667,30 @@ void LidarOdometry::poseEstimation() { src_->setPose(T_best_); }
 void LidarOdometry::updateMap() {
     // src/lidar_odometry.cpp:344-376 (shouldUpdateMap is never read by the reference)
     TicToc t_map;
-    const Matrix3f R = T_best_.block33();
-    const Vector3f T = T_best_.topRightCorner();
     Frame::PCPtr kps = src_->getKeypoints();
-    for (size_t i = 0; i < cloud1_bshot_.size(); i++) {
-        Vector3f kp_pos = R * kps->at(i) + T;
-        Keypoint::Ptr kp = Keypoint::createKeypoint(kp_pos, seg_ratios_[i], cloud1_bshot_[i]);
-        globalMap_.addKeypoint(kp);
+    if (gpuMap()) {
+        // csrc/gmap.hip: the same inserts in HBM; the descriptors are the rows featureMatching staged
+        const int k = (int)cloud1_bshot_.size();
+        map_log_.push_back(MapLogEntry{kps, src_->getDescriptors(), std::vector<float>(seg_ratios_.begin(),
+                                                                                       seg_ratios_.begin() + k),
+                                       T_best_});
+        int msz = 0;
+        check(bsh::gmap_insert(ctx_, k ? &(*kps)[0][0] : nullptr, seg_ratios_.data(), ctx_->ma.p, k, T_best_.m, &msz),
+              "map update");
+        stats_.map_size = msz;
+    } else {
+        const Matrix3f R = T_best_.block33();
+        const Vector3f T = T_best_.topRightCorner();
+        for (size_t i = 0; i < cloud1_bshot_.size(); i++) {
+            Vector3f kp_pos = R * kps->at(i) + T;
+            Keypoint::Ptr kp = Keypoint::createKeypoint(kp_pos, seg_ratios_[i], cloud1_bshot_[i]);
+            globalMap_.addKeypoint(kp);
+        }
+        stats_.map_size = globalMap_.size();
     }
     status_ = RUN;
     std::memcpy(stats_.T_ransac, T_ransac_.m, sizeof(stats_.T_ransac));
     std::memcpy(stats_.pose, T_best_.m, sizeof(stats_.pose));
-    stats_.map_size = globalMap_.size();
     stats_.host_ms[6] = (float)t_map.toc();
     ctx_->hmark("M_map");
 }
@@ -655,6 +746,7 @@ PointCloudXYZ LidarOdometry::issKpDetection(const PointCloudXYZ& kps) {
 }
 
 Frame::PCPtr LidarOdometry::getKeypoints() {
+    syncHostMap();
     Frame::PCPtr kps = std::make_shared<std::vector<Vector3f>>();
     globalMap_.getAllKeypoints(*kps);
     return kps;
@@ -678,6 +770,7 @@ std::vector<bshot_descriptor> LidarOdometry::eigen2dc(Frame::DCPPtr pcptr) {
 }
 
 std::vector<LidarOdometry::PC> LidarOdometry::getBlockKeypoints() {
+    syncHostMap();
     std::vector<PC> kpblock;
     globalMap_.getBlockKeypoints(kpblock);
     return kpblock;

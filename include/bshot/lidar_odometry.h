@@ -78,9 +78,13 @@ class LidarOdometry {
     bshot_ctx* context() { return ctx_; }
     const std::vector<float>& segRatios() const { return seg_ratios_; }
     const PointCloudXYZ& targetKeypoints() const { return cloud2_kps_; }
-    const std::vector<bshot_descriptor>& targetDescriptors() const { return cloud2_bshot_; }
+    // with the GPU map the target descriptors stay in HBM until asked for
+    const std::vector<bshot_descriptor>& targetDescriptors();
     const std::vector<std::pair<int, int>>& inlierCorrespondences() const { return corr_; }
-    Map& globalMap() { return globalMap_; }
+    Map& globalMap() {
+        syncHostMap();
+        return globalMap_;
+    }
     const std::string& lastError() const { return err_; }
 
   private:
@@ -118,6 +122,22 @@ class LidarOdometry {
     PointCloudXYZ isskps_src, isskps_ref;
     bshot_frame_stats stats_;
     std::string err_;
+    // GPU map (context option gpu_map, csrc/gmap.hip): the map lives in HBM; the host Map above is
+    // rebuilt on demand (getKeypoints, getBlockKeypoints, globalMap) by replaying what updateMap
+    // offered it, in order
+    struct MapLogEntry {
+        Frame::PCPtr kps;
+        Frame::DCPPtr desc;
+        std::vector<float> ratios;
+        Matrix4f T;
+    };
+    std::vector<MapLogEntry> map_log_;
+    size_t map_log_done_ = 0;
+    bool targets_on_device_ = false;  // cloud2_bshot_ not filled: the rows are in the context
+    int last_na_ = 0;
+    void syncHostMap();
+    bool gpuMap() const;
+    void ransacStep(int na, int nb, const std::vector<int32_t>& cq, const std::vector<int32_t>& cm, int nc);
 };
 
 }  // namespace myslam

@@ -27,6 +27,8 @@ typedef struct {
     int icp_max_iter;       /* 10 (PCL default) */
     int run_icp;            /* 1     test/odometry_test.cpp:41 */
     int run_iss;            /* 1 (ISS runs every frame, :164-170) */
+    int map_canonical;      /* 0: map blocks in libstdc++ unordered_map order (the reference); 1: in
+                               first-insert order (the GPU map's canonical mode, not the reference's) */
 } oracle_params;
 
 typedef struct {

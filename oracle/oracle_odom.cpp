@@ -41,6 +41,9 @@ class OMap {
     typedef std::unordered_map<V3, std::shared_ptr<Kp>, MapHasher> Block;
     const int prec = 10000;
     std::unordered_map<unsigned long, Block> blocks;
+    // canonical order (the GPU map's mode 2, not the reference's): each block's keys in first-insert order
+    bool canonical = false;
+    std::unordered_map<unsigned long, std::vector<V3>> first_order;
 
     unsigned long block_id(const V3& p) const {  // src/mymap.cpp:95-105
         const float gx = (float)((int)std::round(p.v[0] / (float)prec) * prec);
@@ -58,6 +61,7 @@ class OMap {
             Block b;
             b.insert(std::make_pair(kp->pos, kp));
             blocks.insert(std::make_pair(id, b));
+            if (canonical) first_order[id].push_back(kp->pos);
             return;
         }
         bool cand = true;
@@ -66,7 +70,10 @@ class OMap {
                         dz = kp->pos.v[2] - e.first.v[2];
             if (std::sqrt(dx * dx + (dy * dy + dz * dz)) < 800 && kp->ratio <= e.second->ratio) cand = false;
         }
-        if (cand) blocks[id][kp->pos] = kp;
+        if (cand) {
+            if (canonical && blocks[id].find(kp->pos) == blocks[id].end()) first_order[id].push_back(kp->pos);
+            blocks[id][kp->pos] = kp;
+        }
     }
     void query(const V3& pos, float range, std::vector<P3>& kps, std::vector<Desc>& ds) {  // :28-74
         kps.clear();
@@ -83,6 +90,13 @@ class OMap {
                     const V3 c = {{(float)x, (float)y, (float)z}};
                     auto it = blocks.find(block_id(c));
                     if (it == blocks.end()) continue;
+                    if (canonical) {
+                        for (const V3& q : first_order[it->first]) {
+                            kps.push_back({q.v[0], q.v[1], q.v[2]});
+                            ds.push_back(it->second.find(q)->second->d);
+                        }
+                        continue;
+                    }
                     for (auto& e : it->second) {
                         kps.push_back({e.first.v[0], e.first.v[1], e.first.v[2]});
                         ds.push_back(e.second->d);
@@ -173,6 +187,7 @@ class OOdom {
     float T_best[16];
 
     explicit OOdom(const oracle_params& pp) : p(pp) {
+        map.canonical = pp.map_canonical != 0;
         for (int i = 0; i < 16; ++i) ransac_T[i] = T_best[i] = (i % 5 == 0) ? 1.f : 0.f;
     }
 
@@ -303,6 +318,7 @@ void oracle_default_params(oracle_params* p) {
     p->iss_salient = 60.f; p->iss_nonmax = 40.f; p->iss_gamma21 = 0.975; p->iss_gamma32 = 0.975; p->iss_min_nn = 5;
     p->normal_radius = 3000.f; p->normal_max_nn = 300; p->shot_radius = 3000.f; p->map_range = 100000.f;
     p->ransac_max_iter = 2000; p->ransac_thresh = 1500.0; p->icp_max_iter = 10; p->run_icp = 1; p->run_iss = 1;
+    p->map_canonical = 0;
 }
 void* oracle_odom_create(const oracle_params* p) { return new OOdom(*p); }
 void oracle_odom_destroy(void* h) { delete static_cast<OOdom*>(h); }

@@ -21,6 +21,7 @@ class OParams(ctypes.Structure):
         ("normal_radius", ctypes.c_float), ("normal_max_nn", ctypes.c_int), ("shot_radius", ctypes.c_float),
         ("map_range", ctypes.c_float), ("ransac_max_iter", ctypes.c_int), ("ransac_thresh", ctypes.c_double),
         ("icp_max_iter", ctypes.c_int), ("run_icp", ctypes.c_int), ("run_iss", ctypes.c_int),
+        ("map_canonical", ctypes.c_int),
     ]
 
 

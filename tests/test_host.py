@@ -1,10 +1,14 @@
 """Host-side product code (no GPU): top-K selection, RANSAC, keypoint map, bitset layout --
 each checked against the oracle or against the reference formula restated here."""
+import os
+
 import numpy as np
 import pytest
 
 import bshot_py
 import oracle_ref as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # ----------------------------------------------------------------------------- top-K (std::sort tail)
@@ -164,3 +168,15 @@ def test_map_query_block_scan_order(seed):
         b = maps[1].query(pos, rng_mm)
         assert len(a[0]) == len(b[0])
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_umap_order_restatement_matches_libstdcxx(tmp_path):
+    """csrc/umap_order.h (the GPU map's per-block iteration order) against this image's libstdc++
+    std::unordered_map<Vector3f, ., MapHasher>: bucket counts and iteration order after every insert
+    of random 10 mm-grid keys, repeats included (b-shot-slam_amd/tools/umap_order_check.cpp)."""
+    import subprocess
+    exe = tmp_path / "umcheck"
+    src = os.path.join(ROOT, "b-shot-slam_amd", "tools", "umap_order_check.cpp")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", str(exe), src])
+    out = subprocess.run([str(exe), "300"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
