@@ -48,14 +48,14 @@ struct GMap {
     size_t cpool_cap = 0;
     // per-sweep scratch
     DBuf<float> kin, refin;
-    PinBuf<float> p_kin, p_refin;
+    PinBuf<float> p_kin, p_refin, p_tgt;
     DBuf<unsigned long long> keys;
     DBuf<unsigned int> vals;
     DBuf<int> seg, qcnt;
     DBuf<unsigned char> tmp;
     ~GMap() {
         kpos.release(); kdesc.release(); tkey.release(); tval.release(); blk.release(); ctr.release(); p_ctr.release();
-        ipool.release(); cpool.release(); kin.release(); refin.release(); p_kin.release(); p_refin.release();
+        ipool.release(); cpool.release(); kin.release(); refin.release(); p_kin.release(); p_refin.release(); p_tgt.release();
         keys.release(); vals.release(); seg.release(); qcnt.release(); tmp.release();
     }
 };

@@ -586,9 +586,12 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
     *nb_out = nb;
     tgt.resize(3 * (size_t)nb);
     right_nn.assign(nb > 0 ? nb : 1, 0);
-    HIPCHK(c->p_g3.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc pinned targets");
+    // its own pinned staging: the context's gather buffer (p_g3) belongs to the lookahead worker's
+    // ISS gather, which runs concurrently
+    GMap& g = *c->gmap;
+    HIPCHK(g.p_tgt.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc pinned targets");
     if (nb > 0)
-        HIPCHK(hipMemcpyAsync(c->p_g3.p, c->gtgt.p, sizeof(float) * 3 * nb, hipMemcpyDeviceToHost, c->stream),
+        HIPCHK(hipMemcpyAsync(g.p_tgt.p, c->gtgt.p, sizeof(float) * 3 * nb, hipMemcpyDeviceToHost, c->stream),
                "D2H targets");
     const bool run = na > 0 && nb > 0;
     if (run) {
@@ -601,7 +604,7 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
     }
     HIPCHK(hipStreamSynchronize(c->stream), "sync match");
     c->resolve_events();
-    if (nb > 0) std::memcpy(tgt.data(), c->p_g3.p, sizeof(float) * 3 * nb);
+    if (nb > 0) std::memcpy(tgt.data(), g.p_tgt.p, sizeof(float) * 3 * nb);
     if (!run) return BSHOT_OK;
     std::memcpy(left_nn, c->p_left.p, sizeof(int) * na);
     std::memcpy(right_nn.data(), c->p_left.p + na, sizeof(int) * nb);
