@@ -63,7 +63,9 @@ ABI_SYMBOLS = [
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
     "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
-    "bshot_odom_set_option", "bshot_odom_drain", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
+    "bshot_odom_set_option", "bshot_odom_drain", "bshot_xchg_unique_id", "bshot_xchg_create",
+    "bshot_xchg_destroy", "bshot_odom_exchange", "bshot_odom_gpu_replica_size", "bshot_odom_gpu_replica_query",
+    "bshot_odom_gpu_replica_insert", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
     "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
     "bshot_pcap_load", "bshot_velodyne_decode", "bshot_velodyne_decode_device",
 ]
@@ -466,6 +468,32 @@ class Odometry:
         rec = np.ascontiguousarray(rec, np.float32).reshape(-1, 15)
         self._chk(self.L.bshot_odom_replica_insert(self.h, replica, _ptr(rec), len(rec)), "replica_insert")
 
+    def exchange(self, xchg, include_self=False):
+        """Map offer of the last sweep -> every rank's GPU replicas over RCCL (bshot_odom_exchange)."""
+        self._chk(self.L.bshot_odom_exchange(self.h, xchg.h, 1 if include_self else 0), "odom_exchange")
+
+    def gpu_replica_insert(self, replica, rec):
+        rec = np.ascontiguousarray(rec, np.float32).reshape(-1, 15)
+        self._chk(self.L.bshot_odom_gpu_replica_insert(self.h, replica, _ptr(rec), len(rec)), "gpu_replica_insert")
+
+    def gpu_replica_size(self, replica):
+        n = self.L.bshot_odom_gpu_replica_size(self.h, replica)
+        if n < 0:
+            raise BshotError(f"gpu_replica_size ({n})")
+        return n
+
+    def gpu_replica_query(self, replica, pos, rng=100000.0, cap=1 << 16):
+        xyz = np.zeros((cap, 3), np.float32)
+        bits = np.zeros((cap, 11), np.uint32)
+        p = np.ascontiguousarray(pos, np.float32)
+        n = self.L.bshot_odom_gpu_replica_query(self.h, replica, _ptr(p), ctypes.c_float(rng), _ptr(xyz), _ptr(bits),
+                                                cap)
+        if n < -1 and -n > cap:
+            return self.gpu_replica_query(replica, pos, rng, -n)
+        if n < 0:
+            raise BshotError(f"gpu_replica_query ({n})")
+        return xyz[:n].copy(), bits[:n].copy()
+
     def replica_size(self, replica):
         return self.L.bshot_odom_replica_size(self.h, replica)
 
@@ -487,6 +515,36 @@ class Odometry:
 
     def stage_reset(self):
         self.L.bshot_stage_reset(P(self.context()))
+
+
+class Exchange:
+    """RCCL map exchange between ranks (bshot_xchg): id from rank 0 (unique_id), shared by the caller."""
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_char * 128)()
+        if lib().bshot_xchg_unique_id(buf) != 0:
+            raise BshotError("bshot_xchg_unique_id")
+        return bytes(buf)
+
+    def __init__(self, uid, nranks, rank, device, kmax):
+        self.L = lib()
+        self.h = P()
+        buf = (ctypes.c_char * 128).from_buffer_copy(uid)
+        rc = self.L.bshot_xchg_create(ctypes.byref(self.h), buf, nranks, rank, device, kmax)
+        if rc != 0:
+            raise BshotError(f"bshot_xchg_create ({rc})")
+
+    def close(self):
+        if self.h:
+            self.L.bshot_xchg_destroy(self.h)
+            self.h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class KeypointMap:

@@ -179,6 +179,8 @@ struct bshot_ctx {
     // block order (default), 2 GPU map in insertion order (canonical; not the reference's order)
     int opt_gpu_map = 1;
     bsh::GMap* gmap = nullptr;
+    std::vector<bsh::GMap*> gmap_replicas;  // other sequences' maps (multi-GPU exchange, bshot_odom_exchange)
+    int opt_xseq_targets = 0;  // 1: the replicas' entries join the matching targets (extension; 0 = reference)
     DBuf<float> gtgt;  // matching targets assembled on the device (float3)
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag

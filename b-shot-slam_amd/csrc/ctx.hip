@@ -1130,6 +1130,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
     else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
+    else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;

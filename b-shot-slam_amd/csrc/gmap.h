@@ -21,6 +21,13 @@ enum { GM_NBLOCKS = 0, GM_NSEG = 1, GM_ITOP = 2, GM_CTOP = 3, GM_MEMBERS = 4, GM
 // members is 5087, umap_order.h's chain)
 constexpr int GM_LDS_N = 4096;
 constexpr int GM_LDS_BK = 5120;
+// exchange record batch: header words, then 15 words per keypoint (x, y, z, ratio, 11 descriptor words)
+constexpr int GM_REC_HDR = 16;
+constexpr int GM_REC_W = 15;
+
+struct QueryBox {
+    int x0, y0, z0, ny, nz, npos;
+};
 
 struct GBlock {
     unsigned long long id;
@@ -32,7 +39,9 @@ struct GBlock {
 
 struct GMap {
     bool ready = false;
+    bool q_active = false;  // the last query_count launched (its total is in p_ctr[GM_QTOT])
     int slots = 0;
+    int last_k = 0;  // keypoints the last gmap_insert offered (slots [slots - last_k, slots))
     DBuf<float4> kpos;
     DBuf<unsigned int> kdesc;
     DBuf<unsigned long long> tkey;
@@ -47,15 +56,15 @@ struct GMap {
     DBuf<unsigned long long> cpool;
     size_t cpool_cap = 0;
     // per-sweep scratch
-    DBuf<float> kin, refin;
-    PinBuf<float> p_kin, p_refin, p_tgt;
+    DBuf<float> kin, refin, hrec;
+    PinBuf<float> p_kin, p_refin, p_tgt, p_hrec;
     DBuf<unsigned long long> keys;
     DBuf<unsigned int> vals;
     DBuf<int> seg, qcnt;
     DBuf<unsigned char> tmp;
     ~GMap() {
         kpos.release(); kdesc.release(); tkey.release(); tval.release(); blk.release(); ctr.release(); p_ctr.release();
-        ipool.release(); cpool.release(); kin.release(); refin.release(); p_kin.release(); p_refin.release(); p_tgt.release();
+        ipool.release(); cpool.release(); kin.release(); refin.release(); p_kin.release(); p_refin.release(); p_tgt.release(); hrec.release(); p_hrec.release();
         keys.release(); vals.release(); seg.release(); qcnt.release(); tmp.release();
     }
 };
@@ -75,6 +84,17 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
                const unsigned int* ref_bits, int kref, const float ref_pose[16], int canonical, int* nb_out,
                std::vector<float>& tgt, int32_t* left_nn, std::vector<int32_t>& right_nn, int32_t* corr_q,
                int32_t* corr_m, int* n_corr);
+// this sweep's map offer (the last gmap_insert's slots) as an exchange record batch at d_rec
+// (GM_REC_HDR + GM_REC_W * kmax floats), on c->stream
+int gmap_pack_delta(bshot_ctx* c, int kmax, float* d_rec);
+// a record batch (device, count in the header) inserted into replica map `replica` on c->stream
+int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync);
+// host records (bshot_odom_map_delta's 15-float layout) -> replica map (synchronous)
+int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n);
+int gmap_replica_size(bshot_ctx* c, int replica);
+// replica's entries around pos (block loop order; libstdc++ or canonical order) -> host; count or -needed
+int gmap_replica_query(bshot_ctx* c, int replica, const float pos[3], float range, int canonical, float* xyz,
+                       unsigned int* bits, int cap);
 // the last gmap_match's target descriptors (rows [na, na + nb) of c->ma) -> host
 int gmap_target_descriptors(bshot_ctx* c, int na, int nb, unsigned int* out);
 void gmap_free(bshot_ctx* c);

@@ -43,6 +43,8 @@ using bsh::GM_LDS_N;
 using bsh::GM_MEMBERS;
 using bsh::GM_NBLOCKS;
 using bsh::GM_NSEG;
+using bsh::GM_REC_HDR;
+using bsh::GM_REC_W;
 
 struct GMapDev {
     float4* kpos;
@@ -110,11 +112,46 @@ __global__ void k_gmap_prep(const float* __restrict__ kps, const float* __restri
     vals[i] = (unsigned int)i;
 }
 
+// Exchange records (BASELINE config 4): word 0 of a 16-word header = the count (int bits), then kmax
+// records of 15 words: x, y, z (10 mm grid, world), ratio, 11 descriptor words.
+__global__ void k_gmap_pack(GMapDev m, int slot_base, int k, int kmax, float* __restrict__ rec) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) rec[0] = __int_as_float(k);
+    if (i >= k) return;
+    const int s = slot_base + i;
+    float* r = rec + GM_REC_HDR + GM_REC_W * (size_t)i;
+    const float4 p = m.kpos[s];
+    r[0] = p.x; r[1] = p.y; r[2] = p.z; r[3] = p.w;
+#pragma unroll
+    for (int w = 0; w < 11; ++w) r[4 + w] = __uint_as_float(m.kdesc[11 * (size_t)s + w]);
+}
+
+// a record batch -> slots (positions are already on the grid: createKeypoint is idempotent on them),
+// block ids; records past the count get the empty key (sorted last, skipped by k_gmap_segments)
+__global__ void k_gmap_prep_rec(const float* __restrict__ rec, int kmax, int slot_base, GMapDev m,
+                                unsigned long long* __restrict__ keys, unsigned int* __restrict__ vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kmax) return;
+    const int cnt = __float_as_int(rec[0]);
+    vals[i] = (unsigned int)i;
+    if (i >= cnt) {
+        keys[i] = BS_EMPTY_KEY;
+        return;
+    }
+    const float* r = rec + GM_REC_HDR + GM_REC_W * (size_t)i;
+    const int s = slot_base + i;
+    m.kpos[s] = make_float4(r[0], r[1], r[2], r[3]);
+#pragma unroll
+    for (int w = 0; w < 11; ++w) m.kdesc[11 * (size_t)s + w] = __float_as_uint(r[4 + w]);
+    keys[i] = block_id_of(r[0], r[1], r[2]);
+}
+
 // one thread per run of equal block ids in the sorted keys: find or create the block, record the run
 __global__ void k_gmap_segments(const unsigned long long* __restrict__ keys, int k, GMapDev m, int* __restrict__ seg) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= k) return;
     const unsigned long long id = keys[j];
+    if (id == BS_EMPTY_KEY) return;  // padding of a record batch (k_gmap_prep_rec)
     if (j > 0 && keys[j - 1] == id) return;
     int lo = j + 1, hi = k;
     while (lo < hi) {
@@ -400,8 +437,7 @@ static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s)
     return hipSuccess;
 }
 
-static int gmap_init(bshot_ctx* c) {
-    GMap& g = *c->gmap;
+static int gmap_init(bshot_ctx* c, GMap& g) {
     if (g.ready) return BSHOT_OK;
     g.tsize = 1u << 16;
     HIPCHK(g.tkey.ensure(g.tsize), "gmap table");
@@ -424,10 +460,21 @@ static int gmap_init(bshot_ctx* c) {
     return BSHOT_OK;
 }
 
-// room for one more sweep of k keypoints (host-side counters from the last sync): slots, blocks,
-// table load <= 1/2, pools at most half full (a sweep can at most double what its blocks hold)
-static int gmap_reserve(bshot_ctx* c, int k) {
-    GMap& g = *c->gmap;
+static GMap& own_map(bshot_ctx* c) {
+    if (!c->gmap) c->gmap = new GMap();
+    return *c->gmap;
+}
+
+static GMap& replica_map(bshot_ctx* c, int r) {
+    if ((int)c->gmap_replicas.size() <= r) c->gmap_replicas.resize(r + 1, nullptr);
+    if (!c->gmap_replicas[r]) c->gmap_replicas[r] = new GMap();
+    return *c->gmap_replicas[r];
+}
+
+// room for one more batch of k keypoints (counters as of the map's last D2H, which a later sync on
+// the stream has completed): slots, blocks, table load <= 1/2, pools at most half full (a batch
+// can at most double what its blocks hold)
+static int gmap_reserve(bshot_ctx* c, GMap& g, int k) {
     const int* h = g.p_ctr.p;
     HIPCHK(grow_keep(g.kpos, (size_t)g.slots, (size_t)g.slots + k + 1, c->stream), "gmap slots");
     HIPCHK(grow_keep(g.kdesc, 11 * (size_t)g.slots, 11 * ((size_t)g.slots + k + 1), c->stream), "gmap slots");
@@ -436,6 +483,7 @@ static int gmap_reserve(bshot_ctx* c, int k) {
     g.blk_cap = g.blk.cap;
     if (2 * (nb + k) > g.tsize) {
         // rehash the block table on the host side of a sync: rebuilt from the headers
+        HIPCHK(hipStreamSynchronize(c->stream), "sync map table");
         unsigned int ts = g.tsize;
         while (2 * (nb + k) > ts) ts <<= 1;
         std::vector<GBlock> hb(nb);
@@ -466,91 +514,180 @@ static int gmap_reserve(bshot_ctx* c, int k) {
     return BSHOT_OK;
 }
 
+// sort the batch's block ids (stable: sweep order inside a block), runs -> segments, insert waves;
+// the counters go to the pinned copy (synchronously when sync)
+static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync) {
+    const int B = 256;
+    size_t tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
+                                     c->stream), "gmap sort size");
+    HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
+    HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
+                                     c->stream), "gmap sort");
+    HIPCHK(hipMemsetAsync(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
+    bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, c->stream>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
+    bsk::k_gmap_insert<<<std::min(k, 1024), 64, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
+    HIPCHK(hipGetLastError(), "gmap insert launch");
+    g.slots += k;
+    HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");
+    if (sync) {
+        HIPCHK(hipStreamSynchronize(c->stream), "sync map");
+        if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > LDS image or pool)", BSHOT_ECAP);
+    }
+    return BSHOT_OK;
+}
+
+static int gmap_scratch(bshot_ctx* c, GMap& g, int k) {
+    HIPCHK(g.keys.ensure(2 * (size_t)k), "gmap keys");
+    HIPCHK(g.vals.ensure(2 * (size_t)k), "gmap vals");
+    HIPCHK(g.seg.ensure(3 * (size_t)k), "gmap segments");
+    return BSHOT_OK;
+}
+
 int gmap_insert(bshot_ctx* c, const float* kps_host, const float* ratio_host, const unsigned int* d_bits, int k,
                 const float T[16], int* map_size) {
-    if (!c->gmap) c->gmap = new GMap();
-    GMap& g = *c->gmap;
-    int rc = gmap_init(c);
+    GMap& g = own_map(c);
+    int rc = gmap_init(c, g);
     if (rc) return rc;
+    g.last_k = k;
     if (k > 0) {
-        rc = gmap_reserve(c, k);
-        if (rc) return rc;
+        if ((rc = gmap_reserve(c, g, k)) || (rc = gmap_scratch(c, g, k))) return rc;
         HIPCHK(g.kin.ensure(4 * (size_t)k), "gmap in");
         HIPCHK(g.p_kin.ensure(4 * (size_t)k), "gmap pinned in");
         std::memcpy(g.p_kin.p, kps_host, sizeof(float) * 3 * k);
         std::memcpy(g.p_kin.p + 3 * (size_t)k, ratio_host, sizeof(float) * k);
         HIPCHK(hipMemcpyAsync(g.kin.p, g.p_kin.p, sizeof(float) * 4 * k, hipMemcpyHostToDevice, c->stream), "H2D map in");
-        HIPCHK(g.keys.ensure(2 * (size_t)k), "gmap keys");
-        HIPCHK(g.vals.ensure(2 * (size_t)k), "gmap vals");
-        HIPCHK(g.seg.ensure(3 * (size_t)k), "gmap segments");
-        const int B = 256;
-        bsk::k_gmap_prep<<<(k + B - 1) / B, B, 0, c->stream>>>(g.kin.p, g.kin.p + 3 * (size_t)k, d_bits, k, xf(T),
-                                                               g.slots, dev_view(g), g.keys.p, g.vals.p);
-        size_t tb = 0;
-        HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
-                                         c->stream), "gmap sort size");
-        HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
-        HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
-                                         c->stream), "gmap sort");
-        HIPCHK(hipMemsetAsync(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
-        bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, c->stream>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
-        bsk::k_gmap_insert<<<std::min(k, 1024), 64, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
-        HIPCHK(hipGetLastError(), "gmap insert launch");
-        g.slots += k;
+        bsk::k_gmap_prep<<<(k + 255) / 256, 256, 0, c->stream>>>(g.kin.p, g.kin.p + 3 * (size_t)k, d_bits, k, xf(T),
+                                                                 g.slots, dev_view(g), g.keys.p, g.vals.p);
+        if ((rc = gmap_run_insert(c, g, k, true))) return rc;
+    } else {
+        HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");
+        HIPCHK(hipStreamSynchronize(c->stream), "sync map");
     }
-    HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");
-    HIPCHK(hipStreamSynchronize(c->stream), "sync map");
-    if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > LDS image or pool)", BSHOT_ECAP);
     *map_size = g.p_ctr.p[GM_MEMBERS];
     return BSHOT_OK;
 }
 
-int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_kps, const unsigned int* ref_bits,
-               int kref, const float ref_pose[16], int na, int canonical, int* nb_out) {
-    if (!c->gmap) c->gmap = new GMap();
-    GMap& g = *c->gmap;
-    int rc = gmap_init(c);
+int gmap_pack_delta(bshot_ctx* c, int kmax, float* d_rec) {
+    GMap& g = own_map(c);
+    int rc = gmap_init(c, g);
     if (rc) return rc;
+    const int k = std::min(g.last_k, kmax);
+    bsk::k_gmap_pack<<<(std::max(k, 1) + 255) / 256, 256, 0, c->stream>>>(dev_view(g), g.slots - g.last_k, k, kmax, d_rec);
+    HIPCHK(hipGetLastError(), "gmap pack launch");
+    return BSHOT_OK;
+}
+
+int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync) {
+    GMap& g = replica_map(c, replica);
+    int rc = gmap_init(c, g);
+    if (rc) return rc;
+    if (kmax <= 0) return BSHOT_OK;
+    if ((rc = gmap_reserve(c, g, kmax)) || (rc = gmap_scratch(c, g, kmax))) return rc;
+    bsk::k_gmap_prep_rec<<<(kmax + 255) / 256, 256, 0, c->stream>>>(d_rec, kmax, g.slots, dev_view(g), g.keys.p, g.vals.p);
+    return gmap_run_insert(c, g, kmax, sync);
+}
+
+int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n) {
+    // host records (bshot_odom_map_delta layout: x, y, z, ratio, 11 words) -> a device batch
+    GMap& g = replica_map(c, replica);
+    int rc = gmap_init(c, g);
+    if (rc) return rc;
+    const size_t per = GM_REC_HDR + (size_t)GM_REC_W * (n > 0 ? n : 1);
+    HIPCHK(g.hrec.ensure(per), "alloc replica batch");
+    HIPCHK(g.p_hrec.ensure(per), "alloc pinned replica batch");
+    std::memset(g.p_hrec.p, 0, sizeof(float) * GM_REC_HDR);
+    std::memcpy(g.p_hrec.p, &n, sizeof(int));
+    if (n > 0) std::memcpy(g.p_hrec.p + GM_REC_HDR, rec, sizeof(float) * GM_REC_W * n);
+    HIPCHK(hipMemcpyAsync(g.hrec.p, g.p_hrec.p, sizeof(float) * per, hipMemcpyHostToDevice, c->stream), "H2D batch");
+    return gmap_insert_records(c, replica, g.hrec.p, n, true);
+}
+
+int gmap_replica_size(bshot_ctx* c, int replica) {
+    if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
+    GMap& g = *c->gmap_replicas[replica];
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    if (g.p_ctr.p[GM_ERR]) return -2;
+    return g.p_ctr.p[GM_MEMBERS];
+}
+
+// the 21^3 block loop over one map: counts + scan (async; the total lands in the pinned GM_QTOT slot)
+static int query_count(bshot_ctx* c, GMap& g, const QueryBox& q) {
+    if (q.npos <= 0 || g.p_ctr.p[GM_NBLOCKS] <= 0) {
+        g.p_ctr.p[GM_QTOT] = 0;
+        g.q_active = false;
+        return BSHOT_OK;
+    }
+    HIPCHK(g.qcnt.ensure((size_t)3 * q.npos + 1), "gmap query");
+    int* cnt = g.qcnt.p;
+    bsk::k_gmap_qcount<<<(q.npos + 255) / 256, 256, 0, c->stream>>>(dev_view(g), q.x0, q.y0, q.z0, q.ny, q.nz, q.npos, cnt,
+                                                                    cnt + q.npos);
+    bsk::k_gmap_scan<<<1, 1024, 0, c->stream>>>(cnt, q.npos, cnt + 2 * q.npos, cnt + 3 * q.npos);
+    HIPCHK(hipMemcpyAsync(g.p_ctr.p + GM_QTOT, cnt + 3 * q.npos, sizeof(int), hipMemcpyDeviceToHost, c->stream),
+           "D2H map total");
+    g.q_active = true;
+    return BSHOT_OK;
+}
+
+static QueryBox query_box(const float pos[3], float range) {
     const int prec = 10000;
     // the reference's loop bounds (src/mymap.cpp:30-36), as Map::getKeypoints computes them
-    const int x_min = (int)std::round((pos[0] - range) / (float)prec) * prec;
+    QueryBox q;
+    q.x0 = (int)std::round((pos[0] - range) / (float)prec) * prec;
     const int x_max = (int)std::round((pos[0] + range) / (float)prec) * prec;
-    const int y_min = (int)std::round((pos[1] - range) / (float)prec) * prec;
+    q.y0 = (int)std::round((pos[1] - range) / (float)prec) * prec;
     const int y_max = (int)std::round((pos[1] + range) / (float)prec) * prec;
-    const int z_min = (int)std::round((pos[2] - range) / (float)prec) * prec;
+    q.z0 = (int)std::round((pos[2] - range) / (float)prec) * prec;
     const int z_max = (int)std::round((pos[2] + range) / (float)prec) * prec;
-    int npos = 0, nx = 0, ny = 0, nz = 0;
-    if (x_max >= x_min && y_max >= y_min && z_max >= z_min) {
-        nx = (x_max - x_min) / prec + 1;
-        ny = (y_max - y_min) / prec + 1;
-        nz = (z_max - z_min) / prec + 1;
-        npos = nx * ny * nz;
+    q.npos = 0;
+    q.ny = q.nz = 0;
+    if (x_max >= q.x0 && y_max >= q.y0 && z_max >= q.z0) {
+        const int nx = (x_max - q.x0) / prec + 1;
+        q.ny = (y_max - q.y0) / prec + 1;
+        q.nz = (z_max - q.z0) / prec + 1;
+        q.npos = nx * q.ny * q.nz;
     }
-    int mmap = 0;
-    if (npos > 0 && g.p_ctr.p[GM_NBLOCKS] > 0) {
-        HIPCHK(g.qcnt.ensure((size_t)3 * npos + 1), "gmap query");
-        int* cnt = g.qcnt.p;
-        int* bidx = cnt + npos;
-        int* off = bidx + npos;
-        int* tot = off + npos;
-        bsk::k_gmap_qcount<<<(npos + 255) / 256, 256, 0, c->stream>>>(dev_view(g), x_min, y_min, z_min, ny, nz, npos, cnt,
-                                                                      bidx);
-        bsk::k_gmap_scan<<<1, 1024, 0, c->stream>>>(cnt, npos, off, tot);
-        HIPCHK(hipMemcpyAsync(g.p_ctr.p + GM_QTOT, tot, sizeof(int), hipMemcpyDeviceToHost, c->stream), "D2H map total");
-        HIPCHK(hipStreamSynchronize(c->stream), "sync map query");
-        mmap = g.p_ctr.p[GM_QTOT];
+    return q;
+}
+
+int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_kps, const unsigned int* ref_bits,
+               int kref, const float ref_pose[16], int na, int canonical, int* nb_out) {
+    GMap& g = own_map(c);
+    int rc = gmap_init(c, g);
+    if (rc) return rc;
+    const QueryBox q = query_box(pos, range);
+    // the maps whose entries become targets: this sequence's, then (option xseq_targets, an
+    // extension for cross-sequence matching; off reproduces the reference) the replicas in rank order
+    std::vector<GMap*> maps{&g};
+    if (c->opt_xseq_targets)
+        for (GMap* r : c->gmap_replicas)
+            if (r && r->ready) maps.push_back(r);
+    bool any = false;
+    for (GMap* m : maps) {
+        if ((rc = query_count(c, *m, q))) return rc;
+        any = any || m->q_active;
     }
-    const int nb = mmap + kref;
+    if (any) HIPCHK(hipStreamSynchronize(c->stream), "sync map query");
+    int mtot = 0;
+    for (GMap* m : maps) mtot += m->q_active ? m->p_ctr.p[GM_QTOT] : 0;
+    const int nb = mtot + kref;
     // targets: positions in c->gtgt (float3), descriptors in c->ma after the na source rows
     HIPCHK(c->gtgt.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc targets");
     if (c->ma.cap < 11 * ((size_t)na + nb)) {
         // keep the source rows already staged at the front
         HIPCHK(grow_keep(c->ma, 11 * (size_t)na, 11 * ((size_t)na + nb), c->stream), "alloc descriptors");
     }
-    if (mmap > 0) {
-        int* cnt = g.qcnt.p;
-        bsk::k_gmap_qfill<<<std::min((npos + 3) / 4, 2048), 256, 0, c->stream>>>(
-            dev_view(g), cnt, cnt + npos, cnt + 2 * npos, npos, canonical, c->gtgt.p, c->ma.p + 11 * (size_t)na);
+    int base = 0;
+    for (GMap* m : maps) {
+        if (!m->q_active) continue;
+        const int mm = m->p_ctr.p[GM_QTOT];
+        if (mm > 0) {
+            int* cnt = m->qcnt.p;
+            bsk::k_gmap_qfill<<<std::min((q.npos + 3) / 4, 2048), 256, 0, c->stream>>>(
+                dev_view(*m), cnt, cnt + q.npos, cnt + 2 * q.npos, q.npos, canonical, c->gtgt.p + 3 * (size_t)base,
+                c->ma.p + 11 * ((size_t)na + base));
+        }
+        base += mm;
     }
     if (kref > 0) {
         HIPCHK(g.refin.ensure(14 * (size_t)kref), "gmap ref");
@@ -561,11 +698,40 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
                "H2D ref");
         bsk::k_gmap_ref<<<(kref + 255) / 256, 256, 0, c->stream>>>(
             g.refin.p, reinterpret_cast<const unsigned int*>(g.refin.p + 3 * (size_t)kref), kref, xf(ref_pose),
-            c->gtgt.p + 3 * (size_t)mmap, c->ma.p + 11 * ((size_t)na + mmap));
+            c->gtgt.p + 3 * (size_t)mtot, c->ma.p + 11 * ((size_t)na + mtot));
     }
     HIPCHK(hipGetLastError(), "gmap query launch");
     *nb_out = nb;
     return BSHOT_OK;
+}
+
+int gmap_replica_query(bshot_ctx* c, int replica, const float pos[3], float range, int canonical, float* xyz,
+                       unsigned int* bits, int cap) {
+    if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
+    GMap& g = *c->gmap_replicas[replica];
+    const QueryBox q = query_box(pos, range);
+    HIPCHK(hipStreamSynchronize(c->stream), "sync replica");
+    int rc = query_count(c, g, q);
+    if (rc) return rc;
+    if (!g.q_active) return 0;
+    HIPCHK(hipStreamSynchronize(c->stream), "sync replica query");
+    const int m = g.p_ctr.p[GM_QTOT];
+    if (m > cap) return -m;
+    if (m == 0) return 0;
+    DBuf<float> pos3;
+    DBuf<unsigned int> desc;
+    HIPCHK(pos3.ensure(3 * (size_t)m), "alloc replica query");
+    HIPCHK(desc.ensure(11 * (size_t)m), "alloc replica query");
+    int* cnt = g.qcnt.p;
+    bsk::k_gmap_qfill<<<std::min((q.npos + 3) / 4, 2048), 256, 0, c->stream>>>(dev_view(g), cnt, cnt + q.npos,
+                                                                               cnt + 2 * q.npos, q.npos, canonical,
+                                                                               pos3.p, desc.p);
+    HIPCHK(hipMemcpyAsync(xyz, pos3.p, sizeof(float) * 3 * m, hipMemcpyDeviceToHost, c->stream), "D2H replica");
+    HIPCHK(hipMemcpyAsync(bits, desc.p, sizeof(unsigned int) * 11 * m, hipMemcpyDeviceToHost, c->stream), "D2H replica");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync replica");
+    pos3.release();
+    desc.release();
+    return m;
 }
 
 int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], float range, const float* ref_kps,
@@ -626,6 +792,8 @@ int gmap_target_descriptors(bshot_ctx* c, int na, int nb, unsigned int* out) {
 void gmap_free(bshot_ctx* c) {
     delete c->gmap;
     c->gmap = nullptr;
+    for (GMap* r : c->gmap_replicas) delete r;
+    c->gmap_replicas.clear();
 }
 
 }  // namespace bsh

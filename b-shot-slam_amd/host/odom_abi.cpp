@@ -10,6 +10,10 @@
 
 #include "../../include/bshot/lidar_odometry.h"
 #include "../../include/bshot_abi.h"
+#include "../csrc/ctx.h"
+#include "../csrc/gmap.h"
+
+int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self);  // host/xchg.cpp
 
 struct bshot_odom {
     std::unique_ptr<myslam::LidarOdometry> lo;
@@ -147,6 +151,32 @@ int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2
     o->next2_d = n_next2 > 0 ? d_next2 : nullptr;
     o->next2_n = n_next2;
     return BSHOT_OK;
+}
+
+int bshot_odom_exchange(bshot_odom* o, bshot_xchg* x, int include_self) {
+    if (!o || !x) return BSHOT_EINVAL;
+    const int rc = bshot_odom_exchange_ctx(o->lo->context(), x, include_self);
+    if (rc < 0) o->err = bshot_last_error(o->lo->context());
+    return rc;
+}
+
+int bshot_odom_gpu_replica_insert(bshot_odom* o, int replica, const float* rec, int n) {
+    if (!o || replica < 0 || n < 0 || (n > 0 && !rec)) return BSHOT_EINVAL;
+    const int rc = bsh::gmap_insert_host_records(o->lo->context(), replica, rec, n);
+    if (rc < 0) o->err = bshot_last_error(o->lo->context());
+    return rc;
+}
+
+int bshot_odom_gpu_replica_size(bshot_odom* o, int replica) {
+    if (!o) return BSHOT_EINVAL;
+    return bsh::gmap_replica_size(o->lo->context(), replica);
+}
+
+int bshot_odom_gpu_replica_query(bshot_odom* o, int replica, const float pos[3], float range, float* xyz,
+                                 uint32_t* bits, int cap) {
+    if (!o || !pos || !xyz || !bits) return BSHOT_EINVAL;
+    bshot_ctx* c = o->lo->context();
+    return bsh::gmap_replica_query(c, replica, pos, range, c->opt_gpu_map == 2, xyz, bits, cap);
 }
 
 int bshot_odom_drain(bshot_odom* o) {

@@ -58,7 +58,10 @@ def parse():
     ap.add_argument("--keypoints", type=int, default=2048)
     ap.add_argument("--sensor", type=int, default=0, help="0 HDL-64 (130k), 1 VLP-128 style (256k), 2 HDL-32E (--from-lasers only)")
     ap.add_argument("--shot-radius", type=float, default=3000.0)
-    ap.add_argument("--map-bcast", action="store_true")
+    ap.add_argument("--map-bcast", action="store_true",
+                    help="per-sweep map exchange between ranks (C++ over RCCL, into GPU replicas)")
+    ap.add_argument("--map-bcast-py", action="store_true",
+                    help="with --map-bcast: the Python all_gather of host records into host replicas instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
@@ -134,6 +137,14 @@ def main():
         name, val = kv.split("=")
         odo.set_option(name, int(val))
     tot_pts = 0
+    xchg = None
+    if a.map_bcast and world > 1 and not a.map_bcast_py:
+        # the RCCL id travels once over the process group; the per-sweep exchange is the library's
+        uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(bshot_py.Exchange.unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        xchg = bshot_py.Exchange(bytes(uid.cpu().numpy().tobytes()), world, rank, local, a.keypoints)
 
     def step(i):
         # sweeps are preprocessed when first needed (this one or a lookahead)
@@ -145,7 +156,10 @@ def main():
             if a.depth >= 2 and i + 2 < nframes:
                 odo.set_next2_device(frames[i + 2].data_ptr(), npts[i + 2])
         st = odo.process_device(frames[i].data_ptr(), npts[i])
-        if a.map_bcast and world > 1:
+        if xchg is not None:
+            # C++ / RCCL: the sweep's map offer all-gathered from HBM into the GPU replicas, no host sync
+            odo.exchange(xchg)
+        elif a.map_bcast and world > 1:
             for r, rec in exchange_map_delta(odo.map_delta(), dist, dev):
                 odo.replica_insert(r, rec)
         return st
@@ -326,7 +340,7 @@ def main():
                                    f"full extract+describe+match+RANSAC+ICP+map per sweep",
                        "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
                        "icp_iters": icp_it, "parallelism": f"frame-shard x{world}" +
-                       (" + RCCL map bcast" if a.map_bcast else "")},
+                       (" + RCCL map exchange" if a.map_bcast else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "stage_ms_per_sweep": {k: round(v[0] / a.steps, 4) for k, v in stages.items() if v[1]},
@@ -336,6 +350,8 @@ def main():
                                           np.round(np.mean([list(s.host_ms) for s in stats], axis=0), 3).tolist())),
         }
         print(json.dumps(line))
+    if xchg is not None:
+        xchg.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -200,6 +200,26 @@ int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next);
 int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2);
 /* odometry knobs: forwarded to bshot_set_option on the odometry's context */
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value);
+/* Multi-GPU map exchange (BASELINE config 4; extension, no reference counterpart):
+ * one process per GPU; rank 0 makes the 128-byte RCCL id (bshot_xchg_unique_id), every rank receives
+ * it (any side channel, e.g. torch.distributed) and calls bshot_xchg_create. bshot_odom_exchange,
+ * after each process call, all-gathers every rank's map offer of that sweep (<= kmax keypoints:
+ * 10 mm grid position, ratio, 11 descriptor words) over RCCL from device buffers and inserts the
+ * other ranks' batches into GPU replicas of their maps (replica r = rank r's map; include_self also
+ * inserts this rank's own batch into replica `rank`), on the context's main stream, no host sync.
+ * Requires the GPU map (option gpu_map >= 1). RCCL is loaded at run time. */
+typedef struct bshot_xchg bshot_xchg;
+int bshot_xchg_unique_id(void* id128);
+int bshot_xchg_create(bshot_xchg** out, const void* id128, int nranks, int rank, int device, int kmax);
+void bshot_xchg_destroy(bshot_xchg* x);
+int bshot_odom_exchange(bshot_odom* o, bshot_xchg* x, int include_self);
+/* GPU replica of rank r's map: entry count (syncs), and its entries around pos within range (the
+ * reference's block loop; libstdc++ order) -> xyz (n x 3), bits (n x 11); count or -needed */
+int bshot_odom_gpu_replica_size(bshot_odom* o, int replica);
+/* host records (bshot_odom_map_delta's layout) into GPU replica r, for transports other than RCCL */
+int bshot_odom_gpu_replica_insert(bshot_odom* o, int replica, const float* rec, int n);
+int bshot_odom_gpu_replica_query(bshot_odom* o, int replica, const float pos[3], float range, float* xyz,
+                                 uint32_t* bits, int cap);
 /* wait for the lookahead work started by the last process call (the prefetched sweep's describe on
  * its worker thread, the queued sweep's launches and top-K) to be issued and finished; the results
  * stay ready for the next process call. Extension (no reference counterpart). */

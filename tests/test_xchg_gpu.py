@@ -1,0 +1,130 @@
+"""BASELINE config 4 / SURVEY.md §8e: the per-sweep map exchange between sequences (one per rank).
+
+* RCCL path (host/xchg.cpp): a one-rank communicator on the box's single GPU all-gathers the sweep's
+  map offer from device buffers into a GPU replica of the rank's own map (include_self); the replica
+  must hold exactly the map the odometry itself matches against -- same entries, same libstdc++
+  block order -- and the same size.
+* Cross-sequence targets (option xseq_targets, the replicas' consumer): the replica's entries join the
+  matching targets between the own map's and the ref keypoints.
+* Two ranks (two processes sharing the GPU, gloo as the transport of the host records): every rank
+  ends with identical replicas of every sequence, and its own poses are bit-identical to a solo run
+  (the exchange never perturbs a sequence unless xseq_targets asks for it)."""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bshot_py
+
+pytestmark = pytest.mark.gpu
+
+K = 800
+
+
+def _frames(seed=42, n=6):
+    return [bshot_py.synth_sweep(f, seed=seed)[0][::2].copy() for f in range(n)]
+
+
+def _u(a):
+    return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
+
+
+def test_rccl_exchange_self_replica():
+    uid = bshot_py.Exchange.unique_id()
+    x = bshot_py.Exchange(uid, 1, 0, 0, K)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+    try:
+        prev = None
+        for f, xyz in enumerate(_frames()):
+            rq = None
+            if prev is not None:
+                rq = od.gpu_replica_query(0, prev[0][:3, 3])
+            st = od.process(xyz)
+            if prev is not None:
+                tx, tb = od.target()
+                m = len(tx) - prev[1]  # map entries, then the ref keypoints
+                assert m == len(rq[0]) and m > 0
+                assert np.array_equal(_u(tx[:m]), _u(rq[0])) and np.array_equal(tb[:m], rq[1]), f
+            od.exchange(x, include_self=True)
+            assert od.gpu_replica_size(0) == st.map_size, f
+            prev = (np.array(st.pose, np.float32).reshape(4, 4), st.n_keypoints)
+    finally:
+        od.close()
+        x.close()
+
+
+def test_xseq_targets_append_replicas():
+    uid = bshot_py.Exchange.unique_id()
+    x = bshot_py.Exchange(uid, 1, 0, 0, K)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+    od.set_option("xseq_targets", 1)
+    try:
+        kref = 0
+        for f, xyz in enumerate(_frames(n=4)):
+            st = od.process(xyz)
+            if f > 0:
+                tx, tb = od.target()
+                m = (len(tx) - kref) // 2
+                assert m > 0 and 2 * m + kref == len(tx)
+                # own map entries, then the replica's copy of them, then the ref keypoints
+                assert np.array_equal(_u(tx[:m]), _u(tx[m:2 * m])) and np.array_equal(tb[:m], tb[m:2 * m]), f
+            od.exchange(x, include_self=True)
+            kref = st.n_keypoints
+    finally:
+        od.close()
+        x.close()
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        frames = _frames(seed=42 + rank, n=5)
+        solo = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+        solo_poses = [_u(solo.process(x).pose).copy() for x in frames]
+        solo.close()
+        od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+        ok = True
+        for f, xyz in enumerate(frames):
+            st = od.process(xyz)
+            ok &= np.array_equal(_u(st.pose), solo_poses[f])
+            deltas = [None] * world
+            dist.all_gather_object(deltas, od.map_delta())
+            for r in range(world):
+                od.gpu_replica_insert(r, deltas[r])
+            sizes = [None] * world
+            dist.all_gather_object(sizes, st.map_size)
+            ok &= all(od.gpu_replica_size(r) == sizes[r] for r in range(world))
+            digest = []
+            for r in range(world):
+                xyz_r, bits_r = od.gpu_replica_query(r, np.array([0.0, 800.0 * f, 0.0], np.float32))
+                digest.append(hashlib.sha1(_u(xyz_r).tobytes() + bits_r.tobytes()).hexdigest())
+            digests = [None] * world
+            dist.all_gather_object(digests, digest)
+            ok &= all(d == digests[0] for d in digests)
+        od.close()
+        dist.destroy_process_group()
+        q.put((rank, bool(ok)))
+    except Exception as e:  # reported to the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_identical_replicas_and_solo_poses():
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}, res
