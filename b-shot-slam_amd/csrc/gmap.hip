@@ -196,9 +196,12 @@ __device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long lon
 // one wave per touched block (grid-strides over the device-side segment count)
 __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
                                                     const int* __restrict__ seg, int slot_base) {
-    // 116 KiB of static LDS (one workgroup per CU; the sweep touches ~100 blocks)
-    __shared__ int s_ord[GM_LDS_N], s_pos[GM_LDS_N], s_slot[GM_LDS_N], s_nxt[GM_LDS_N], s_bk[GM_LDS_BK];
-    __shared__ uint64_t s_code[GM_LDS_N];
+    // the block's LDS image (130 KiB, one workgroup per CU; a sweep touches ~100 blocks): list
+    // indices as ushort, hash codes as u32 (10 mm-grid keys), each member's current position + ratio
+    __shared__ unsigned short s_ord[GM_LDS_N], s_pos[GM_LDS_N], s_nxt[GM_LDS_N], s_bk[GM_LDS_BK];
+    __shared__ int s_slot[GM_LDS_N];
+    __shared__ unsigned int s_code[GM_LDS_N];
+    __shared__ float4 s_mem[GM_LDS_N];
     const int lane = lane_id();
     const int nseg = m.ctr[GM_NSEG];
     for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
@@ -208,15 +211,17 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
             if (lane == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
             continue;
         }
-        // stage the block's arrays
+        // stage the block
         for (int i = lane; i < B.n; i += 64) {
-            s_ord[i] = m.ipool[B.ord + i];
-            s_pos[i] = m.ipool[B.pos + i];
-            s_slot[i] = m.ipool[B.mslot + i];
-            s_code[i] = m.cpool[B.code + i];
+            s_ord[i] = (unsigned short)m.ipool[B.ord + i];
+            s_pos[i] = (unsigned short)m.ipool[B.pos + i];
+            const int sl = m.ipool[B.mslot + i];
+            s_slot[i] = sl;
+            s_mem[i] = m.kpos[sl];
+            s_code[i] = (unsigned int)m.cpool[B.code + i];
         }
         if (B.bk >= 0)
-            for (int i = lane; i < B.bkt; i += 64) s_bk[i] = m.ipool[B.bk + i];
+            for (int i = lane; i < B.bkt; i += 64) s_bk[i] = (unsigned short)m.ipool[B.bk + i];
         __syncthreads();
         um::State S{B.n, B.bkt, B.next_resize};
         int added = 0;
@@ -228,7 +233,7 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
             bool rej = false;
             int hit = -1;
             for (int i = lane; i < S.n; i += 64) {
-                const float4 e = m.kpos[s_slot[i]];
+                const float4 e = s_mem[i];
                 const float dx = p.x - e.x, dy = p.y - e.y, dz = p.z - e.z;
                 if (sqrtf(dx * dx + (dy * dy + dz * dz)) < 800.f && p.w <= e.w) rej = true;
                 if (e.x == p.x && e.y == p.y && e.z == p.z) hit = i;
@@ -238,15 +243,18 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
             if (hm) {
                 const int owner = (int)__ffsll((long long)hm) - 1;
                 const int mi = __shfl(hit, owner, 64);
-                if (lane == 0) s_slot[mi] = slot;
+                if (lane == 0) { s_slot[mi] = slot; s_mem[mi] = p; }
                 __syncthreads();
                 continue;
             }
             const int x = S.n;
             int at = 0;
             if (lane == 0) {
+                const unsigned long long code = map_hash(p.x, p.y, p.z);
+                if (code > 0xFFFFFFFFull) atomicOr(&m.ctr[GM_ERR], 8);
                 s_slot[x] = slot;
-                s_code[x] = map_hash(p.x, p.y, p.z);
+                s_mem[x] = p;
+                s_code[x] = (unsigned int)code;
                 int nb;
                 if (um::need_rehash(S, &nb)) um::rehash(S, nb, s_ord, s_pos, s_code, s_bk, s_nxt);
                 at = um::insert_position(S, x, s_ord, s_pos, s_code, s_bk);
@@ -259,13 +267,13 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
             // writes of the chunks before it)
             for (int hi = S.n; hi > at; hi -= 64) {
                 const int i = hi - lane;
-                int v = 0;
+                unsigned short v = 0;
                 if (i > at) v = s_ord[i - 1];
                 __syncthreads();
-                if (i > at) { s_ord[i] = v; s_pos[v] = i; }
+                if (i > at) { s_ord[i] = v; s_pos[v] = (unsigned short)i; }
                 __syncthreads();
             }
-            if (lane == 0) { s_ord[at] = x; s_pos[x] = at; }
+            if (lane == 0) { s_ord[at] = (unsigned short)x; s_pos[x] = (unsigned short)at; }
             __syncthreads();
             S.n += 1;
             ++added;
@@ -301,7 +309,10 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
             m.ipool[B.mslot + i] = s_slot[i];
             m.cpool[B.code + i] = s_code[i];
         }
-        for (int i = lane; i < S.bkt; i += 64) m.ipool[B.bk + i] = s_bk[i];
+        for (int i = lane; i < S.bkt; i += 64) {
+            const unsigned short v = s_bk[i];
+            m.ipool[B.bk + i] = v == (unsigned short)um::UM_EMPTY ? um::UM_EMPTY : (v == (unsigned short)um::UM_BB ? um::UM_BB : (int)v);
+        }
         if (lane == 0) {
             B.n = S.n; B.bkt = S.bkt; B.next_resize = S.next_resize;
             m.blk[b] = B;

@@ -19,6 +19,8 @@
 // iteration order), pos[member] (its index in ord), code[member] (hash code), buckets[bkt] (member id
 // of the bucket's before node, UM_BB for the list head, UM_EMPTY for none). Members are numbered in
 // insertion order (0, 1, ...). Replacing the value of an existing key changes nothing here.
+// The GPU map instantiates the index type as unsigned short and the code type as uint32_t (hash
+// codes of 10 mm-grid keys fit); the CPU check runs both that and the int / uint64 form.
 #pragma once
 #include <stdint.h>
 
@@ -30,6 +32,8 @@
 
 namespace um {
 
+// index arrays (ord, pos, buckets, scratch) may be int or a narrower unsigned type (the GPU map keeps
+// them as ushort in LDS); the two sentinels are the type's all-ones and all-ones-minus-one
 constexpr int UM_EMPTY = -1;
 constexpr int UM_BB = -2;
 
@@ -58,55 +62,61 @@ UM_HD inline bool need_rehash(State& s, int* nb) {
     return true;
 }
 
-// Rehash to nb buckets. nxt: scratch of >= n ints (a singly linked list over member ids).
-UM_HD inline void rehash(State& s, int nb, int* ord, int* pos, const uint64_t* code, int* buckets, int* nxt) {
-    for (int b = 0; b < nb; ++b) buckets[b] = UM_EMPTY;
-    int head = UM_EMPTY, bbegin = 0;
+// Rehash to nb buckets. nxt: scratch of >= n entries (a singly linked list over member ids).
+template <typename I, typename C>
+UM_HD inline void rehash(State& s, int nb, I* ord, I* pos, const C* code, I* buckets, I* nxt) {
+    const I E = (I)UM_EMPTY, BB = (I)UM_BB;
+    for (int b = 0; b < nb; ++b) buckets[b] = E;
+    I head = E;
+    int bbegin = 0;
     for (int i = 0; i < s.n; ++i) {
-        const int p = ord[i];
-        const int b = (int)(code[p] % (uint64_t)nb);
-        if (buckets[b] == UM_EMPTY) {
+        const I p = ord[i];
+        const int b = (int)(code[p] % (C)nb);
+        if (buckets[b] == E) {
             nxt[p] = head;
             head = p;
-            buckets[b] = UM_BB;
-            if (nxt[p] != UM_EMPTY) buckets[bbegin] = p;
+            buckets[b] = BB;
+            if (nxt[p] != E) buckets[bbegin] = p;
             bbegin = b;
-        } else if (buckets[b] == UM_BB) {
+        } else if (buckets[b] == BB) {
             // the bucket's first node is the list head: p goes in front of it
             nxt[p] = head;
             head = p;
         } else {
-            const int before = buckets[b];
+            const I before = buckets[b];
             nxt[p] = nxt[before];
             nxt[before] = p;
         }
     }
     int i = 0;
-    for (int p = head; p != UM_EMPTY; p = nxt[p]) { ord[i] = p; pos[p] = i; ++i; }
+    for (I p = head; p != E; p = nxt[p]) { ord[i] = p; pos[p] = (I)i; ++i; }
     s.bkt = nb;
     s.next_resize = nb;
 }
 
 // list position the new member x takes (and the bucket bookkeeping), before the shift of ord
-UM_HD inline int insert_position(State& s, int x, const int* ord, const int* pos, const uint64_t* code, int* buckets) {
-    const int b = (int)(code[x] % (uint64_t)s.bkt);
-    if (buckets[b] != UM_EMPTY) {
-        const int before = buckets[b];
-        return before == UM_BB ? 0 : pos[before] + 1;
+template <typename I, typename C>
+UM_HD inline int insert_position(State& s, int x, const I* ord, const I* pos, const C* code, I* buckets) {
+    const I E = (I)UM_EMPTY, BB = (I)UM_BB;
+    const int b = (int)(code[x] % (C)s.bkt);
+    if (buckets[b] != E) {
+        const I before = buckets[b];
+        return before == BB ? 0 : (int)pos[before] + 1;
     }
-    if (s.n > 0) buckets[(int)(code[ord[0]] % (uint64_t)s.bkt)] = x;
-    buckets[b] = UM_BB;
+    if (s.n > 0) buckets[(int)(code[ord[0]] % (C)s.bkt)] = (I)x;
+    buckets[b] = BB;
     return 0;
 }
 
 // the whole insert of a new member x (one thread): rehash if due, then link at its bucket's begin
-UM_HD inline void insert(State& s, int x, int* ord, int* pos, const uint64_t* code, int* buckets, int* nxt) {
+template <typename I, typename C>
+UM_HD inline void insert(State& s, int x, I* ord, I* pos, const C* code, I* buckets, I* nxt) {
     int nb;
     if (need_rehash(s, &nb)) rehash(s, nb, ord, pos, code, buckets, nxt);
     const int at = insert_position(s, x, ord, pos, code, buckets);
-    for (int i = s.n; i > at; --i) { ord[i] = ord[i - 1]; pos[ord[i]] = i; }
-    ord[at] = x;
-    pos[x] = at;
+    for (int i = s.n; i > at; --i) { ord[i] = ord[i - 1]; pos[ord[i]] = (I)i; }
+    ord[at] = (I)x;
+    pos[x] = (I)at;
     s.n += 1;
 }
 

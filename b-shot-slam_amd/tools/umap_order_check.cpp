@@ -15,16 +15,16 @@ struct Hasher {  // include/mymap.h MapHasher over the shim's Vector3f (Eigen re
     unsigned long operator()(const myslam::Vector3f& p) const { return (unsigned long)std::fabs(std::round(p.sum())); }
 };
 
-int main(int argc, char** argv) {
-    const int trials = argc > 1 ? atoi(argv[1]) : 200;
-    std::mt19937 rng(7);
+template <typename I, typename C>
+static int run(int trials, unsigned seed) {
+    std::mt19937 rng(seed);
     for (int t = 0; t < trials; ++t) {
         const int target = 1 + (int)(rng() % (t < 20 ? 6000u : 700u));
         const float span = (float)(100 + rng() % 10000);
         std::unordered_map<myslam::Vector3f, int, Hasher> ref;
         std::vector<myslam::Vector3f> keys;
-        std::vector<int> ord, pos, bk, nxt;
-        std::vector<uint64_t> code;
+        std::vector<I> ord, pos, bk, nxt;
+        std::vector<C> code;
         um::State s = um::initial();
         std::uniform_real_distribution<float> U(-span, span);
         for (int i = 0; i < target; ++i) {
@@ -36,7 +36,7 @@ int main(int argc, char** argv) {
             if (!is_new) continue;
             const int x = (int)keys.size();
             keys.push_back(p);
-            code.push_back((uint64_t)Hasher()(p));
+            code.push_back((C)Hasher()(p));
             ord.resize(keys.size());
             pos.resize(keys.size());
             nxt.resize(keys.size());
@@ -60,6 +60,13 @@ int main(int argc, char** argv) {
             }
         }
     }
-    std::printf("umap order: %d trials identical\n", trials);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const int trials = argc > 1 ? atoi(argv[1]) : 200;
+    // int / uint64 (the restatement as written) and ushort / uint32 (the GPU map's LDS image)
+    if (run<int, uint64_t>(trials, 7) || run<unsigned short, uint32_t>(trials, 11)) return 1;
+    std::printf("umap order: %d trials x 2 index types identical\n", trials);
     return 0;
 }
