@@ -9,7 +9,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+# ORACLE_LIB: an alternative build of the restatement (the sanitizer build, oracle/Makefile sanitize)
+ORACLE_LIB = os.environ.get("ORACLE_LIB") or os.path.join(ORACLE_DIR, "build", "liboracle.so")
 P = ctypes.c_void_p
 
 

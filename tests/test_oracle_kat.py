@@ -6,6 +6,9 @@ The reference itself cannot be built in this image (PCL/Eigen/FLANN absent), so 
 independently: FLANN radius-search semantics, the SR ratio formulas, the B-SHOT binarisation
 cascade, first-index Hamming argmin + mutual check, the Jacobi eigen-solver and umeyama.
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -232,3 +235,23 @@ def test_umeyama_recovers_rigid_transform(use_float):
     Re = U @ S @ Vt
     T = orc.umeyama(src, dst, False)
     assert np.allclose(T[:3, :3], Re, atol=1e-10) and np.allclose(T[:3, 3], dm - Re @ sm, atol=1e-7)
+
+
+@pytest.mark.skipif(bool(os.environ.get("ORACLE_LIB")), reason="already running under the sanitizer build")
+def test_oracle_under_sanitizers():
+    """the CPU restatement built with AddressSanitizer + UndefinedBehaviorSanitizer
+    (oracle/Makefile `sanitize`) runs the oracle's CPU tests -- known-answer tests, host checks, the
+    golden fixtures, the preprocessor and capture restatements, the edge frames -- without a report."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "oracle"), "sanitize"])
+    pre = ":".join(subprocess.check_output(["gcc", f"-print-file-name={n}"], text=True).strip()
+                   for n in ("libasan.so", "libubsan.so"))
+    env = dict(os.environ, ORACLE_LIB=os.path.join(root, "oracle", "build", "asan", "liboracle.so"),
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               LD_PRELOAD=pre)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider",
+                        "-k", "oracle_kat or host or golden or edge or preprocess or velodyne",
+                        os.path.join(root, "tests")], env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
