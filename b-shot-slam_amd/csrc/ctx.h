@@ -204,10 +204,9 @@ struct bshot_ctx {
     int opt_pre_fast = 1;  // preprocessor: one 32-bit sort for azimuth-ordered lasers with tabled verticals
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
     int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
-    int opt_icp_tile = 1;  // 1: LDS-tiled NN over target spans (k_icp_tile); 0: wave per source point (k_icp_wave)
     DBuf<unsigned long long> ipart;  // k_icp_tile span minima
     DBuf<unsigned int> icnt;         // k_icp_tile per-block arrival counters
-    int opt_icp_grid = 1;  // 1: exact 1-NN on hashed grids of the targets (k_icp_grid); 0: brute-force passes
+    int opt_icp_grid = 1;  // 1: exact 1-NN on hashed grids of the targets (k_icp_grid); 0: LDS-tiled brute force (k_icp_tile)
     bsh::DevGrid icp_g1, icp_g2;  // ICP target grids (cells 1000 / 5000 mm), built once per ICP call
     int opt_icp_dev = 0;  // 1: ICP loop resident on the device (one sync); 0: host Umeyama per iteration (faster under load)
     DBuf<float> isrc, itgt3;

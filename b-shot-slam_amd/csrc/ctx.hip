@@ -535,32 +535,22 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
         c->stage_end(sg9, st);
         return BSHOT_OK;
     }
-    // plan: sort pieces of <= ~3072 keys per keypoint; 64-rank chunks
-    const int piece = 3072;
-    int n_plan = 0;
+    // host plan (after a device-plan overflow): 64-rank chunks and the LPT launch order
+    const int n_plan = 0;
     long long nch = 0;
-    for (int q = 0; q < k; ++q) {
-        const long long nq = c->p_offs.p[q + 1] - c->p_offs.p[q];
-        if (nq > 0) n_plan += (int)((nq + piece - 1) / piece);
-        nch += (nq + 63) / 64;
-    }
+    for (int q = 0; q < k; ++q) nch += (c->p_offs.p[q + 1] - c->p_offs.p[q] + 63) / 64;
     if (nch > 0x7FFFFFFF) return c->fail("describe: too many neighbourhood chunks", BSHOT_ECAP);
     HIPCHK(c->p_plan.ensure(4 * (size_t)n_plan + 2 * (size_t)k + 1), "alloc pinned plan");
-    int* hp = c->p_plan.p;
-    int* hcb = hp + 4 * (size_t)n_plan;
+    int* hcb = c->p_plan.p;
     int* hperm = hcb + k + 1;
     for (int q = 0; q < k; ++q) hperm[q] = q;
     std::stable_sort(hperm, hperm + k, [&](int x, int y) {
         return c->p_offs.p[x + 1] - c->p_offs.p[x] > c->p_offs.p[y + 1] - c->p_offs.p[y];
     });
-    int w = 0, cbr = 0;
+    int cbr = 0;
     for (int q = 0; q < k; ++q) {
-        const long long nq = c->p_offs.p[q + 1] - c->p_offs.p[q];
         hcb[q] = cbr;
-        cbr += (int)((nq + 63) / 64);
-        if (nq <= 0) continue;
-        const int J = (int)((nq + piece - 1) / piece);
-        for (int j = 0; j < J; ++j, ++w) { hp[4 * w] = q; hp[4 * w + 1] = j; hp[4 * w + 2] = J; hp[4 * w + 3] = 0; }
+        cbr += (int)((c->p_offs.p[q + 1] - c->p_offs.p[q] + 63) / 64);
     }
     hcb[k] = cbr;
     HIPCHK(c->plan.ensure(n_plan > 0 ? n_plan : 1), "alloc plan");
@@ -572,8 +562,6 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->signs.ensure(2 * (size_t)(cbr > 0 ? cbr : 1)), "alloc signs");  // per-chunk sign counts
     HIPCHK(c->recS.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
     HIPCHK(c->recV.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
-    if (n_plan > 0)
-        HIPCHK(hipMemcpyAsync(c->plan.p, hp, sizeof(int4) * n_plan, hipMemcpyHostToDevice, st), "H2D plan");
     HIPCHK(c->perm.ensure(k), "alloc perm");
     HIPCHK(hipMemcpyAsync(c->cb.p, hcb, sizeof(int) * ((size_t)k + 1), hipMemcpyHostToDevice, st), "H2D cb");
     HIPCHK(hipMemcpyAsync(c->perm.p, hperm, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D perm");
@@ -743,7 +731,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             const int mc = std::max(65536, 2 * nt);
             HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true, mc), "icp grid");
             HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false, mc), "icp grid 2");
-        } else if (c->opt_icp_tile) {
+        } else {
             HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
             HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
             HIPCHK(hipMemsetAsync(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
@@ -759,13 +747,9 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                 HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->icp_g1, c->icp_g2,
                                        c->itgt.p, nt, c->p_best.p, c->stream),
                        "icp iteration");
-            else if (c->opt_icp_tile)
+            else
                 HIPCHK(launch_icp_tile(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt,
                                        c->ipart.p, (int)std::min<size_t>(c->ipart.cap, 0x7FFFFFFF), c->icnt.p,
-                                       c->p_best.p, c->stream),
-                       "icp iteration");
-            else
-                HIPCHK(launch_icp_wave(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt,
                                        c->p_best.p, c->stream),
                        "icp iteration");
             c->stage_end(sg14);
@@ -1121,13 +1105,12 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     if (!c || !name) return BSHOT_EINVAL;
     const std::string k(name);
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
-    else if (k == "describe2") c->opt_describe2 = value < 0 ? 0 : (value > 2 ? 2 : value);
+    else if (k == "describe2") c->opt_describe2 = value ? 2 : 0;  // the piece-sort variant (1) is retired
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
-    else if (k == "icp_tile") c->opt_icp_tile = value ? 1 : 0;
     else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;

@@ -2,9 +2,7 @@
 // neighbourhood (up to ~22k points for keypoints near the sensor, ~3x the mean) into fixed-size
 // pieces so no single keypoint bounds a launch. Same arithmetic, same order as describe.hip.
 //
-//   k_sort2       (keypoint, piece) workgroups: each piece owns the d2 buckets whose prefix start
-//                 falls in its share of the segment; bucket-scatter into LDS, exact rank inside the
-//                 bucket, write the sorted (d2, idx) keys
+//   (sorting: k_shot_rank, csrc/describe.hip -- exact rank inside the count pass's d2 buckets)
 //   k_lrf_chunks  wave per 64-rank chunk: 7 weighted-covariance terms by the xor-butterfly tree
 //   k_lrf_eig     thread per keypoint: chunk sums in chunk order, Jacobi eigenvectors
 //   k_lrf_sign    wave per chunk: sign counts for the x/z disambiguation (integer, order-free)
@@ -21,98 +19,6 @@
 #include "kernels.h"
 
 namespace bsk {
-
-#define S2_BUCKETS 1024
-#define S2_CAP 6144
-
-__device__ __forceinline__ int s2_bucket(unsigned long long key, float sc) {
-    const float d2 = __uint_as_float((unsigned)(key >> 32));
-    int bk = (int)(d2 * sc);
-    return bk < 0 ? 0 : (bk > S2_BUCKETS - 1 ? S2_BUCKETS - 1 : bk);
-}
-
-// plan[w] = {q, piece j, pieces J, 0}
-__global__ void __launch_bounds__(256) k_sort2(const int4* __restrict__ plan, const long long* __restrict__ offs,
-                                               float R, const unsigned long long* __restrict__ seg,
-                                               unsigned long long* __restrict__ out, int* __restrict__ err) {
-    __shared__ unsigned int hist[S2_BUCKETS];
-    __shared__ unsigned int pre[S2_BUCKETS];
-    __shared__ unsigned int cur[S2_BUCKETS];
-    __shared__ unsigned int wsum[4];
-    __shared__ int blo, bhi;
-    __shared__ unsigned long long buf[S2_CAP];
-    const int t = threadIdx.x;
-    const int4 pl = plan[blockIdx.x];
-    const int q = pl.x, j = pl.y, J = pl.z;
-    const long long o = offs[q];
-    const int n = (int)(offs[q + 1] - o);
-    if (n <= 0) return;
-    const unsigned long long* a = seg + o;
-    unsigned long long* dst = out + o;
-    const float R2 = (float)((double)R * (double)R);
-    const float sc = (float)S2_BUCKETS / R2;
-    for (int i = t; i < S2_BUCKETS; i += 256) hist[i] = 0;
-    if (t == 0) { blo = S2_BUCKETS; bhi = -1; }
-    __syncthreads();
-    // 8 loads in flight per thread (the segment lives in L2/HBM)
-    for (int i0 = t; i0 < n; i0 += 256 * 8) {
-        unsigned long long kk[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) kk[u] = i0 + 256 * u < n ? a[i0 + 256 * u] : ~0ull;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (kk[u] != ~0ull) atomicAdd(&hist[s2_bucket(kk[u], sc)], 1u);
-    }
-    __syncthreads();
-    // exclusive scan: 4 buckets per thread
-    const unsigned int s4 = hist[4 * t] + hist[4 * t + 1] + hist[4 * t + 2] + hist[4 * t + 3];
-    int tot;
-    const int ex = wave_excl_scan((int)s4, tot);
-    if (lane_id() == 63) wsum[t >> 6] = (unsigned)tot;
-    __syncthreads();
-    unsigned int run = (unsigned)ex;
-    for (int w = 0; w < (t >> 6); ++w) run += wsum[w];
-    const unsigned int lo_cnt = (unsigned)(((long long)j * n) / J), hi_cnt = (unsigned)(((long long)(j + 1) * n) / J);
-    for (int u = 0; u < 4; ++u) {
-        const int b = 4 * t + u;
-        pre[b] = run;
-        if (hist[b] > 0 && run >= lo_cnt && run < hi_cnt) {
-            atomicMin(&blo, b);
-            atomicMax(&bhi, b);
-        }
-        run += hist[b];
-    }
-    __syncthreads();
-    if (bhi < 0) return;  // no bucket starts in this piece (uniform)
-    const unsigned int base = pre[blo], end = pre[bhi] + hist[bhi];
-    if (end - base > S2_CAP) {
-        if (t == 0) atomicOr(err, 8);
-        return;
-    }
-    for (int b = blo + t; b <= bhi; b += 256) cur[b] = pre[b] - base;
-    __syncthreads();
-    for (int i0 = t; i0 < n; i0 += 256 * 8) {
-        unsigned long long kk[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) kk[u] = i0 + 256 * u < n ? a[i0 + 256 * u] : ~0ull;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (kk[u] == ~0ull) continue;
-            const int b = s2_bucket(kk[u], sc);
-            if (b >= blo && b <= bhi) buf[atomicAdd(&cur[b], 1u)] = kk[u];
-        }
-    }
-    __syncthreads();
-    const int m = (int)(end - base);
-    for (int i = t; i < m; i += 256) {
-        const unsigned long long key = buf[i];
-        const int b = s2_bucket(key, sc);
-        const unsigned int s0 = pre[b] - base, c = hist[b];
-        unsigned int rank = 0;
-        for (unsigned int u = 0; u < c; ++u) rank += buf[s0 + u] < key ? 1u : 0u;
-        dst[base + s0 + rank] = key;
-    }
-}
 
 // owner[c] = keypoint of chunk c (block per keypoint)
 __global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restrict__ cb, int* __restrict__ owner) {
@@ -653,21 +559,16 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     int cblocks = (A.n_chunks + 3) / 4;
     if (A.max_blocks > 0 && cblocks > A.max_blocks) cblocks = A.max_blocks;
     if (part == 0) {
-        if (A.bstart) {
-            if (A.n_chunks > 0) {
-                bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
-                if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
-                                            A.max_blocks)))
-                    return e;
-            }
-        } else if (A.n_plan > 0) {
-            bsk::k_sort2<<<A.n_plan, 256, 0, s>>>(A.plan, A.offs, A.R, A.seg, A.sorted, A.err);
+        if (A.n_chunks > 0) {
+            bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
+            if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
+                                        A.max_blocks)))
+                return e;
         }
         return hipGetLastError();
     }
     if (part == 1) {
         if (A.n_chunks > 0) {
-            if (!A.bstart) bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
             bsk::k_lrf_chunks<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.R, A.offs, A.cb, A.owner, A.sorted,
                                                        A.csum);
         }

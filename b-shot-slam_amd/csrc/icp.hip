@@ -18,126 +18,9 @@ using bsh::IcpState;
 // small LDS tile (4 KB): ICP runs on the main stream beside LDS-heavy side-stream kernels
 #define ICP_TILE 256
 
-__global__ void __launch_bounds__(ICP_THREADS) k_icp_nn(const float* __restrict__ src, int ns,
-                                                        const float4* __restrict__ tgt, int nt, int tile,
-                                                        unsigned long long* __restrict__ best) {
-    __shared__ float4 tt[ICP_TILE];
-    const int t = threadIdx.x;
-    const int i = blockIdx.x * ICP_THREADS + t;
-    const int r0 = blockIdx.y * tile, r1 = min(nt, r0 + tile);
-    float qx = 0.f, qy = 0.f, qz = 0.f;
-    if (i < ns) { qx = src[3 * i]; qy = src[3 * i + 1]; qz = src[3 * i + 2]; }
-    unsigned long long m = ~0ull;
-    for (int s0 = r0; s0 < r1; s0 += ICP_TILE) {
-        const int cnt = min(ICP_TILE, r1 - s0);
-        __syncthreads();
-        for (int j = t; j < cnt; j += ICP_THREADS) tt[j] = tgt[s0 + j];
-        __syncthreads();
-        for (int j = 0; j < cnt; ++j) {
-            const float4 p = tt[j];
-            const float d2 = d2_flann(qx, qy, qz, p.x, p.y, p.z);
-            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)(s0 + j);
-            m = key < m ? key : m;
-        }
-    }
-    if (i < ns) atomicMin(&best[i], m);
-}
-
 struct Xf16 {
     float m[16];
 };
-
-// One ICP iteration in one launch: every source point is first moved by the previous iteration's
-// step T (when apply; same float expression as the host's bg::xform), the moved cloud is written
-// to src_out by the blockIdx.y == 0 blocks, the 1-NN keys go to best via atomicMin, and the
-// next iteration's best array is reset -- no separate H2D, fill or transform launches.
-__global__ void __launch_bounds__(ICP_THREADS) k_icp_iter(const float* __restrict__ src_in, float* __restrict__ src_out,
-                                                          Xf16 T, int apply, int ns, const float4* __restrict__ tgt,
-                                                          int nt, int tile, unsigned long long* __restrict__ best,
-                                                          unsigned long long* __restrict__ best_next) {
-    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
-    __shared__ float4 tt[ICP_TILE];
-    const int t = threadIdx.x;
-    const int i = blockIdx.x * ICP_THREADS + t;
-    const int r0 = blockIdx.y * tile, r1 = min(nt, r0 + tile);
-    float qx = 0.f, qy = 0.f, qz = 0.f;
-    if (i < ns) {
-        const float x = src_in[3 * i], y = src_in[3 * i + 1], z = src_in[3 * i + 2];
-        if (apply) {
-            qx = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
-            qy = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
-            qz = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
-        } else {
-            qx = x; qy = y; qz = z;
-        }
-        if (blockIdx.y == 0) {
-            src_out[3 * i] = qx; src_out[3 * i + 1] = qy; src_out[3 * i + 2] = qz;
-            best_next[i] = ~0ull;
-        }
-    }
-    unsigned long long m = ~0ull;
-    for (int s0 = r0; s0 < r1; s0 += ICP_TILE) {
-        const int cnt = min(ICP_TILE, r1 - s0);
-        __syncthreads();
-        for (int j = t; j < cnt; j += ICP_THREADS) tt[j] = tgt[s0 + j];
-        __syncthreads();
-        for (int j = 0; j < cnt; ++j) {
-            const float4 p = tt[j];
-            const float d2 = d2_flann(qx, qy, qz, p.x, p.y, p.z);
-            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)(s0 + j);
-            m = key < m ? key : m;
-        }
-    }
-    if (i < ns) atomicMin(&best[i], m);
-}
-
-// One ICP iteration, wave per source point: the previous step T is applied (same float expression
-// as the host's bg::xform; the moved point goes to src_out), the 64 lanes stride over the targets
-// with 4 float4 loads in flight, and the packed (d2 bits << 32 | target index) minimum is reduced
-// in the wave and stored by lane 0 straight into best_out, which may be pinned host memory: no
-// atomics, no reset of a best array and no device-to-host copy between the iterations.
-__global__ void __launch_bounds__(256) k_icp_wave(const float* __restrict__ src_in, float* __restrict__ src_out,
-                                                  Xf16 T, int apply, int ns, const float* __restrict__ tgt, int nt,
-                                                  unsigned long long* __restrict__ best_out) {
-    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
-    const int lane = lane_id();
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= ns) return;
-    const float x = src_in[3 * i], y = src_in[3 * i + 1], z = src_in[3 * i + 2];
-    float qx = x, qy = y, qz = z;
-    if (apply) {
-        qx = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
-        qy = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
-        qz = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
-    }
-    if (lane == 0) {
-        src_out[3 * i] = qx; src_out[3 * i + 1] = qy; src_out[3 * i + 2] = qz;
-    }
-    unsigned long long m = ~0ull;
-    int j = lane;
-    for (; j + 192 < nt; j += 256) {
-        float p[4][3];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float* t3 = tgt + 3 * (size_t)(j + 64 * u);
-            p[u][0] = t3[0]; p[u][1] = t3[1]; p[u][2] = t3[2];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float d2 = d2_flann(qx, qy, qz, p[u][0], p[u][1], p[u][2]);
-            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)(j + 64 * u);
-            m = key < m ? key : m;
-        }
-    }
-    for (; j < nt; j += 64) {
-        const float* t3 = tgt + 3 * (size_t)j;
-        const float d2 = d2_flann(qx, qy, qz, t3[0], t3[1], t3[2]);
-        const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)j;
-        m = key < m ? key : m;
-    }
-    m = wave_min_u64(m);
-    if (lane == 0) best_out[i] = m;
-}
 
 // One ICP iteration, LDS-tiled: a workgroup holds 256 source points (a thread each) and one
 // contiguous span of the targets (blockIdx.y), streamed through LDS in tiles of 512 float4 that
@@ -480,43 +363,6 @@ hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t 
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     bsk::k_gather<<<(k + 255) / 256, 256, 0, s>>>(pts4, idx, k, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_icp_nn(const float* src, int ns, const float4* tgt, int nt, unsigned long long* best, hipStream_t s) {
-    if (ns <= 0 || nt <= 0) return hipSuccess;
-    bsk::k_fill_u64b<<<(ns + 255) / 256, 256, 0, s>>>(best, ns, ~0ull);
-    const int qb = (ns + ICP_THREADS - 1) / ICP_THREADS;
-    int splits = (1024 + qb - 1) / qb;
-    int tile = (nt + splits - 1) / splits;
-    if (tile < 256) tile = 256;
-    splits = (nt + tile - 1) / tile;
-    dim3 grid(qb, splits);
-    bsk::k_icp_nn<<<grid, ICP_THREADS, 0, s>>>(src, ns, tgt, nt, tile, best);
-    return hipGetLastError();
-}
-
-hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,
-                           int nt, unsigned long long* best, unsigned long long* best_next, hipStream_t s) {
-    if (ns <= 0 || nt <= 0) return hipSuccess;
-    const int qb = (ns + ICP_THREADS - 1) / ICP_THREADS;
-    int splits = (1024 + qb - 1) / qb;
-    int tile = (nt + splits - 1) / splits;
-    if (tile < 256) tile = 256;
-    splits = (nt + tile - 1) / tile;
-    bsk::Xf16 T;
-    for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
-    bsk::k_icp_iter<<<dim3(qb, splits), ICP_THREADS, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, tile, best,
-                                                              best_next);
-    return hipGetLastError();
-}
-
-hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
-                           int nt, unsigned long long* best_out, hipStream_t s) {
-    if (ns <= 0 || nt <= 0) return hipSuccess;
-    bsk::Xf16 T;
-    for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
-    bsk::k_icp_wave<<<(ns + 3) / 4, 256, 0, s>>>(src_in, src_out, T, apply, ns, tgt, nt, best_out);
     return hipGetLastError();
 }
 

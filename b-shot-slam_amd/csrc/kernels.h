@@ -44,7 +44,6 @@ hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, in
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
-// wave per source point, results stored straight to best_out (may be pinned host memory)
 // LDS-tiled NN pass over target spans (k_icp_tile); part: icp_tile_splits(ns, nt) x ns keys, cnt:
 // ceil(ns / 256) zeroed counters
 int icp_tile_splits(int ns, int nt);
@@ -54,10 +53,6 @@ hipError_t launch_icp_tile(const float* src_in, float* src_out, const float* T16
 // exact 1-NN on two hashed grids of the targets (cells r1 < r2; k_icp_grid), brute force past them
 hipError_t launch_icp_grid(const float* src_in, float* src_out, const float* T16, int apply, int ns, const DevGrid& g1,
                            const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best_out, hipStream_t s);
-hipError_t launch_icp_wave(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
-                           int nt, unsigned long long* best_out, hipStream_t s);
-hipError_t launch_icp_iter(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float4* tgt,
-                           int nt, unsigned long long* best, unsigned long long* best_next, hipStream_t s);
 // device-resident ICP loop state (ctx_icp with opt icp_dev): step T, accumulated fin, PCL
 // convergence bookkeeping
 struct IcpState {
@@ -69,8 +64,6 @@ struct IcpState {
 // one (NN, update) iteration pair; no-ops once st->done
 hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int ns, const float4* tgt, int nt,
                           unsigned long long* best, unsigned long long* best_next, hipStream_t s);
-hipError_t launch_icp_nn(const float* src, int ns, const float4* tgt, int nt, unsigned long long* best, hipStream_t s);
-
 // load-balanced SHOT (describe2.hip): sort pieces, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;

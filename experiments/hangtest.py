@@ -4,7 +4,7 @@ import os
 import sys
 
 faulthandler.dump_traceback_later(int(os.environ.get("HT_TIMEOUT", "60")), exit=True)
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "b-shot-slam_amd"))
 import bshot_py  # noqa: E402
 
 pc, _ = bshot_py.synth_sweep(3)

@@ -4,7 +4,7 @@ import os
 import sys
 
 faulthandler.dump_traceback_later(int(os.environ.get("HT_TIMEOUT", "40")), exit=True)
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "b-shot-slam_amd"))
 import numpy as np  # noqa: E402
 
 import bshot_py  # noqa: E402

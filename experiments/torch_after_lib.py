@@ -3,7 +3,7 @@ usage: python torch_after_lib.py {ctx|ctx_nodestroy|odo|sr}"""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "b-shot-slam_amd"))
 import bshot_py  # noqa: E402
 
 mode = sys.argv[1]

@@ -71,7 +71,7 @@ def test_odometry_no_icp_no_iss():
 
 
 @pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"queue_thread": 1}), (2, {"topk_thread": 0}),
-                                        (2, {"icp_grid": 0, "icp_tile": 0, "ransac_dev": 0}),
+                                        (2, {"icp_grid": 0, "ransac_dev": 0}),
                                         (2, {"icp_grid": 0})])
 def test_odometry_lookahead_device_frames(depth, opts):
     """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
