@@ -127,6 +127,8 @@ struct bshot_ctx {
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
     int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
+    int opt_sr_tile = 0;        // SR cell tiles: ladder level of a tile's cell (0: one query per wave; tiled measured slower)
+    int opt_sr_tile_q = 128;    // tiled SR: queries a workgroup takes before it retires
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
     int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)

@@ -225,7 +225,8 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks),
+                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks, c->opt_sr_tile,
+                                c->opt_sr_tile_q),
                "seg_ratio launch");
         c->stage_end(sg2, st);
         HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
@@ -1110,6 +1111,8 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
+    else if (k == "sr_tile") c->opt_sr_tile = value < 0 ? 0 : (value > 3 ? 3 : value);
+    else if (k == "sr_tile_q") c->opt_sr_tile_q = value < 64 ? 64 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);

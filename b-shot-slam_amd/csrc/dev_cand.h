@@ -16,7 +16,9 @@
 
 namespace bsk {
 
+#ifndef CAND_GROUP
 #define CAND_GROUP 4
+#endif
 
 struct CandLds {
     int mark[64 * CAND_GROUP];

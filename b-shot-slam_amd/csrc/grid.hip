@@ -70,14 +70,16 @@ __global__ void k_grid_cells(const unsigned long long* __restrict__ keys, const 
 // ---- nested ladder grids (cells c, 2c, 4c, 8c) from ONE sort -------------------------------
 // floor(x / (2^L c)) == floor(x / c) >> L exactly (division by a power of two commutes with the
 // double rounding), so a level-L cell is a prefix of the hierarchical key
-//   (16-bit biased level-3 x, y, z) | level-2 child bits | level-1 child bits | level-0 child bits
-// and points sorted by that key are contiguous per cell at every level.
+//   (18-bit biased level-3 x, y, z) | level-2 child bits | level-1 child bits | level-0 child bits
+// (63 bits; the radix sort's 8 passes are those of any key over 56 bits) and points sorted by that
+// key are contiguous per cell at every level. The level-0 range |ix| < 2^20 is that of cell_key, so
+// every grid of the ladder indexes the same points (+-196 km per axis at c0 = 187.5 mm).
 __device__ __forceinline__ bool ladder_cells(float x, float y, float z, float c0, int& ix, int& iy, int& iz) {
     if (!(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z))) return false;
     ix = cell_of(x, c0);
     iy = cell_of(y, c0);
     iz = cell_of(z, c0);
-    const int lim = (1 << 15) << 3;  // level-3 coordinate must fit 16 bits biased
+    const int lim = 1 << 20;  // cell_key's level-0 range; level-3 coordinate fits 18 bits biased
     return ix > -lim && ix < lim && iy > -lim && iy < lim && iz > -lim && iz < lim;
 }
 
@@ -90,9 +92,9 @@ __global__ void k_ladder_keys(const float* __restrict__ xyz, int n, float c0, un
     unsigned long long k = BS_EMPTY_KEY;
     int ix, iy, iz;
     if (ladder_cells(x, y, z, c0, ix, iy, iz)) {
-        const unsigned long long x3 = (unsigned)((ix >> 3) + (1 << 15)), y3 = (unsigned)((iy >> 3) + (1 << 15)),
-                                 z3 = (unsigned)((iz >> 3) + (1 << 15));
-        k = (x3 << 41) | (y3 << 25) | (z3 << 9);
+        const unsigned long long x3 = (unsigned)((ix >> 3) + (1 << 17)), y3 = (unsigned)((iy >> 3) + (1 << 17)),
+                                 z3 = (unsigned)((iz >> 3) + (1 << 17));
+        k = (x3 << 45) | (y3 << 27) | (z3 << 9);
 #pragma unroll
         for (int L = 2; L >= 0; --L) {
             const unsigned cbits = (unsigned)((((ix >> L) & 1) << 2) | (((iy >> L) & 1) << 1) | ((iz >> L) & 1));
@@ -146,7 +148,7 @@ static unsigned int pow2_at_least(unsigned int x) {
     return p;
 }
 
-// g[0..3]: grids of cell c0, 2 c0, 4 c0, 8 c0 built from one 57-bit radix sort; g[0] owns the
+// g[0..3]: grids of cell c0, 2 c0, 4 c0, 8 c0 built from one 63-bit radix sort; g[0] owns the
 // sort buffers and the cell-sorted points, g[1..3] own only their hash tables and alias g[0].spts
 hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s) {
     hipError_t e;
@@ -161,8 +163,10 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
         if ((e = hipMalloc(&g0.vals, sizeof(unsigned int) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.vals2, sizeof(unsigned int) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.spts, sizeof(float4) * g0.cap))) return e;
+        if ((e = hipMalloc(&g0.tiles, sizeof(int2) * g0.cap))) return e;
+        if ((e = hipMalloc(&g0.tctr, sizeof(int) * 2))) return e;
         size_t tb = 0;
-        if ((e = rocprim::radix_sort_pairs(nullptr, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)g0.cap, 0, 57,
+        if ((e = rocprim::radix_sort_pairs(nullptr, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)g0.cap, 0, 63,
                                            s)))
             return e;
         g0.tmp_bytes = tb;
@@ -181,7 +185,7 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
     const int B = 256;
     bsk::k_ladder_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, c0, g0.keys, g0.vals, d_pts4);
     size_t tb = g0.tmp_bytes;
-    if ((e = rocprim::radix_sort_pairs(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 57, s)))
+    if ((e = rocprim::radix_sort_pairs(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 63, s)))
         return e;
     for (int L = 0; L < 4; ++L) {
         DevGrid& gl = *gp[L];
@@ -234,6 +238,8 @@ void grid_free(DevGrid& g) {
     if (g.spts) (void)hipFree(g.spts);
     if (g.table) (void)hipFree(g.table);
     if (g.ncells) (void)hipFree(g.ncells);
+    if (g.tiles) (void)hipFree(g.tiles);
+    if (g.tctr) (void)hipFree(g.tctr);
     if (g.tmp) (void)hipFree(g.tmp);
     g = DevGrid();
 }

@@ -145,9 +145,14 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
     // itself (PCL usually stops within a few dozen), then the rest of the stream is drawn and the
     // GPU scores it in one launch (identical counts: same float expression,
     // tests/test_parity_gpu.py::test_ransac_dev_matches_host)
-    const int host_max = ctx ? std::max(8, 24000 / std::max(1, nidx)) : max_iter + 1;
+    // The GPU launch goes out first (asynchronously) and the host scores the first hypotheses while
+    // it runs; the scan waits for the GPU counts only if PCL's adaptive loop outlasts the host share.
+    // (A loop that ends early leaves the launch unread; the next RANSAC reuses its buffers only
+    // after later syncs on the same stream.)
+    const int host_max = ctx ? std::max(8, 4000 / std::max(1, nidx)) : max_iter + 1;
     const int* gcnt = nullptr;
-    auto gpu_scores = [&]() -> int {
+    bool gpu_launched = false;
+    auto gpu_launch = [&]() -> int {
         bshot_ctx* c = ctx;
         const int nhyp = draw_until(max_iter + 1);
         if (nhyp <= 0) return BSHOT_OK;
@@ -166,10 +171,19 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
             hipMemcpyAsync(c->p_rcnt.p, c->rcnt.p, sizeof(int) * nhyp, hipMemcpyDeviceToHost, c->stream))
             return c->fail("ransac: launch", BSHOT_EHIP);
         c->stage_end(sg);
-        if (hipStreamSynchronize(c->stream)) return c->fail("ransac: sync", BSHOT_EHIP);
-        gcnt = c->p_rcnt.p;
+        gpu_launched = true;
         return BSHOT_OK;
     };
+    auto gpu_scores = [&]() -> int {
+        if (!gpu_launched) return BSHOT_OK;  // empty stream
+        if (hipStreamSynchronize(ctx->stream)) return ctx->fail("ransac: sync", BSHOT_EHIP);
+        gcnt = ctx->p_rcnt.p;
+        return BSHOT_OK;
+    };
+    if (ctx) {
+        const int e = gpu_launch();
+        if (e) return e;
+    }
 
     // ---- phase 2: RandomSampleConsensus::computeModel acceptance scan
     const double log_prob = std::log(1.0 - 0.99);

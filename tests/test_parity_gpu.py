@@ -44,6 +44,48 @@ def test_seg_ratio_bit_exact(ctx, cloud, sr_ref, ladder):
     ctx.set_option("ladder_grids", 4)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 0])
+def test_seg_ratio_tiles_bit_exact(ctx, cloud, sr_ref, tile):
+    """Cell-tiled SR (tiles = runs of one ladder level-`tile` cell; 0 = one query per wave, the default)."""
+    ctx.set_option("sr_tile", tile)
+    ctx.set_cloud(cloud)
+    idx, rat = ctx.seg_ratio()
+    ctx.set_option("sr_tile", 0)
+    ridx, rrat = sr_ref
+    np.testing.assert_array_equal(idx, ridx)
+    np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32))
+
+
+def _edge_cloud():
+    """Sparse far points, a dense clump whose neighbourhoods overflow the LDS stage (> 2048
+    candidates: the per-query fallback), exact duplicates, origin points, NaN/inf rows and points
+    beyond the ladder keys' range (no grid cell: ratio NaN)."""
+    rng = np.random.default_rng(11)
+    far = rng.uniform(-90000, 90000, (3000, 3))
+    clump = np.array([2000.0, -1000.0, 300.0]) + rng.normal(0, 250, (6000, 3))
+    plane = np.stack([rng.uniform(-8000, 8000, 20000), rng.uniform(-8000, 8000, 20000), np.full(20000, -1800.0)], 1)
+    dup = clump[:40]
+    bad = np.array([[np.nan, 0, 0], [0, np.inf, 0], [0, 0, -np.inf], [6e7, 0, 0], [0, -6e7, 100]])
+    xyz = np.concatenate([far, clump, plane, dup, np.zeros((5, 3)), bad]).astype(np.float32)
+    return xyz[rng.permutation(len(xyz))]
+
+
+@pytest.mark.parametrize("sr_type", [0, 1, 2])
+def test_seg_ratio_tiles_edge_cases(sr_type):
+    xyz = _edge_cloud()
+    ridx, rrat = orc.seg_ratio(xyz, sr_type=sr_type)
+    c = bshot_py.Context(0, bshot_py.default_params(sr_type=sr_type))
+    try:
+        for tile in (1, 3, 0):
+            c.set_option("sr_tile", tile)
+            c.set_cloud(xyz)
+            idx, rat = c.seg_ratio()
+            np.testing.assert_array_equal(idx, ridx, err_msg=f"tile {tile}")
+            np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32), err_msg=f"tile {tile}")
+    finally:
+        c.close()
+
+
 def test_topk_keypoints_exact(sr_ref):
     ridx, rrat = sr_ref
     for k in (600, 2048):
