@@ -690,7 +690,14 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             HIPCHK(hipMemcpyAsync(c->isrc.p, d_src0, sizeof(float) * 3 * ns, hipMemcpyDeviceToDevice, c->stream),
                    "icp src");
             HIPCHK(hipMemsetAsync(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
-            HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
+            const bool use_grid = c->opt_icp_grid != 0;
+            if (use_grid) {
+                const int mc = std::max(65536, 2 * nt);
+                HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true, mc), "icp grid");
+                HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false, mc), "icp grid 2");
+            } else {
+                HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
+            }
             // max_iter (NN, update) pairs queued at once; converged iterations return immediately
             HIPCHK(c->istate.ensure(1), "alloc icp state");
             HIPCHK(c->p_istate.ensure(1), "alloc pinned icp state");
@@ -709,10 +716,16 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             const int n_it = max_iter > 1 ? max_iter : 1;
             for (int j = 0; j < n_it; ++j) {
                 const int b = j & 1;
-                HIPCHK(launch_icp_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
-                                      c->istate.p, ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b,
-                                      c->ibest.p + (size_t)ns * (b ^ 1), c->stream),
-                       "icp iteration");
+                if (use_grid)
+                    HIPCHK(launch_icp_grid_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
+                                               c->istate.p, ns, c->icp_g1, c->icp_g2, c->itgt.p, nt, c->ibest.p,
+                                               c->stream),
+                           "icp iteration");
+                else
+                    HIPCHK(launch_icp_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
+                                          c->istate.p, ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b,
+                                          c->ibest.p + (size_t)ns * (b ^ 1), c->stream),
+                           "icp iteration");
             }
             c->stage_end(sg14);
             HIPCHK(hipMemcpyAsync(c->p_istate.p, c->istate.p, sizeof(IcpState), hipMemcpyDeviceToHost, c->stream),

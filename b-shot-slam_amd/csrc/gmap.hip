@@ -193,26 +193,38 @@ __device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long lon
     return true;
 }
 
-// one wave per touched block (grid-strides over the device-side segment count)
-__global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
-                                                    const int* __restrict__ seg, int slot_base) {
-    // the block's LDS image (130 KiB, one workgroup per CU; a sweep touches ~100 blocks): list
-    // indices as ushort, hash codes as u32 (10 mm-grid keys), each member's current position + ratio
+// one workgroup per touched block (grid-strides over the device-side segment count). A batch's
+// candidates are first tested against the block's members as staged (all pairs, in parallel):
+// members are never removed and their ratios only change through an exact-position replacement,
+// so until the batch makes one, a candidate is rejected exactly when a staged member or a member
+// the batch has added so far rejects it. The candidates then go in sweep order: the added members
+// are tested, the insert position is found (lane 0, um::) and the bucket-order list is shifted by
+// the whole workgroup. After a replacement the remaining candidates are tested against every member.
+#define GM_INS_T 512
+__global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
+                                                          const int* __restrict__ seg, int slot_base) {
+    // the block's LDS image (142 KiB, one workgroup per CU; a sweep touches ~100 blocks): list
+    // indices as ushort, hash codes as u32 (10 mm-grid keys), each member's current position + ratio,
+    // and the batch's per-candidate results against the staged members
     __shared__ unsigned short s_ord[GM_LDS_N], s_pos[GM_LDS_N], s_nxt[GM_LDS_N], s_bk[GM_LDS_BK];
     __shared__ int s_slot[GM_LDS_N];
     __shared__ unsigned int s_code[GM_LDS_N];
     __shared__ float4 s_mem[GM_LDS_N];
-    const int lane = lane_id();
+    __shared__ unsigned short s_hit0[GM_LDS_N];  // staged member at the candidate's position (0xFFFF: none)
+    __shared__ unsigned char s_rej0[GM_LDS_N];   // rejected by a staged member
+    __shared__ int s_rej, s_hit, s_at, s_nb, s_nr;
+    __shared__ GBlock s_B;
+    const int tid = threadIdx.x;
     const int nseg = m.ctr[GM_NSEG];
     for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
         const int j0 = seg[3 * sg], cnt = seg[3 * sg + 1], b = seg[3 * sg + 2];
         GBlock B = m.blk[b];
         if (B.n + cnt > GM_LDS_N) {
-            if (lane == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
+            if (tid == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
             continue;
         }
         // stage the block
-        for (int i = lane; i < B.n; i += 64) {
+        for (int i = tid; i < B.n; i += GM_INS_T) {
             s_ord[i] = (unsigned short)m.ipool[B.ord + i];
             s_pos[i] = (unsigned short)m.ipool[B.pos + i];
             const int sl = m.ipool[B.mslot + i];
@@ -221,35 +233,73 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
             s_code[i] = (unsigned int)m.cpool[B.code + i];
         }
         if (B.bk >= 0)
-            for (int i = lane; i < B.bkt; i += 64) s_bk[i] = (unsigned short)m.ipool[B.bk + i];
+            for (int i = tid; i < B.bkt; i += GM_INS_T) s_bk[i] = (unsigned short)m.ipool[B.bk + i];
+        for (int t = tid; t < cnt; t += GM_INS_T) {
+            s_hit0[t] = 0xFFFF;
+            s_rej0[t] = 0;
+        }
+        __syncthreads();
+        // src/mymap.cpp:14-22: rejected when a keypoint of the block within 800 mm has a
+        // segmentation ratio >= this one's; an exact key hit is the entry operator[] replaces.
+        // Threads = C candidates (their loads all in flight) x R member ranges, members read from LDS.
+        const int S0 = B.n;
+        {
+            const int C = cnt < GM_INS_T ? cnt : GM_INS_T, R = GM_INS_T / C;
+            const int part = tid / C, tc = tid - part * C;
+            const int span = (S0 + R - 1) / R, i0 = part * span, i1 = min(S0, i0 + span);
+            if (part < R && i0 < i1)
+                for (int t = tc; t < cnt; t += C) {
+                    const float4 p = m.kpos[slot_base + (int)vals[j0 + t]];
+                    bool r = false;
+                    int h = -1;
+                    for (int i = i0; i < i1; ++i) {
+                        const float4 e = s_mem[i];
+                        const float dx = p.x - e.x, dy = p.y - e.y, dz = p.z - e.z;
+                        r = r || (sqrtf(dx * dx + (dy * dy + dz * dz)) < 800.f && p.w <= e.w);
+                        if (e.x == p.x && e.y == p.y && e.z == p.z) h = i;  // members are unique
+                    }
+                    if (r) s_rej0[t] = 1;
+                    if (h >= 0) s_hit0[t] = (unsigned short)h;
+                }
+        }
         __syncthreads();
         um::State S{B.n, B.bkt, B.next_resize};
         int added = 0;
+        bool exact = false;  // a replacement changed a staged member's ratio: full scans from here on
         for (int t = 0; t < cnt; ++t) {
+            if (!exact && s_rej0[t]) continue;  // rejected by a staged member
             const int slot = slot_base + (int)vals[j0 + t];
             const float4 p = m.kpos[slot];
-            // src/mymap.cpp:14-22: rejected when a keypoint of the block within 800 mm has a
-            // segmentation ratio >= this one's; an exact key hit is the entry operator[] replaces
+            const int lo = exact ? 0 : S0;  // members to test now
             bool rej = false;
-            int hit = -1;
-            for (int i = lane; i < S.n; i += 64) {
-                const float4 e = s_mem[i];
-                const float dx = p.x - e.x, dy = p.y - e.y, dz = p.z - e.z;
-                if (sqrtf(dx * dx + (dy * dy + dz * dz)) < 800.f && p.w <= e.w) rej = true;
-                if (e.x == p.x && e.y == p.y && e.z == p.z) hit = i;
+            int hit = (!exact && s_hit0[t] != 0xFFFF) ? (int)s_hit0[t] : -1;
+            if (!rej && S.n > lo) {
+                if (tid == 0) { s_rej = 0; s_hit = 0x7FFFFFFF; }
+                __syncthreads();
+                bool r = false;
+                int h = 0x7FFFFFFF;
+                for (int i = lo + tid; i < S.n; i += GM_INS_T) {
+                    const float4 e = s_mem[i];
+                    const float dx = p.x - e.x, dy = p.y - e.y, dz = p.z - e.z;
+                    if (sqrtf(dx * dx + (dy * dy + dz * dz)) < 800.f && p.w <= e.w) r = true;
+                    if (e.x == p.x && e.y == p.y && e.z == p.z) h = i;
+                }
+                if (r) s_rej = 1;
+                if (h != 0x7FFFFFFF) atomicMin(&s_hit, h);
+                __syncthreads();
+                rej = s_rej != 0;
+                if (s_hit != 0x7FFFFFFF) hit = s_hit;
+                __syncthreads();  // s_rej / s_hit are rewritten by the next candidate
             }
-            if (__ballot(rej)) continue;
-            const unsigned long long hm = __ballot(hit >= 0);
-            if (hm) {
-                const int owner = (int)__ffsll((long long)hm) - 1;
-                const int mi = __shfl(hit, owner, 64);
-                if (lane == 0) { s_slot[mi] = slot; s_mem[mi] = p; }
+            if (rej) continue;
+            if (hit >= 0) {
+                if (tid == 0) { s_slot[hit] = slot; s_mem[hit] = p; }
+                exact = true;
                 __syncthreads();
                 continue;
             }
             const int x = S.n;
-            int at = 0;
-            if (lane == 0) {
+            if (tid == 0) {
                 const unsigned long long code = map_hash(p.x, p.y, p.z);
                 if (code > 0xFFFFFFFFull) atomicOr(&m.ctr[GM_ERR], 8);
                 s_slot[x] = slot;
@@ -257,31 +307,33 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
                 s_code[x] = (unsigned int)code;
                 int nb;
                 if (um::need_rehash(S, &nb)) um::rehash(S, nb, s_ord, s_pos, s_code, s_bk, s_nxt);
-                at = um::insert_position(S, x, s_ord, s_pos, s_code, s_bk);
+                s_at = um::insert_position(S, x, s_ord, s_pos, s_code, s_bk);
+                s_nb = S.bkt;
+                s_nr = S.next_resize;
             }
-            at = __shfl(at, 0, 64);
-            S.bkt = __shfl(S.bkt, 0, 64);
-            S.next_resize = __shfl(S.next_resize, 0, 64);
             __syncthreads();
+            const int at = s_at;
+            S.bkt = s_nb;
+            S.next_resize = s_nr;
             // shift ord[at, n) one place up, top chunk first (reads of a chunk never overlap the
             // writes of the chunks before it)
-            for (int hi = S.n; hi > at; hi -= 64) {
-                const int i = hi - lane;
+            for (int hi = S.n; hi > at; hi -= GM_INS_T) {
+                const int i = hi - tid;
                 unsigned short v = 0;
                 if (i > at) v = s_ord[i - 1];
                 __syncthreads();
                 if (i > at) { s_ord[i] = v; s_pos[v] = (unsigned short)i; }
                 __syncthreads();
             }
-            if (lane == 0) { s_ord[at] = (unsigned short)x; s_pos[x] = (unsigned short)at; }
+            if (tid == 0) { s_ord[at] = (unsigned short)x; s_pos[x] = (unsigned short)at; }
             __syncthreads();
             S.n += 1;
             ++added;
         }
         // write the block back (arrays regrow by doubling)
-        long long off = 0;
-        bool ok = true;
-        if (lane == 0) {
+        if (tid == 0) {
+            long long off = 0;
+            bool ok = true;
             if (S.n > B.cap) {
                 const int nc = std::max(16, std::max(S.n, 2 * B.cap));
                 long long io = 0, co = 0;
@@ -297,26 +349,27 @@ __global__ void __launch_bounds__(64) k_gmap_insert(GMapDev m, const unsigned in
                 ok = pool_alloc(&m.ctr[GM_ITOP], m.ipool_cap, S.bkt, &m.ctr[GM_ERR], &off);
                 if (ok) { B.bk = (int)off; B.bk_cap = S.bkt; }
             }
+            s_rej = ok ? 1 : 0;
+            if (ok) {
+                B.n = S.n; B.bkt = S.bkt; B.next_resize = S.next_resize;
+                m.blk[b] = B;
+                s_B = B;
+                if (added) atomicAdd(&m.ctr[GM_MEMBERS], added);
+            }
         }
-        ok = __shfl((int)ok, 0, 64) != 0;
-        B.cap = __shfl(B.cap, 0, 64);
-        B.ord = __shfl(B.ord, 0, 64); B.pos = __shfl(B.pos, 0, 64); B.mslot = __shfl(B.mslot, 0, 64);
-        B.code = __shfl(B.code, 0, 64); B.bk = __shfl(B.bk, 0, 64); B.bk_cap = __shfl(B.bk_cap, 0, 64);
-        if (!ok) continue;
-        for (int i = lane; i < S.n; i += 64) {
-            m.ipool[B.ord + i] = s_ord[i];
-            m.ipool[B.pos + i] = s_pos[i];
-            m.ipool[B.mslot + i] = s_slot[i];
-            m.cpool[B.code + i] = s_code[i];
-        }
-        for (int i = lane; i < S.bkt; i += 64) {
-            const unsigned short v = s_bk[i];
-            m.ipool[B.bk + i] = v == (unsigned short)um::UM_EMPTY ? um::UM_EMPTY : (v == (unsigned short)um::UM_BB ? um::UM_BB : (int)v);
-        }
-        if (lane == 0) {
-            B.n = S.n; B.bkt = S.bkt; B.next_resize = S.next_resize;
-            m.blk[b] = B;
-            if (added) atomicAdd(&m.ctr[GM_MEMBERS], added);
+        __syncthreads();
+        if (s_rej) {
+            const GBlock Bw = s_B;
+            for (int i = tid; i < S.n; i += GM_INS_T) {
+                m.ipool[Bw.ord + i] = s_ord[i];
+                m.ipool[Bw.pos + i] = s_pos[i];
+                m.ipool[Bw.mslot + i] = s_slot[i];
+                m.cpool[Bw.code + i] = s_code[i];
+            }
+            for (int i = tid; i < S.bkt; i += GM_INS_T) {
+                const unsigned short v = s_bk[i];
+                m.ipool[Bw.bk + i] = v == (unsigned short)um::UM_EMPTY ? um::UM_EMPTY : (v == (unsigned short)um::UM_BB ? um::UM_BB : (int)v);
+            }
         }
         __syncthreads();
     }
@@ -537,7 +590,7 @@ static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync) {
                                      c->stream), "gmap sort");
     HIPCHK(hipMemsetAsync(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
     bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, c->stream>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
-    bsk::k_gmap_insert<<<std::min(k, 1024), 64, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
+    bsk::k_gmap_insert<<<std::min(k, 1024), GM_INS_T, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
     HIPCHK(hipGetLastError(), "gmap insert launch");
     g.slots += k;
     HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");

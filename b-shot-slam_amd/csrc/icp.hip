@@ -113,8 +113,17 @@ __global__ void __launch_bounds__(256) k_icp_tile(const float* __restrict__ src_
 __global__ void __launch_bounds__(64 * ICPG_WAVES) k_icp_grid(const float* __restrict__ src_in, float* __restrict__ src_out,
                                                               Xf16 T, int apply, int ns, GridView g1, GridView g2,
                                                               float r1, float r2, const float4* __restrict__ tgt4, int nt,
-                                                              unsigned long long* __restrict__ best_out) {
+                                                              unsigned long long* __restrict__ best_out,
+                                                              const IcpState* __restrict__ st) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
+    // device-resident loop (st != null): the step transform and whether to apply it come from the
+    // loop state; a converged loop's remaining launches return at once
+    if (st) {
+        if (st->done) return;
+        apply = st->it > 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) T.m[q] = st->T[q];
+    }
     __shared__ CandLds cl[ICPG_WAVES];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     CandLds* cs = &cl[wave];
@@ -373,7 +382,19 @@ hipError_t launch_icp_grid(const float* src_in, float* src_out, const float* T16
     for (int i = 0; i < 16; ++i) T.m[i] = T16 ? T16[i] : ((i % 5) == 0 ? 1.f : 0.f);
     const int blocks = (ns + ICPG_WAVES - 1) / ICPG_WAVES;
     bsk::k_icp_grid<<<blocks, 64 * ICPG_WAVES, 0, s>>>(src_in, src_out, T, apply, ns, g1.view(), g2.view(), g1.cell,
-                                                        g2.cell, tgt4, nt, best_out);
+                                                        g2.cell, tgt4, nt, best_out, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_icp_grid_dev(const float* src_in, float* src_out, IcpState* st, int ns, const DevGrid& g1,
+                               const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best, hipStream_t s) {
+    if (ns <= 0 || nt <= 0) return hipSuccess;
+    bsk::Xf16 T;
+    for (int i = 0; i < 16; ++i) T.m[i] = (i % 5) == 0 ? 1.f : 0.f;
+    const int blocks = (ns + ICPG_WAVES - 1) / ICPG_WAVES;
+    bsk::k_icp_grid<<<blocks, 64 * ICPG_WAVES, 0, s>>>(src_in, src_out, T, 0, ns, g1.view(), g2.view(), g1.cell, g2.cell,
+                                                        tgt4, nt, best, st);
+    bsk::k_icp_update<<<1, ICPU_THREADS, 0, s>>>(st, src_out, tgt4, best, ns);
     return hipGetLastError();
 }
 

@@ -63,6 +63,10 @@ struct IcpState {
     int it, done, max_iter, pad;
 };
 // one (NN, update) iteration pair; no-ops once st->done
+// one device-resident ICP iteration on the target grids: k_icp_grid with the loop state's step,
+// then k_icp_update (returns at once when the loop has converged)
+hipError_t launch_icp_grid_dev(const float* src_in, float* src_out, IcpState* st, int ns, const DevGrid& g1,
+                               const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best, hipStream_t s);
 hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int ns, const float4* tgt, int nt,
                           unsigned long long* best, unsigned long long* best_next, hipStream_t s);
 // load-balanced SHOT (describe2.hip): sort pieces, LRF over 64-rank chunks, records + ordered apply

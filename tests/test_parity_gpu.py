@@ -161,7 +161,10 @@ def test_match_exact_random_and_ties(ctx):
             np.testing.assert_array_equal(g, r)
 
 
-def test_icp_exact(ctx, cloud, sr_ref):
+@pytest.mark.parametrize("icp_dev", [0, 1])
+def test_icp_exact(ctx, cloud, sr_ref, icp_dev):
+    """A11 with the host Umeyama per iteration (icp_dev 0) and the device-resident loop (1)."""
+    ctx.set_option("icp_dev", icp_dev)
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 600)
     tgt = cloud[kidx]
@@ -169,13 +172,14 @@ def test_icp_exact(ctx, cloud, sr_ref):
     src = (tgt @ np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], np.float32).T + np.array([300, -200, 50], np.float32))
     src = src.astype(np.float32)
     T, it = ctx.icp(src, tgt)
+    ctx.set_option("icp_dev", 0)
     Tr, itr = orc.icp(src, tgt)
     assert it == itr
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
 
 
-@pytest.mark.parametrize("icp_grid", [1, 0])
-def test_icp_grid_edge_cases(icp_grid):
+@pytest.mark.parametrize("icp_grid,icp_dev", [(1, 0), (0, 0), (1, 1), (0, 1)])
+def test_icp_grid_edge_cases(icp_grid, icp_dev):
     """A11 1-NN on the target grids (k_icp_grid) vs the oracle's brute force: sources far beyond
     every ball (brute-force fallback), exact-duplicate targets (index tie), targets exactly on a
     ball radius (d2 == rs^2 is outside the ball), a non-finite source, sparse and dense targets."""
@@ -190,6 +194,7 @@ def test_icp_grid_edge_cases(icp_grid):
     c = bshot_py.Context(0)
     try:
         c.set_option("icp_grid", icp_grid)
+        c.set_option("icp_dev", icp_dev)
         for s2 in (src, src[:64]):
             T, it = c.icp(s2, tgt)
             Tr, itr = orc.icp(s2, tgt)
