@@ -252,11 +252,13 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
         HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient * (float)c->opt_iss_cell, s.pts4.p, st, false),
                "grid build (ISS)");
+        c->hmark("Q_iss_grid");
         HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
                           s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks),
                "iss launch");
         c->stage_end(sg3, st);
+        c->hmark("Q_iss_k");
         HIPCHK(hipMemcpyAsync(s.h_flag.p, s.issflag.p, n, hipMemcpyDeviceToHost, st), "D2H iss");
     }
     HIPCHK(hipMemcpyAsync(s.h_err.p + 1, s.errw.p + 1, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
@@ -1124,6 +1126,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
+    else if (k == "ransac_zc") c->opt_ransac_zc = value ? 1 : 0;
     else if (k == "sr_tile") c->opt_sr_tile = value < 0 ? 0 : (value > 3 ? 3 : value);
     else if (k == "sr_tile_q") c->opt_sr_tile_q = value < 64 ? 64 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;

@@ -164,7 +164,10 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
         std::memcpy(c->p_rpts.p + 3 * nidx, ct.data(), sizeof(float) * 3 * nidx);
         std::memcpy(c->p_rhyp.p, spos.data(), sizeof(int) * 3 * nhyp);
         const int sg = c->stage_begin(BSHOT_STAGE_RANSAC);
-        if (hipMemcpyAsync(c->rpts.p, c->p_rpts.p, sizeof(float) * np, hipMemcpyHostToDevice, c->stream) ||
+        if (c->opt_ransac_zc && nidx <= RANSAC_ZC_MAXN) {
+            if (bsh::launch_ransac_score_zc(c->p_rpts.p, nidx, c->p_rhyp.p, nhyp, thr2, c->p_rcnt.p, c->stream))
+                return c->fail("ransac: launch", BSHOT_EHIP);
+        } else if (hipMemcpyAsync(c->rpts.p, c->p_rpts.p, sizeof(float) * np, hipMemcpyHostToDevice, c->stream) ||
             hipMemcpyAsync(c->rhyp.p, c->p_rhyp.p, sizeof(int) * 3 * nhyp, hipMemcpyHostToDevice, c->stream) ||
             bsh::launch_ransac_score(c->rpts.p, c->rpts.p + 3 * nidx, nidx, c->rhyp.p, nhyp, thr2, c->rcnt.p,
                                      c->stream) ||
@@ -176,13 +179,17 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
     };
     auto gpu_scores = [&]() -> int {
         if (!gpu_launched) return BSHOT_OK;  // empty stream
+        ctx->hmark("M_rs_wait");
         if (hipStreamSynchronize(ctx->stream)) return ctx->fail("ransac: sync", BSHOT_EHIP);
+        ctx->hmark("M_rs_synced");
         gcnt = ctx->p_rcnt.p;
         return BSHOT_OK;
     };
     if (ctx) {
+        ctx->hmark("M_rs_begin");
         const int e = gpu_launch();
         if (e) return e;
+        ctx->hmark("M_rs_launched");
     }
 
     // ---- phase 2: RandomSampleConsensus::computeModel acceptance scan

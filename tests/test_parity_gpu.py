@@ -213,12 +213,16 @@ def test_icp_grid_edge_cases(icp_grid, icp_dev):
         c.close()
 
 
-@pytest.mark.parametrize("seed,frac", [(1, 0.6), (2, 0.3), (3, 0.9), (4, 0.05), (6, 0.15)])
-def test_ransac_dev_matches_host(ctx, seed, frac):
-    """A10 with the hypotheses scored on the GPU (bshot_ransac_dev) == host RANSAC == oracle, bit for bit."""
+@pytest.mark.parametrize("seed,frac,zc", [(1, 0.6, 0), (2, 0.3, 0), (3, 0.9, 0), (4, 0.05, 0), (6, 0.15, 0),
+                                          (1, 0.6, 1), (4, 0.05, 1)])
+def test_ransac_dev_matches_host(ctx, seed, frac, zc):
+    """A10 with the hypotheses scored on the GPU (bshot_ransac_dev; zc = 1: read from / written to
+    pinned host memory by one kernel) == host RANSAC == oracle, bit for bit."""
     from test_host import _corr_set
     src, tgt, cq, cm = _corr_set(seed, inlier_frac=frac)
+    ctx.set_option("ransac_zc", zc)
     rc, T, iq, im = ctx.ransac(src, tgt, cq, cm)
+    ctx.set_option("ransac_zc", 0)
     hrc, hT, hq, hm = bshot_py.ransac(src, tgt, cq, cm)
     orc_rc, oT, oq, om = orc.ransac(src, tgt, cq, cm)
     assert rc == hrc == orc_rc
