@@ -210,7 +210,7 @@ struct bshot_ctx {
     DBuf<unsigned long long> ipart;  // k_icp_tile span minima
     DBuf<unsigned int> icnt;         // k_icp_tile per-block arrival counters
     int opt_icp_grid = 1;  // 1: exact 1-NN on hashed grids of the targets (k_icp_grid); 0: LDS-tiled brute force (k_icp_tile)
-    bsh::DevGrid icp_g1, icp_g2;  // ICP target grids (cells 1000 / 5000 mm), built once per ICP call
+    bsh::DevGrid icp_lad[4];  // ICP target grids: nested cells 1000 .. 8000 mm (levels 0 and 2 used), one sort per ICP call
     int opt_icp_dev = 0;  // 1: ICP loop resident on the device (one sync); 0: host Umeyama per iteration (faster under load)
     DBuf<float> isrc, itgt3;
     DBuf<float4> itgt;

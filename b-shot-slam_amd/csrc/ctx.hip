@@ -660,6 +660,13 @@ int ctx_sync_main(bshot_ctx* c) {
     return BSHOT_OK;
 }
 
+// the ICP targets' grids (cells 1000 and 4000 mm) from one nested-key sort of itgt3; float4 targets
+// in index order -> itgt
+static hipError_t icp_grids(bshot_ctx* c, int nt, int min_cap) {
+    DevGrid* lad[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
+    return grid_build_ladder(lad, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, 0x5u, min_cap);
+}
+
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
             const float* d_tgt) {
     bg::Mat4f fin = bg::Mat4f::identity();
@@ -695,8 +702,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             const bool use_grid = c->opt_icp_grid != 0;
             if (use_grid) {
                 const int mc = std::max(65536, 2 * nt);
-                HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true, mc), "icp grid");
-                HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false, mc), "icp grid 2");
+                HIPCHK(icp_grids(c, nt, mc), "icp grids");
             } else {
                 HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
             }
@@ -720,7 +726,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                 const int b = j & 1;
                 if (use_grid)
                     HIPCHK(launch_icp_grid_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
-                                               c->istate.p, ns, c->icp_g1, c->icp_g2, c->itgt.p, nt, c->ibest.p,
+                                               c->istate.p, ns, c->icp_lad[0], c->icp_lad[2], c->itgt.p, nt, c->ibest.p,
                                                c->stream),
                            "icp iteration");
                 else
@@ -745,8 +751,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             // the targets are fixed for the whole ICP call: two hashed grids of them, built once
             HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
             const int mc = std::max(65536, 2 * nt);
-            HIPCHK(grid_build(c->icp_g1, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, true, mc), "icp grid");
-            HIPCHK(grid_build(c->icp_g2, c->itgt3.p, nt, 5000.f, c->itgt.p, c->stream, false, mc), "icp grid 2");
+            HIPCHK(icp_grids(c, nt, mc), "icp grids");
         } else {
             HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
             HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
@@ -760,7 +765,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             // one launch per iteration; the NN keys land in pinned host memory (no copy)
             const float* s_in = it == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
             if (use_grid)
-                HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->icp_g1, c->icp_g2,
+                HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->icp_lad[0], c->icp_lad[2],
                                        c->itgt.p, nt, c->p_best.p, c->stream),
                        "icp iteration");
             else
@@ -862,8 +867,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->pf2.release();
     bsh::gmap_free(c);
     c->gtgt.release();
-    bsh::grid_free(c->icp_g1);
-    bsh::grid_free(c->icp_g2);
+    for (auto& g : c->icp_lad) bsh::grid_free(g);
     c->errw.release(); c->normals.release(); c->kps.release(); c->counts.release(); c->offs.release();
     c->seg.release(); c->segtmp.release(); c->rf.release(); c->shot.release(); c->ok.release(); c->bits.release();
     c->ma.release(); c->lbest.release(); c->left.release();

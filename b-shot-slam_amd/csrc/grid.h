@@ -40,7 +40,10 @@ struct DevGrid {
 hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s,
                       bool write_pts4 = true, int min_cap = 0);
 void grid_free(DevGrid& g);
-// four nested grids (cells c0, 2c0, 4c0, 8c0) from one sort; g[1..3].spts alias g[0].spts
-hipError_t grid_build_ladder(DevGrid* const* g, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s);
+// four nested grids (cells c0, 2c0, 4c0, 8c0) from one sort; g[1..3].spts alias g[0].spts.
+// level_mask: the levels whose hash tables are built (the sorted points are always written);
+// min_cap as grid_build's
+hipError_t grid_build_ladder(DevGrid* const* g, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s,
+                             unsigned level_mask = 0xFu, int min_cap = 0);
 
 }  // namespace bsh

@@ -115,7 +115,7 @@ __global__ void k_ladder_cells(const unsigned long long* __restrict__ keys, cons
     const float4 p = pts4[vals[j]];
     if (write_spts) spts[j] = p;
     const unsigned long long k = keys[j];
-    if (k == BS_EMPTY_KEY) return;
+    if (k == BS_EMPTY_KEY || L < 0) return;  // L < 0: scatter only
     const unsigned long long pk = k >> (3 * L);
     if (j > 0 && (keys[j - 1] >> (3 * L)) == pk) return;
     int lo = j + 1, hi = n;
@@ -150,14 +150,15 @@ static unsigned int pow2_at_least(unsigned int x) {
 
 // g[0..3]: grids of cell c0, 2 c0, 4 c0, 8 c0 built from one 63-bit radix sort; g[0] owns the
 // sort buffers and the cell-sorted points, g[1..3] own only their hash tables and alias g[0].spts
-hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s) {
+hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s,
+                             unsigned level_mask, int min_cap) {
     hipError_t e;
     DevGrid& g0 = *gp[0];
     bool fresh = n > g0.cap || !g0.keys || g0.alias;
     for (int L = 1; L < 4; ++L) fresh = fresh || !gp[L]->alias || gp[L]->spts != g0.spts || !gp[L]->table;
     if (fresh) {
         for (int L = 0; L < 4; ++L) grid_free(*gp[L]);
-        g0.cap = n + n / 4 + 1024;
+        g0.cap = std::max(n + n / 4 + 1024, min_cap);
         if ((e = hipMalloc(&g0.keys, sizeof(unsigned long long) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.keys2, sizeof(unsigned long long) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.vals, sizeof(unsigned int) * g0.cap))) return e;
@@ -191,6 +192,13 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
         DevGrid& gl = *gp[L];
         gl.n = n;
         gl.cell = c0 * (float)(1 << L);
+        // level 0 always scatters the sorted points (the other levels alias them)
+        if (L > 0 && !((level_mask >> L) & 1u)) continue;
+        if (L == 0 && !(level_mask & 1u)) {
+            bsk::k_ladder_cells<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, -1, c0, gl.table, gl.H - 1,
+                                                              g0.spts, 1);
+            continue;
+        }
         bsk::k_grid_clear<<<(gl.H + B - 1) / B, B, 0, s>>>(gl.table, gl.H);
         bsk::k_ladder_cells<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, L, c0, gl.table, gl.H - 1,
                                                           g0.spts, L == 0);
