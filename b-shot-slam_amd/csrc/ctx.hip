@@ -171,8 +171,13 @@ int ctx_make_side_stream(bshot_ctx* c) {
     }
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
-    for (hipStream_t* p : sts)
-        if (hipStreamCreateWithPriority(p, hipStreamNonBlocking, lo_prio) != hipSuccess) return BSHOT_EHIP;
+    for (hipStream_t* p : sts) {
+        // opt_side_prio: the describe (side) stream's priority, 0 lowest (as pre / iss) .. 2 the main stream's
+        int pr = lo_prio;
+        if (p == &c->side && c->opt_side_prio > 0)
+            pr = c->opt_side_prio >= 2 ? hi_prio : lo_prio + (hi_prio - lo_prio) / 2;
+        if (hipStreamCreateWithPriority(p, hipStreamNonBlocking, pr) != hipSuccess) return BSHOT_EHIP;
+    }
     return BSHOT_OK;
 }
 
@@ -1147,7 +1152,10 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;
     else if (k == "timing_mask") c->timing_mask = (unsigned)value;
     else if (k == "dev_plan_hint") c->seg_hint = value < 0 ? 0 : value;  // tests: force / avoid a re-plan
-    else if (k == "side_cu_reserve") {
+    else if (k == "side_prio") {
+        c->opt_side_prio = value < 0 ? 0 : (value > 2 ? 2 : value);
+        return bsh::ctx_make_side_stream(c);
+    } else if (k == "side_cu_reserve") {
         c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);
     }

@@ -102,7 +102,7 @@ hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 
 // A10 RANSAC: score (inlier count) of every hypothesis (csrc/ransac.hip)
 // the scores from / into pinned host memory (one queue entry); nidx <= RANSAC_ZC_MAXN (LDS stage)
-#define RANSAC_ZC_MAXN 2560
+#define RANSAC_ZC_MAXN 768
 hipError_t launch_ransac_score_zc(const float* h_pts, int nidx, const int* h_hyp, int nhyp, double thr2, int* h_cnt,
                                   hipStream_t s);
 hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,

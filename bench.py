@@ -211,6 +211,7 @@ def main():
     k_eff = float(np.mean([s.n_keypoints for s in stats]))
     m_eff = float(np.mean([s.n_target for s in stats]))
     icp_it = float(np.mean([s.icp_iters for s in stats]))
+    corr = float(np.mean([s.n_mutual for s in stats]))
     n_eff = float(np.mean(npts[a.warmup:nwork]))
     ctx.close()
     # the dominant kernel among those with an algorithmic-bytes figure (k_seg_ratio in every
@@ -339,7 +340,7 @@ def main():
                                    f"{int(n_eff)} pts/sweep, K={a.keypoints}, SHOT r={a.shot_radius:g} mm, "
                                    f"full extract+describe+match+RANSAC+ICP+map per sweep",
                        "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
-                       "icp_iters": icp_it, "parallelism": f"frame-shard x{world}" +
+                       "icp_iters": icp_it, "mutual_corr": round(corr, 1), "parallelism": f"frame-shard x{world}" +
                        (" + RCCL map exchange" if a.map_bcast else "")},
             "roofline": roof,
             "cpu_baseline": cpu,

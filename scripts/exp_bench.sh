@@ -4,5 +4,5 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 for args in "$@"; do
   timeout -k 10 300 python bench.py --no-cpu-baseline $args > gpurun_out/eb.json 2> gpurun_out/eb.err || { tail -5 gpurun_out/eb.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('gpurun_out/eb.json')); print(sys.argv[1], d['value'], d['ms_per_step'], d['ms_per_step_median'], d['host_ms_per_sweep'])" "$args"
+  python -c "import json,sys; d=json.load(open('gpurun_out/eb.json')); print(sys.argv[1], d['value'], d['ms_per_step'], d['ms_per_step_median'], d['host_ms_per_sweep'], 'corr', d['config'].get('mutual_corr'))" "$args"
 done
