@@ -1,19 +1,24 @@
 #!/bin/bash
 # One GPU-box session: GPU parity tests, smoke, bench line, rocprofv3 kernel stats, HBM PMC passes.
 # Every GPU step has its own time limit and the chain stops at the first failure.
-# usage (from the repo root, via gpurun): bash scripts/gpu_round.sh [tag]
+# usage (from the repo root, via gpurun): bash scripts/gpu_round.sh [tag] [all|tests|perf]
+# (tests and perf as two gpurun calls keep each under gpurun's 20-minute limit)
 set -u
 TAG=${1:-r01}
+PART=${2:-all}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
+if [ "$PART" != perf ]; then
 echo "[gpu_round] $(date +%T) pytest -m gpu" &&
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1 &&
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1 &&
 tail -3 $O/pytest_gpu_$TAG.log &&
 echo "[gpu_round] $(date +%T) smoke" &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 &&
-cat $O/smoke_$TAG.log &&
+cat $O/smoke_$TAG.log || exit 1
+fi
+[ "$PART" = tests ] && exit 0
 echo "[gpu_round] $(date +%T) bench" &&
 timeout -k 10 600 python bench.py --profile-stages > $O/bench_$TAG.json 2> $O/bench_$TAG.err &&
 cat $O/bench_$TAG.json &&
