@@ -104,3 +104,21 @@ def test_gpu_reproduces_sequence_fixture(seq):
         assert np.array_equal(_u(np.array(st.T_ransac, np.float32)), _u(seq[f"T_ransac_{f}"].reshape(-1))), f
         assert np.array_equal(_u(np.array(st.pose, np.float32)), _u(seq[f"pose_{f}"].reshape(-1))), f
     od.close()
+
+
+def test_sequence_1000f_covers_gate_branches():
+    """The config-3 golden (tests/golden/sequence_1000f.npz, replayed bit-exact on the GPU by
+    tests/test_sequence_gpu.py) drives every branch of the gate (src/lidar_odometry.cpp:273-289):
+    NaN h_diff (acos of a rounded T_ij(1,1) > 1: every comparison false, so not gated by the
+    angle test), gated frames (previous pose kept, map not flagged) and accepted frames."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "sequence_1000f.npz"))
+    fields = [str(x) for x in g["stat_fields"]]
+    gated = g["stats"][:, fields.index("gated")]
+    nan_h = np.isnan(g["h_diff"])
+    assert nan_h.sum() >= 1
+    assert (gated == 1).sum() >= 1 and (gated == 0).sum() >= 1
+    # a NaN-h_diff frame is gated only by t_diff > 1200 or < 15 correspondences
+    t = g["t_diff"]
+    inl = g["stats"][:, fields.index("n_inliers")]  # corr_ = the RANSAC inliers
+    for f in np.flatnonzero(nan_h):
+        assert gated[f] == (1 if (t[f] > 1200 or inl[f] < 15) else 0), f
