@@ -170,9 +170,6 @@ struct bshot_ctx {
     DBuf<int> kidx;
     PinBuf<int> p_kidx;
     PinBuf<float> p_kps3;
-    // tuning knob "describe2": 2 load-balanced SHOT with the bucketed gather + in-bucket rank
-    // (default), 1 load-balanced SHOT with the piece sort, 0 wave/WG per keypoint
-    int opt_describe2 = 2;
     int opt_chunk_blocks = 0;  // grid cap of the 64-rank chunk kernels (0: one block per 4 chunks)
     int opt_dev_plan = 1;      // describe planned on the device (no mid-describe host sync) once sizes are known
     bool plan_on_host = false;  // next describe: plan on the host (after a device-plan overflow)
@@ -260,9 +257,7 @@ int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n);  // adopts a mat
 int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n);   // grids + SR + ISS on the side stream
 int ctx_sr_launch(bshot_ctx* c);   // SR of the current cloud (main stream) unless already launched
 int ctx_iss_launch(bshot_ctx* c);  // ISS of the current cloud (side stream) unless already launched
-// keypoints in c->kps; bits in c->bits. force_v1: the one-workgroup-per-keypoint SHOT path
-// (fallback when a describe2 sort piece overflows, errw bit 8)
-int ctx_describe_dev(bshot_ctx* c, int k, bool force_v1 = false);              // keypoints in c->kps; bits in c->bits
+int ctx_describe_dev(bshot_ctx* c, int k);              // keypoints in c->kps; bits in c->bits
 int ctx_match_dev(bshot_ctx* c, int na, int nb);        // descriptors in c->ma / c->mb
 // H2D indices, gather xyz of pts4[idx] into dst (device, k x 3); async
 int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst);
@@ -271,7 +266,7 @@ int ctx_sync_main(bshot_ctx* c);
 int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n);
-int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1 = false);
+int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k);
 // persistent-normals state around a lookahead describe of k keypoints on stream st: a describe
 // writes slots [0, k) and zero-fills past the logical size, so slots [0, min(k, size)) and the size
 // are all it can change. snapshot: queued on st before the describe; restore: after the describe

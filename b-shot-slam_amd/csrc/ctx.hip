@@ -426,7 +426,7 @@ int ctx_normals_restore(bshot_ctx* c) {
 void ctx_normals_discard(bshot_ctx* c) { c->normals_snap_size = -1; }
 
 // keypoints already in c->kps (device, k x 3)
-int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool force_v1) {
+int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > 512)
         return c->fail("normal_max_nn must be in [1, 512]", BSHOT_EINVAL);
     const int n = S.n;
@@ -454,12 +454,9 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     c->stage_end(sg4, st);
     const float R = c->prm.shot_radius;
     const int sg5 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
-    const bool bucketed = c->opt_describe2 == 2 && !force_v1;
-    if (bucketed) {
-        HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
-        HIPCHK(c->sbst.ensure(1024 * (size_t)k), "alloc bucket starts");
-    }
-    if (bucketed && c->opt_dev_plan && !c->plan_on_host && k <= 8192 && c->seg_hint > 0) {
+    HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
+    HIPCHK(c->sbst.ensure(1024 * (size_t)k), "alloc bucket starts");
+    if (c->opt_dev_plan && !c->plan_on_host && k <= 8192 && c->seg_hint > 0) {
         // the whole describe queued without a host round trip: the plan (segment offsets, chunk
         // bases, LPT order) is computed on the device against capacities sized from the largest
         // neighbourhood total seen so far (+25%); an overflow (errw bit 16) makes the caller
@@ -509,8 +506,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
         return BSHOT_OK;
     }
     c->plan_on_host = false;
-    HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st, bucketed ? c->sbh.p : nullptr),
-           "shot count");
+    HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st, c->sbh.p), "shot count");
     c->stage_end(sg5, st);
     HIPCHK(c->p_offs.ensure((size_t)k + 1), "alloc pinned offs");
     HIPCHK(hipMemcpyAsync(c->p_offs.p, c->offs.p, sizeof(long long) * ((size_t)k + 1), hipMemcpyDeviceToHost,
@@ -523,26 +519,9 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
     const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
-    if (bucketed)
-        HIPCHK(launch_shot_gather_b(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->sbh.p, c->sbst.p, c->seg.p, st),
-               "shot gather");
-    else
-        HIPCHK(launch_shot_gather(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->seg.p, st), "shot gather");
+    HIPCHK(launch_shot_gather_b(S.grid_coarse, c->kps.p, k, R, c->offs.p, c->sbh.p, c->sbst.p, c->seg.p, st),
+           "shot gather");
     c->stage_end(sg6, st);
-    if (!c->opt_describe2 || force_v1) {
-        const int sg7 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
-        HIPCHK(launch_shot_sort(c->offs.p, k, R, c->seg.p, c->segtmp.p, st), "shot sort");
-        c->stage_end(sg7, st);
-        const int sg8 = c->stage_begin(BSHOT_STAGE_LRF, st);
-        HIPCHK(launch_lrf(S.pts4.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p, st), "lrf");
-        c->stage_end(sg8, st);
-        const int sg9 = c->stage_begin(BSHOT_STAGE_HIST, st);
-        HIPCHK(launch_shot_hist(S.pts4.p, c->normals.p, c->kps.p, k, R, c->offs.p, c->seg.p, c->rf.p, c->ok.p,
-                                c->shot.p, c->bits.p, st),
-               "shot hist");
-        c->stage_end(sg9, st);
-        return BSHOT_OK;
-    }
     // host plan (after a device-plan overflow): 64-rank chunks and the LPT launch order
     const int n_plan = 0;
     long long nch = 0;
@@ -579,7 +558,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k, bool for
     A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
     A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
-    A.bstart = bucketed ? c->sbst.p : nullptr;
+    A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
@@ -603,7 +582,7 @@ bool ctx_describe_replan(bshot_ctx* c, const int* err) {
     return true;
 }
 
-int ctx_describe_dev(bshot_ctx* c, int k, bool force_v1) { return ctx_describe_on(c, c->cs, c->stream, k, force_v1); }
+int ctx_describe_dev(bshot_ctx* c, int k) { return ctx_describe_on(c, c->cs, c->stream, k); }
 
 int ctx_match_dev(bshot_ctx* c, int na, int nb) {
     HIPCHK(c->lbest.ensure((size_t)na + nb + 1), "alloc best");
@@ -1008,10 +987,7 @@ int bshot_describe(bshot_ctx* c, const float* kps, int k, float* shot, float* rf
             if ((rc = ctx_describe_dev(c, k))) return rc;
             continue;
         }
-        if (!(herr[0] & 8)) break;
-        // a describe2 sort piece overflowed its LDS buffer (pathological duplicate d2): rerun the
-        // SHOT stages one workgroup per keypoint
-        if ((rc = ctx_describe_dev(c, k, true))) return rc;
+        break;
     }
     if (herr[0] & 2) return c->fail("normals: neighbourhood with too many exactly tied boundary keys (kNN list overflow)", BSHOT_ECAP);
     return BSHOT_OK;
@@ -1130,7 +1106,6 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     if (!c || !name) return BSHOT_EINVAL;
     const std::string k(name);
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
-    else if (k == "describe2") c->opt_describe2 = value ? 2 : 0;  // the piece-sort variant (1) is retired
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;

@@ -20,8 +20,6 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
 // bh (nullable, [k][1024] u32): per-keypoint d2-bucket histogram for the bucketed gather
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s, unsigned int* bh = nullptr);
-hipError_t launch_shot_gather(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
-                              unsigned long long* seg, hipStream_t s);
 // bucket-grouped gather (bstart: per-keypoint bucket starts) and the in-bucket rank that sorts it
 hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
                                 const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s,
@@ -34,13 +32,6 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
                             hipStream_t s, int max_blocks = 0);
-hipError_t launch_shot_sort(const long long* offs, int k, float R, unsigned long long* seg, unsigned long long* tmp,
-                            hipStream_t s);
-hipError_t launch_lrf(const float4* pts4, const float* kps, int k, float R, const long long* offs,
-                      const unsigned long long* seg, float* rf, int* ok, hipStream_t s);
-hipError_t launch_shot_hist(const float4* pts4, const float4* normals, const float* kps, int k, float R,
-                            const long long* offs, const unsigned long long* seg, const float* rf, const int* ok,
-                            float* shot, unsigned int* bits, hipStream_t s);
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);

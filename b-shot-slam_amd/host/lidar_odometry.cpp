@@ -348,8 +348,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
             if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe (replan)");
             continue;
         }
-        if (!(c->p_err.p[0] & 8)) break;
-        if (bsh::ctx_describe_on(c, S, c->side, k, true) != BSHOT_OK) fail("lookahead describe (fallback)");
+        break;
     }
     if (k > 0 && (c->p_err.p[0] & 2)) throw std::runtime_error("normals neighbourhood overflow");
     la.words.assign(c->p_bits.p, c->p_bits.p + 11 * (size_t)k);
@@ -472,9 +471,7 @@ void LidarOdometry::computeDescriptors() {
             check(bsh::ctx_describe_dev(ctx_, k), "describe (replan)");
             continue;
         }
-        if (!(ctx_->p_err.p[0] & 8)) break;
-        // a load-balanced sort piece overflowed (pathological duplicate d2): one workgroup per keypoint
-        check(bsh::ctx_describe_dev(ctx_, k, true), "describe (fallback)");
+        break;
     }
     if (k > 0 && (ctx_->p_err.p[0] & 2)) check(BSHOT_ECAP, "normals neighbourhood overflow");
     cloud1_bshot_.resize(k);

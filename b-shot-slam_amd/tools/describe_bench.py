@@ -17,12 +17,12 @@ idx, rat = c.seg_ratio()
 kp, _ = bshot_py.select_topk(idx, rat, 2048)
 kps = pc[kp]
 ref = None
-# arguments: describe2 knob values, or name=value option sets ("chunk_blocks=2048,describe2=2")
-for arg in sys.argv[1:] or ["2", "1"]:
-    opts = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in arg.split(",")) if "=" in arg else {"describe2": int(arg)}
+# arguments: name=value option sets ("chunk_blocks=2048,dev_plan=0"); none: the defaults
+for arg in sys.argv[1:] or ["default"]:
+    opts = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in arg.split(",")) if "=" in arg else {}
     for kk, vv in opts.items():
         c.set_option(kk, vv)
-    d2 = arg
+    label = arg
     c.describe(kps)
     c.set_timing(True)
     c.stage_reset()
@@ -33,6 +33,6 @@ for arg in sys.argv[1:] or ["2", "1"]:
     same = ref is None or np.array_equal(bits, ref)
     ref = bits if ref is None else ref
     ms = {k: round(v[0] / 10, 4) for k, v in st.items() if v[1]}
-    print(json.dumps({"describe2": d2, "identical_bits": bool(same), "bits_sha": hashlib.sha1(bits.tobytes()).hexdigest()[:12],
+    print(json.dumps({"options": label, "identical_bits": bool(same), "bits_sha": hashlib.sha1(bits.tobytes()).hexdigest()[:12],
                       "shot_sha": hashlib.sha1(shot.tobytes()).hexdigest()[:12], "total_ms": round(sum(ms.values()), 4), **ms}))
 c.close()

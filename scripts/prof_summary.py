@@ -138,7 +138,7 @@ def main(tag):
     for f in (f"pre_bench_{tag}.json", f"prof_bench_{tag}.json", f"bench_{tag}.json", f"bench_driver_{tag}.json", f"host_phases_{tag}.txt", f"bench_{tag}.err", f"pytest_gpu_{tag}.log", f"smoke_{tag}.log"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f"{tag}_{f.replace('_' + tag, '')}"))
-    print(json.dumps({k: v for k, v in out["kernels"].items() if "k_seg_ratio" in k or "k_shot_hist" in k}))
+    print(json.dumps({k: v for k, v in out["kernels"].items() if "k_seg_ratio" in k}))
 
 
 if __name__ == "__main__":

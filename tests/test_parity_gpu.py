@@ -101,11 +101,9 @@ def test_iss_exact(ctx, cloud):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("k,d2", [(600, 2), (2048, 2), (2048, 1), (2048, 0)])
-def test_describe_parity(ctx, cloud, sr_ref, k, d2):
-    """d2 = 2: load-balanced SHOT with the bucketed gather + in-bucket rank (default); 1: with the
-    piece sort; 0: one workgroup per keypoint."""
-    ctx.set_option("describe2", d2)
+@pytest.mark.parametrize("k", [600, 2048])
+def test_describe_parity(ctx, cloud, sr_ref, k):
+    """Load-balanced SHOT: bucketed gather + in-bucket rank, chunked LRF, records + ordered apply."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, k)
     kps = cloud[kidx]
@@ -126,7 +124,6 @@ def test_describe_parity(ctx, cloud, sr_ref, k, d2):
     np.testing.assert_array_equal(rf.view(np.uint32)[~np.isnan(rf)], rrf.view(np.uint32)[~np.isnan(rrf)])
     np.testing.assert_array_equal(shot.view(np.uint32)[~np.isnan(shot)], rs.view(np.uint32)[~np.isnan(rs)])
     np.testing.assert_array_equal(bits, rb)
-    ctx.set_option("describe2", 2)
 
 
 @pytest.mark.parametrize("hint", [1 << 26, 1])
