@@ -129,6 +129,7 @@ struct bshot_ctx {
     int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
     int opt_ransac_zc = 0;      // RANSAC scores read/written in pinned host memory (one queue entry; A/B even)
     int opt_side_prio = 0;      // describe (side) stream priority: 0 low (as SR/ISS ahead), 1 middle, 2 the main stream's
+    int opt_hist_fused = 8;     // SHOT records computed and applied in one kernel: waves per workgroup (0: contrib + apply)
     int opt_sr_tile = 0;        // SR cell tiles: ladder level of a tile's cell (0: one query per wave; tiled measured slower)
     int opt_sr_tile_q = 128;    // tiled SR: queries a workgroup takes before it retires
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)

@@ -474,8 +474,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
         HIPCHK(c->okf.ensure(k), "alloc okf");
         HIPCHK(c->signs.ensure(2 * (size_t)chunk_cap), "alloc signs");
-        HIPCHK(c->recS.ensure(320 * (size_t)chunk_cap), "alloc records");
-        HIPCHK(c->recV.ensure(320 * (size_t)chunk_cap), "alloc records");
+        if (!c->opt_hist_fused) {  // the fused SHOT kernel keeps its records in LDS
+            HIPCHK(c->recS.ensure(320 * (size_t)chunk_cap), "alloc records");
+            HIPCHK(c->recV.ensure(320 * (size_t)chunk_cap), "alloc records");
+        }
         HIPCHK(launch_shot_count_plan(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->sbh.p, seg_cap, chunk_cap,
                                       c->offs.p, c->cb.p, c->perm.p, c->errw.p, st),
                "shot count + plan");
@@ -494,6 +496,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
         A.bstart = c->sbst.p;
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
+        A.hist_fused = c->opt_hist_fused;
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
@@ -547,8 +550,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
     HIPCHK(c->okf.ensure(k), "alloc okf");
     HIPCHK(c->signs.ensure(2 * (size_t)(cbr > 0 ? cbr : 1)), "alloc signs");  // per-chunk sign counts
-    HIPCHK(c->recS.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
-    HIPCHK(c->recV.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
+    if (!c->opt_hist_fused) {
+        HIPCHK(c->recS.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
+        HIPCHK(c->recV.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
+    }
     HIPCHK(c->perm.ensure(k), "alloc perm");
     HIPCHK(hipMemcpyAsync(c->cb.p, hcb, sizeof(int) * ((size_t)k + 1), hipMemcpyHostToDevice, st), "H2D cb");
     HIPCHK(hipMemcpyAsync(c->perm.p, hperm, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D perm");
@@ -560,6 +565,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
     A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
+    A.hist_fused = c->opt_hist_fused;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -1111,6 +1117,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "ransac_zc") c->opt_ransac_zc = value ? 1 : 0;
+    else if (k == "hist_fused") c->opt_hist_fused = value < 0 ? 0 : (value == 1 ? 8 : value);  // 1: default width
     else if (k == "sr_tile") c->opt_sr_tile = value < 0 ? 0 : (value > 3 ? 3 : value);
     else if (k == "sr_tile_q") c->opt_sr_tile_q = value < 64 ? 64 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;

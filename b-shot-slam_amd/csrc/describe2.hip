@@ -241,44 +241,16 @@ __device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0,
 #define PST2_RAD_135 2.3561944901923449288469825374596
 #define PST2_RAD_PI_7_8 2.7488935718910690836548129603691
 
-// records of chunk c (64 ranks): recS[320 c + 64 j + r] = bin of slot j of rank r (u16),
-// recV[...] = its value; slot order = PCL's add order per neighbour (cos neighbour, radius,
-// inclination, azimuth, main bin); unused slots and padding ranks -> bin 360 with value +0
-__global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__ pts4,
-                                                      const float4* __restrict__ normals,
-                                                      const float* __restrict__ kps, int k, float R,
-                                                      const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                      const int* __restrict__ owner,
-                                                      const unsigned long long* __restrict__ seg,
-                                                      const float* __restrict__ rf_in, const int* __restrict__ ok_in,
-                                                      unsigned short* __restrict__ recS, float* __restrict__ recV) {
-    const int lane = lane_id();
-    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
-        const int q = owner[c];
-        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-        const long long o = offs[q];
-        const int n = (int)(offs[q + 1] - o);
-        const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
-        if (!(fin && ok_in[q] && n >= 5)) return;
-        const int i = (c - cb[q]) * 64 + lane;
-        unsigned short* rs = recS + (size_t)c * 320 + lane;  // slot-major chunk rows: [slot][64 ranks]
-        float* rv = recV + (size_t)c * 320 + lane;
-        if (i >= n) {
-            // padding ranks of the keypoint's last chunk: no-op records
-    #pragma unroll
-            for (int j = 0; j < 5; ++j) { rs[64 * j] = (unsigned short)360; rv[64 * j] = 0.f; }
-            return;
-        }
+// the <= 5 (bin, value) interpolation records of one neighbour (key = its (d2 bits << 32 | idx)),
+// in PCL's add order (cos neighbour, radius, inclination, azimuth, main bin); unused slots: bin -1
+__device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, const float4* __restrict__ normals,
+                                             float kx, float ky, float kz, float R, const float* rf,
+                                             unsigned long long key, int* bins, float* vals) {
         const double Rd = (double)R;
         const double r12 = Rd / 2, r34 = (Rd * 3) / 4, r14 = Rd / 4;
         const int nr_bins = 10;
-        float rf[9];
     #pragma unroll
-        for (int j = 0; j < 9; ++j) rf[j] = rf_in[9 * (size_t)q + j];
-        int bins[5] = {-1, -1, -1, -1, -1};
-        float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-        const unsigned long long key = seg[o + i];
+        for (int j = 0; j < 5; ++j) { bins[j] = -1; vals[j] = 0.f; }
         const unsigned int idx = (unsigned int)(key & 0xFFFFFFFFu);
         const float4 nv = normals[idx];
         if (__builtin_isfinite(nv.x) && __builtin_isfinite(nv.y) && __builtin_isfinite(nv.z)) {
@@ -349,6 +321,43 @@ __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__
                 vals[4] = (float)w;
             }
         }
+}
+
+// records of chunk c (64 ranks): recS[320 c + 64 j + r] = bin of slot j of rank r (u16),
+// recV[...] = its value; slot order = PCL's add order per neighbour (cos neighbour, radius,
+// inclination, azimuth, main bin); unused slots and padding ranks -> bin 360 with value +0
+__global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__ pts4,
+                                                      const float4* __restrict__ normals,
+                                                      const float* __restrict__ kps, int k, float R,
+                                                      const long long* __restrict__ offs, const int* __restrict__ cb,
+                                                      const int* __restrict__ owner,
+                                                      const unsigned long long* __restrict__ seg,
+                                                      const float* __restrict__ rf_in, const int* __restrict__ ok_in,
+                                                      unsigned short* __restrict__ recS, float* __restrict__ recV) {
+    const int lane = lane_id();
+    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+        const int q = owner[c];
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        const long long o = offs[q];
+        const int n = (int)(offs[q + 1] - o);
+        const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
+        if (!(fin && ok_in[q] && n >= 5)) return;
+        const int i = (c - cb[q]) * 64 + lane;
+        unsigned short* rs = recS + (size_t)c * 320 + lane;  // slot-major chunk rows: [slot][64 ranks]
+        float* rv = recV + (size_t)c * 320 + lane;
+        if (i >= n) {
+            // padding ranks of the keypoint's last chunk: no-op records
+    #pragma unroll
+            for (int j = 0; j < 5; ++j) { rs[64 * j] = (unsigned short)360; rv[64 * j] = 0.f; }
+            return;
+        }
+        float rf[9];
+    #pragma unroll
+        for (int j = 0; j < 9; ++j) rf[j] = rf_in[9 * (size_t)q + j];
+        int bins[5];
+        float vals[5];
+        shot_records(pts4, normals, kx, ky, kz, R, rf, seg[o + i], bins, vals);
         unsigned int bb[5];
         float vv[5];
     #pragma unroll
@@ -548,6 +557,91 @@ __global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps
     }
 }
 
+// Records and ordered apply fused (knob hist_fused): a workgroup per keypoint (LPT order); waves
+// 1..HF_B compute the interpolation records of HF_B chunks into an LDS batch (shot_records, as
+// k_hist_contrib) while wave 0 applies the previous batch in rank order (as k_hist_apply: one
+// in-order ds_add_f32 per rank on lanes 0..4), double-buffered, so the records never leave LDS.
+template <int HF_WAVES>
+__global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __restrict__ pts4,
+                                                              const float4* __restrict__ normals,
+                                                              const float* __restrict__ kps, int k, float R,
+                                                              const int* __restrict__ perm,
+                                                              const long long* __restrict__ offs,
+                                                              const int* __restrict__ cb,
+                                                              const unsigned long long* __restrict__ seg,
+                                                              const float* __restrict__ rf_in,
+                                                              const int* __restrict__ ok_in, float* __restrict__ shot_out,
+                                                              unsigned int* __restrict__ bits_out) {
+    constexpr int HF_B = HF_WAVES - 1;  // chunks per batch (one per producing wave)
+    __shared__ float hist[384];
+    __shared__ unsigned int gcode[88];
+    __shared__ __attribute__((aligned(16))) unsigned short sS[2][HF_B][320];  // [buffer][chunk][slot x 64 ranks]
+    __shared__ __attribute__((aligned(16))) float sV[2][HF_B][320];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    if ((int)blockIdx.x >= k) return;
+    const int q = perm[blockIdx.x];
+    const bool good = apply_good(kps, offs, ok_in, q);
+    const int nch = good ? cb[q + 1] - cb[q] : 0;
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    float rf[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) rf[j] = good ? rf_in[9 * (size_t)q + j] : 0.f;
+    for (int j = threadIdx.x; j < 384; j += 64 * HF_WAVES) hist[j] = 0.0f;
+    auto produce = [&](int t, int buf, int bi) {
+        const int i = t * 64 + lane;
+        int bins[5] = {-1, -1, -1, -1, -1};
+        float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        if (i < n) shot_records(pts4, normals, kx, ky, kz, R, rf, seg[o + i], bins, vals);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            sS[buf][bi][64 * j + lane] = bins[j] < 0 ? (unsigned short)360 : (unsigned short)bins[j];
+            sV[buf][bi][64 * j + lane] = bins[j] < 0 ? 0.f : vals[j];
+        }
+    };
+    if (wave >= 1 && wave - 1 < nch) produce(wave - 1, 0, wave - 1);
+    __syncthreads();
+    const int nb = (nch + HF_B - 1) / HF_B;
+    for (int b = 0; b < nb; ++b) {
+        const int buf = b & 1;
+        if (wave == 0) {
+            if (lane < 5) {
+                for (int half = 0; half < 2 * HF_B && b * HF_B + (half >> 1) < nch; ++half) {
+                    // 32 ranks of chunk half / 2 at a time (keeps the applying path's registers low)
+                    const int bi = half >> 1, r0 = 32 * (half & 1);
+                    const uint4* b4 = reinterpret_cast<const uint4*>(&sS[buf][bi][64 * lane + r0]);
+                    const float4* v4 = reinterpret_cast<const float4*>(&sV[buf][bi][64 * lane + r0]);
+                    uint4 bw[4];
+                    float4 vw[8];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) bw[u] = b4[u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) vw[u] = v4[u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const unsigned int w[4] = {bw[u].x, bw[u].y, bw[u].z, bw[u].w};
+#pragma unroll
+                        for (int h = 0; h < 4; ++h) {
+                            const int r = 8 * u + 2 * h;
+                            const float4 va = vw[r >> 2];
+                            const float v0 = (r & 3) == 0 ? va.x : va.z;
+                            const float v1 = (r & 3) == 0 ? va.y : va.w;
+                            atomicAdd(&hist[w[h] & 0xFFFFu], v0);
+                            atomicAdd(&hist[w[h] >> 16], v1);
+                        }
+                    }
+                }
+            }
+        } else {
+            const int t = (b + 1) * HF_B + wave - 1;
+            if (t < nch) produce(t, buf ^ 1, wave - 1);
+        }
+        __syncthreads();
+    }
+    if (wave == 0) hist_finish(hist, gcode, q, good, lane, shot_out, bits_out);
+}
+
 }  // namespace bsk
 
 namespace bsh {
@@ -578,6 +672,19 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
                                                      A.okf, A.signs);
         bsk::k_lrf_fin<<<(A.k + 63) / 64, 64, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.sorted, A.eig, A.okf,
                                                       A.signs, A.rf, A.ok);
+        return hipGetLastError();
+    }
+    if (A.hist_fused) {
+        // hist_fused = waves per workgroup (1 applies, the rest produce records)
+        if (A.hist_fused <= 4)
+            bsk::k_hist_fused<4><<<A.k, 256, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
+                                                      A.rf, A.ok, A.shot, A.bits);
+        else if (A.hist_fused <= 8)
+            bsk::k_hist_fused<8><<<A.k, 512, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
+                                                      A.rf, A.ok, A.shot, A.bits);
+        else
+            bsk::k_hist_fused<16><<<A.k, 1024, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
+                                                        A.sorted, A.rf, A.ok, A.shot, A.bits);
         return hipGetLastError();
     }
     if (A.n_chunks > 0)

@@ -63,6 +63,7 @@ hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int
 // load-balanced SHOT (describe2.hip): sort pieces, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;
+    int hist_fused = 0;                    // records + ordered apply in one kernel (k_hist_fused)
     float R = 0.f;
     const int4* plan = nullptr;            // {q, piece, pieces, 0}
     const int* cb = nullptr;               // k + 1 chunk offsets

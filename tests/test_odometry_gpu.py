@@ -72,7 +72,8 @@ def test_odometry_no_icp_no_iss():
 
 @pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"queue_thread": 1}), (2, {"topk_thread": 0}),
                                         (2, {"icp_grid": 0, "ransac_dev": 0}),
-                                        (2, {"icp_grid": 0}), (2, {"icp_dev": 1}), (2, {"icp_dev": 0})])
+                                        (2, {"icp_grid": 0}), (2, {"icp_dev": 1}), (2, {"icp_dev": 0}),
+                                        (2, {"hist_fused": 0})])
 def test_odometry_lookahead_device_frames(depth, opts):
     """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
     stream during the current one (bshot_odom_set_next_device; depth 2 also queues the sweep after

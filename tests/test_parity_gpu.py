@@ -101,9 +101,12 @@ def test_iss_exact(ctx, cloud):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("k", [600, 2048])
-def test_describe_parity(ctx, cloud, sr_ref, k):
-    """Load-balanced SHOT: bucketed gather + in-bucket rank, chunked LRF, records + ordered apply."""
+@pytest.mark.parametrize("k,fused", [(600, 0), (600, 8), (2048, 0), (2048, 4), (2048, 8), (2048, 16)])  # k ascending: the module context's persistent normals array must not hold stale slots from a larger K
+def test_describe_parity(ctx, cloud, sr_ref, k, fused):
+    """Load-balanced SHOT: bucketed gather + in-bucket rank, chunked LRF, records + ordered apply
+    (fused = W > 0, the default 8: records computed by W - 1 waves and applied by one, in one
+    workgroup per keypoint, k_hist_fused; 0: k_hist_contrib + k_hist_apply)."""
+    ctx.set_option("hist_fused", fused)
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, k)
     kps = cloud[kidx]
@@ -124,6 +127,7 @@ def test_describe_parity(ctx, cloud, sr_ref, k):
     np.testing.assert_array_equal(rf.view(np.uint32)[~np.isnan(rf)], rrf.view(np.uint32)[~np.isnan(rrf)])
     np.testing.assert_array_equal(shot.view(np.uint32)[~np.isnan(shot)], rs.view(np.uint32)[~np.isnan(rs)])
     np.testing.assert_array_equal(bits, rb)
+    ctx.set_option("hist_fused", 8)
 
 
 @pytest.mark.parametrize("hint", [1 << 26, 1])
