@@ -489,7 +489,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         c->stage_end(sg6, st);
         Describe2Args A;
         A.k = k; A.n_plan = 0; A.n_chunks = chunk_cap; A.R = R;
-        A.plan = nullptr; A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p;
+        A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p;
         A.pts4 = S.pts4.p; A.normals = c->normals.p;
         A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
         A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
@@ -543,7 +543,6 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         cbr += (int)((c->p_offs.p[q + 1] - c->p_offs.p[q] + 63) / 64);
     }
     hcb[k] = cbr;
-    HIPCHK(c->plan.ensure(n_plan > 0 ? n_plan : 1), "alloc plan");
     HIPCHK(c->cb.ensure((size_t)k + 1), "alloc cb");
     HIPCHK(c->owner.ensure(cbr > 0 ? (size_t)cbr : 1), "alloc owner");
     HIPCHK(c->csum.ensure(8 * (size_t)(cbr > 0 ? cbr : 1)), "alloc csum");
@@ -559,7 +558,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(hipMemcpyAsync(c->perm.p, hperm, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D perm");
     Describe2Args A;
     A.k = k; A.n_plan = n_plan; A.n_chunks = cbr; A.R = R;
-    A.plan = c->plan.p; A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p; A.pts4 = S.pts4.p; A.normals = c->normals.p;
+    A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p; A.pts4 = S.pts4.p; A.normals = c->normals.p;
     A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
     A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;

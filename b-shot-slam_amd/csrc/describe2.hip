@@ -1,17 +1,20 @@
 // describe2.hip -- A5/A6/A7 on gfx950, load-balanced: the SHOT stages split every keypoint's
-// neighbourhood (up to ~22k points for keypoints near the sensor, ~3x the mean) into fixed-size
-// pieces so no single keypoint bounds a launch. Same arithmetic, same order as describe.hip.
+// neighbourhood (up to ~22k points for keypoints near the sensor, ~3x the mean) into 64-rank chunks
+// so no single keypoint bounds a launch (PCL SHOTEstimationOMP / SHOTLocalReferenceFrameEstimation,
+// include/bshot_bits.h:113-135; compute_bshot_from_SHOT :144-278).
 //
 //   (sorting: k_shot_rank, csrc/describe.hip -- exact rank inside the count pass's d2 buckets)
 //   k_lrf_chunks  wave per 64-rank chunk: 7 weighted-covariance terms by the xor-butterfly tree
 //   k_lrf_eig     thread per keypoint: chunk sums in chunk order, Jacobi eigenvectors
 //   k_lrf_sign    wave per chunk: sign counts for the x/z disambiguation (integer, order-free)
 //   k_lrf_fin     thread per keypoint: PCL's count + median-5 rule, float LRF rows
-//   k_hist_contrib wave per chunk: the <= 5 (bin, value) interpolation records of every neighbour
-//   k_hist_apply  wave per keypoint: records applied in rank order to the LDS histogram (in-order
-//                 ds_add_f32), L2 normalisation, B-SHOT bits
+//   k_hist_fused  workgroup per keypoint (default): 7 waves compute the <= 5 (bin, value)
+//                 interpolation records of every neighbour into a double-buffered LDS batch while
+//                 one wave applies them in rank order to the LDS histogram (in-order ds_add_f32),
+//                 then L2 normalisation and B-SHOT bits
+//   k_hist_contrib + k_hist_apply: the same as two kernels, records through HBM (hist_fused=0)
 // Chunk c of keypoint q covers ranks [64 (c - cb[q]), ...) where cb is the exclusive scan of
-// ceil(n_q / 64) (host-computed after the count pass).
+// ceil(n_q / 64) (k_desc_plan, or the host plan after an overflow).
 #include <hip/hip_runtime.h>
 
 #include "bshot_math.h"
@@ -27,55 +30,58 @@ __global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restric
     for (int c = cb[q] + threadIdx.x; c < cb[q + 1]; c += 256) owner[c] = q;
 }
 
-// csum[8 c + 0..5]: weighted covariance terms, [6]: weight sum, [7]: valid count
+// csum[8 c + 0..5]: weighted covariance terms, [6]: weight sum, [7]: valid count of chunk c =
+// ranks [64 t, 64 t + 64) of keypoint q (wave; lanes 0..7 store)
+__device__ __forceinline__ void lrf_chunk_terms(const float4* __restrict__ pts4, float kx, float ky, float kz, float R,
+                                                const unsigned long long* __restrict__ sg, int n, int t,
+                                                double* __restrict__ out8) {
+    const int lane = lane_id();
+    const int i = t * 64 + lane;
+    double v[7] = {0, 0, 0, 0, 0, 0, 0};
+    int isv = 0;
+    if (i < n) {
+        const unsigned long long key = sg[i];
+        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+        if (!(p.x == kx && p.y == ky && p.z == kz)) {
+            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+            const double w = (double)R - sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+            v[0] = w * (vx * vx); v[1] = w * (vx * vy); v[2] = w * (vx * vz);
+            v[3] = w * (vy * vy); v[4] = w * (vy * vz); v[5] = w * (vz * vz);
+            v[6] = w;
+            isv = 1;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j) v[j] = wave_tree_sum_d(v[j]);
+    const int nv = __popcll(__ballot(isv != 0));
+    if (lane < 8) {
+        double x = (double)nv;
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+            if (lane == j) x = v[j];
+        out8[lane] = x;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ pts4, const float* __restrict__ kps,
                                                     int k, float R, const long long* __restrict__ offs,
                                                     const int* __restrict__ cb, const int* __restrict__ owner,
                                                     const unsigned long long* __restrict__ seg,
                                                     double* __restrict__ csum) {
-    const int lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
         const int q = owner[c];
-        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         const long long o = offs[q];
-        const int n = (int)(offs[q + 1] - o);
-        const int i = (c - cb[q]) * 64 + lane;
-        double v[7] = {0, 0, 0, 0, 0, 0, 0};
-        int isv = 0;
-        if (i < n) {
-            const unsigned long long key = seg[o + i];
-            const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
-            if (!(p.x == kx && p.y == ky && p.z == kz)) {
-                const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-                const double w = (double)R - sqrt((double)__uint_as_float((unsigned)(key >> 32)));
-                v[0] = w * (vx * vx); v[1] = w * (vx * vy); v[2] = w * (vx * vz);
-                v[3] = w * (vy * vy); v[4] = w * (vy * vz); v[5] = w * (vz * vz);
-                v[6] = w;
-                isv = 1;
-            }
-        }
-    #pragma unroll
-        for (int j = 0; j < 7; ++j) v[j] = wave_tree_sum_d(v[j]);
-        const int nv = __popcll(__ballot(isv != 0));
-        if (lane < 8) {
-            double x = (double)nv;
-    #pragma unroll
-            for (int j = 0; j < 7; ++j)
-                if (lane == j) x = v[j];
-            csum[8 * (size_t)c + lane] = x;
-        }
-    }();
+        lrf_chunk_terms(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], R, seg + o, (int)(offs[q + 1] - o), c - cb[q],
+                        csum + 8 * (size_t)c);
+    }
 }
 
-// eig[8 q + 0..2] = x axis (largest), [3..5] = z axis (smallest), [6] = valid count; okf[q]
-__global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ cb, const double* __restrict__ csum,
-                                                double* __restrict__ eig, int* __restrict__ okf) {
-    const int q = blockIdx.x * 64 + threadIdx.x;
-    if (q >= k) return;
+// chunk sums of keypoint q in chunk order, then the Jacobi eigenvectors: e[0..2] = x axis (largest),
+// [3..5] = z axis (smallest), [6] = valid count; returns the ok flag
+__device__ __forceinline__ int lrf_eig_one(const double* __restrict__ csum, int c0, int c1, double* e) {
     double tot[7] = {0, 0, 0, 0, 0, 0, 0};
     long long valid = 0;
-    const int c0 = cb[q], c1 = cb[q + 1];
     for (int cc = c0; cc < c1; cc += 4) {
         double4 blk[4][2];
 #pragma unroll
@@ -105,47 +111,117 @@ __global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ c
         bm::jacobi3(cov, w, ev);
         if (bm::isfin(w[0]) && bm::isfin(w[1]) && bm::isfin(w[2])) {
             ok = 1;
-            double* e = eig + 8 * (size_t)q;
             e[0] = ev[2]; e[1] = ev[5]; e[2] = ev[8];
             e[3] = ev[0]; e[4] = ev[3]; e[5] = ev[6];
         }
     }
-    eig[8 * (size_t)q + 6] = (double)valid;
+    e[6] = (double)valid;
+    return ok;
+}
+
+// eig[8 q + 0..6] as lrf_eig_one; okf[q]
+__global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ cb, const double* __restrict__ csum,
+                                                double* __restrict__ eig, int* __restrict__ okf) {
+    const int q = blockIdx.x * 64 + threadIdx.x;
+    if (q >= k) return;
+    double e[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int ok = lrf_eig_one(csum, cb[q], cb[q + 1], e);
+    double* eo = eig + 8 * (size_t)q;
+    if (ok)
+        for (int j = 0; j < 6; ++j) eo[j] = e[j];
+    eo[6] = e[6];
     okf[q] = ok;
 }
 
-// csign[2 c] = #(v . x >= 0), csign[2 c + 1] = #(v . z >= 0) over chunk c's valid neighbours
-// (per-chunk counts, summed by k_lrf_fin: no same-address atomics)
+// #(v . x >= 0), #(v . z >= 0) over the valid neighbours of chunk t of a keypoint (wave-uniform result)
+__device__ __forceinline__ int2 lrf_sign_counts(const float4* __restrict__ pts4, float kx, float ky, float kz,
+                                                const unsigned long long* __restrict__ sg, int n, int t, const double* e) {
+    const int lane = lane_id();
+    const int i = t * 64 + lane;
+    int pt = 0, pn = 0;
+    if (i < n) {
+        const unsigned long long key = sg[i];
+        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+        if (!(p.x == kx && p.y == ky && p.z == kz)) {
+            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+            if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
+            if (((vx * e[3] + vy * e[4]) + vz * e[5]) >= 0) pn = 1;
+        }
+    }
+    return make_int2(__popcll(__ballot(pt != 0)), __popcll(__ballot(pn != 0)));
+}
+
+// csign[2 c], [2 c + 1]: chunk c's sign counts (summed by k_lrf_fin: no same-address atomics)
 __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
                                                   const int* __restrict__ owner,
                                                   const unsigned long long* __restrict__ seg,
                                                   const double* __restrict__ eig, const int* __restrict__ okf,
                                                   int* __restrict__ csign) {
-    const int lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
         const int q = owner[c];
-        if (!okf[q]) return;
-        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        if (!okf[q]) continue;
         const long long o = offs[q];
-        const int n = (int)(offs[q + 1] - o);
-        const int i = (c - cb[q]) * 64 + lane;
-        const double* e = eig + 8 * (size_t)q;
-        int pt = 0, pn = 0;
-        if (i < n) {
-            const unsigned long long key = seg[o + i];
-            const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
-            if (!(p.x == kx && p.y == ky && p.z == kz)) {
-                const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-                if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
-                if (((vx * e[3] + vy * e[4]) + vz * e[5]) >= 0) pn = 1;
-            }
+        const int2 v = lrf_sign_counts(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o,
+                                       (int)(offs[q + 1] - o), c - cb[q], eig + 8 * (size_t)q);
+        if (lane_id() == 0) reinterpret_cast<int2*>(csign)[c] = v;
+    }
+}
+
+// PCL's sign disambiguation of keypoint q's eigenvectors e (count rule from the summed sign
+// counts st / sn, median-5 rule over valid neighbours by rank) -> float LRF rows r9
+__device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, float kx, float ky, float kz,
+                                            const unsigned long long* __restrict__ sg, int n, const double* e, int st,
+                                            int sn, float* r9) {
+    const int valid_total = (int)e[6];
+    double x[3] = {e[0], e[1], e[2]}, z[3] = {e[3], e[4], e[5]};
+    int PT = 2 * st - valid_total;
+    int PN = 2 * sn - valid_total;
+    if (PT == 0 || PN == 0) {
+        // median-5 rule over valid neighbours by rank. Excluded neighbours (exact duplicates of the
+        // keypoint) have d2 == 0, so they sit in the leading d2 == 0 run: scan that run, then the
+        // valid rank r lives at index r + (excluded count).
+        const int med = valid_total / 2;
+        int addT = 0, addN = 0;
+        int z0n = 0, excl = 0;
+        while (z0n < n && (unsigned)(sg[z0n] >> 32) == 0u) {
+            const float4 p = pts4[(unsigned)(sg[z0n] & 0xFFFFFFFFu)];
+            if (p.x == kx && p.y == ky && p.z == kz) ++excl;
+            ++z0n;
         }
-        pt = __popcll(__ballot(pt != 0));
-        pn = __popcll(__ballot(pn != 0));
-        if (lane == 0) reinterpret_cast<int2*>(csign)[c] = make_int2(pt, pn);
-    }();
+        for (int r = med - 2; r <= med + 2; ++r) {
+            if (r < 0) continue;
+            int i;
+            if (r < z0n - excl) {
+                // rank inside the zero run: walk it (at most a few keys)
+                int rr = 0;
+                i = -1;
+                for (int u = 0; u < z0n; ++u) {
+                    const float4 p = pts4[(unsigned)(sg[u] & 0xFFFFFFFFu)];
+                    if (p.x == kx && p.y == ky && p.z == kz) continue;
+                    if (rr == r) { i = u; break; }
+                    ++rr;
+                }
+            } else {
+                i = r + excl;
+            }
+            if (i < 0 || i >= n) continue;
+            const float4 p = pts4[(unsigned)(sg[i] & 0xFFFFFFFFu)];
+            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+            if (((vx * x[0] + vy * x[1]) + vz * x[2]) > 0) addT++;
+            if (((vx * z[0] + vy * z[1]) + vz * z[2]) > 0) addN++;
+        }
+        if (PT == 0 && addT < 3) { x[0] = -x[0]; x[1] = -x[1]; x[2] = -x[2]; }
+        if (PN == 0 && addN < 3) { z[0] = -z[0]; z[1] = -z[1]; z[2] = -z[2]; }
+    }
+    if (PT < 0) { x[0] = -x[0]; x[1] = -x[1]; x[2] = -x[2]; }
+    if (PN < 0) { z[0] = -z[0]; z[1] = -z[1]; z[2] = -z[2]; }
+    const float x0 = (float)x[0], x1 = (float)x[1], x2 = (float)x[2];
+    const float z0 = (float)z[0], z1 = (float)z[1], z2 = (float)z[2];
+    r9[0] = x0; r9[1] = x1; r9[2] = x2;
+    r9[3] = z1 * x2 - z2 * x1; r9[4] = z2 * x0 - z0 * x2; r9[5] = z0 * x1 - z1 * x0;
+    r9[6] = z0; r9[7] = z1; r9[8] = z2;
 }
 
 __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
@@ -162,10 +238,6 @@ __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4,
         ok_out[q] = 0;
         return;
     }
-    const double* e = eig + 8 * (size_t)q;
-    const int valid_total = (int)e[6];
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    double x[3] = {e[0], e[1], e[2]}, z[3] = {e[3], e[4], e[5]};
     // sign counts: sum of the keypoint's per-chunk counts (integers, any order)
     int st = 0, sn = 0;
     {
@@ -181,54 +253,10 @@ __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4,
         }
         for (; cc < c1; ++cc) { st += cs2[cc].x; sn += cs2[cc].y; }
     }
-    int PT = 2 * st - valid_total;
-    int PN = 2 * sn - valid_total;
-    if (PT == 0 || PN == 0) {
-        // median-5 rule over valid neighbours by rank. Excluded neighbours (exact duplicates of the
-        // keypoint) have d2 == 0, so they sit in the leading d2 == 0 run: scan that run, then the
-        // valid rank r lives at index r + (excluded count).
-        const long long o = offs[q];
-        const int n = (int)(offs[q + 1] - o);
-        const int med = valid_total / 2;
-        int addT = 0, addN = 0;
-        int z0n = 0, excl = 0;
-        while (z0n < n && (unsigned)(seg[o + z0n] >> 32) == 0u) {
-            const float4 p = pts4[(unsigned)(seg[o + z0n] & 0xFFFFFFFFu)];
-            if (p.x == kx && p.y == ky && p.z == kz) ++excl;
-            ++z0n;
-        }
-        for (int r = med - 2; r <= med + 2; ++r) {
-            if (r < 0) continue;
-            int i;
-            if (r < z0n - excl) {
-                // rank inside the zero run: walk it (at most a few keys)
-                int rr = 0;
-                i = -1;
-                for (int u = 0; u < z0n; ++u) {
-                    const float4 p = pts4[(unsigned)(seg[o + u] & 0xFFFFFFFFu)];
-                    if (p.x == kx && p.y == ky && p.z == kz) continue;
-                    if (rr == r) { i = u; break; }
-                    ++rr;
-                }
-            } else {
-                i = r + excl;
-            }
-            if (i < 0 || i >= n) continue;
-            const float4 p = pts4[(unsigned)(seg[o + i] & 0xFFFFFFFFu)];
-            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-            if (((vx * x[0] + vy * x[1]) + vz * x[2]) > 0) addT++;
-            if (((vx * z[0] + vy * z[1]) + vz * z[2]) > 0) addN++;
-        }
-        if (PT == 0 && addT < 3) { x[0] = -x[0]; x[1] = -x[1]; x[2] = -x[2]; }
-        if (PN == 0 && addN < 3) { z[0] = -z[0]; z[1] = -z[1]; z[2] = -z[2]; }
-    }
-    if (PT < 0) { x[0] = -x[0]; x[1] = -x[1]; x[2] = -x[2]; }
-    if (PN < 0) { z[0] = -z[0]; z[1] = -z[1]; z[2] = -z[2]; }
-    const float x0 = (float)x[0], x1 = (float)x[1], x2 = (float)x[2];
-    const float z0 = (float)z[0], z1 = (float)z[1], z2 = (float)z[2];
-    r9[0] = x0; r9[1] = x1; r9[2] = x2;
-    r9[3] = z1 * x2 - z2 * x1; r9[4] = z2 * x0 - z0 * x2; r9[5] = z0 * x1 - z1 * x0;
-    r9[6] = z0; r9[7] = z1; r9[8] = z2;
+    const long long o = offs[q];
+    double e[7];
+    for (int j = 0; j < 7; ++j) e[j] = eig[8 * (size_t)q + j];
+    lrf_fin_one(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o, (int)(offs[q + 1] - o), e, st, sn, r9);
     ok_out[q] = 1;
 }
 
@@ -580,11 +608,11 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     const int wave = threadIdx.x >> 6, lane = lane_id();
     if ((int)blockIdx.x >= k) return;
     const int q = perm[blockIdx.x];
-    const bool good = apply_good(kps, offs, ok_in, q);
-    const int nch = good ? cb[q + 1] - cb[q] : 0;
     const long long o = offs[q];
     const int n = (int)(offs[q + 1] - o);
     const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const bool good = apply_good(kps, offs, ok_in, q);
+    const int nch = good ? cb[q + 1] - cb[q] : 0;
     float rf[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j) rf[j] = good ? rf_in[9 * (size_t)q + j] : 0.f;
@@ -646,7 +674,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
 
 namespace bsh {
 
-// part 0: sort pieces; 1: LRF; 2: histogram records + ordered apply
+// part 0: in-bucket rank (sorted segments); 1: LRF; 2: histogram records + ordered apply
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.k <= 0) return hipSuccess;
     hipError_t e;
@@ -676,15 +704,13 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     }
     if (A.hist_fused) {
         // hist_fused = waves per workgroup (1 applies, the rest produce records)
-        if (A.hist_fused <= 4)
-            bsk::k_hist_fused<4><<<A.k, 256, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
-                                                      A.rf, A.ok, A.shot, A.bits);
-        else if (A.hist_fused <= 8)
-            bsk::k_hist_fused<8><<<A.k, 512, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
-                                                      A.rf, A.ok, A.shot, A.bits);
-        else
-            bsk::k_hist_fused<16><<<A.k, 1024, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
-                                                        A.sorted, A.rf, A.ok, A.shot, A.bits);
+#define HF_LAUNCH(W)                                                                                               \
+    bsk::k_hist_fused<W><<<A.k, 64 * W, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,    \
+                                                A.rf, A.ok, A.shot, A.bits)
+        if (A.hist_fused <= 4) HF_LAUNCH(4);
+        else if (A.hist_fused <= 8) HF_LAUNCH(8);
+        else HF_LAUNCH(16);
+#undef HF_LAUNCH
         return hipGetLastError();
     }
     if (A.n_chunks > 0)

@@ -60,12 +60,11 @@ hipError_t launch_icp_grid_dev(const float* src_in, float* src_out, IcpState* st
                                const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best, hipStream_t s);
 hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int ns, const float4* tgt, int nt,
                           unsigned long long* best, unsigned long long* best_next, hipStream_t s);
-// load-balanced SHOT (describe2.hip): sort pieces, LRF over 64-rank chunks, records + ordered apply
+// load-balanced SHOT (describe2.hip): in-bucket rank, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;
-    int hist_fused = 0;                    // records + ordered apply in one kernel (k_hist_fused)
+    int hist_fused = 0;                    // records + ordered apply in one kernel (k_hist_fused): waves
     float R = 0.f;
-    const int4* plan = nullptr;            // {q, piece, pieces, 0}
     const int* cb = nullptr;               // k + 1 chunk offsets
     int* owner = nullptr;                  // keypoint of every chunk
     const int* perm = nullptr;             // keypoints by descending neighbourhood size
@@ -74,7 +73,7 @@ struct Describe2Args {
     const float4* normals = nullptr;
     const float* kps = nullptr;
     const unsigned long long* seg = nullptr;  // unsorted keys (gather)
-    unsigned long long* sorted = nullptr;     // sorted keys (output of k_sort2)
+    unsigned long long* sorted = nullptr;     // sorted keys (output of k_shot_rank)
     double* csum = nullptr;                   // 8 per chunk
     double* eig = nullptr;                    // 8 per keypoint
     int* okf = nullptr;                       // eigen ok per keypoint
@@ -85,9 +84,8 @@ struct Describe2Args {
     float* recV = nullptr;
     float* shot = nullptr;
     unsigned int* bits = nullptr;
-    int* err = nullptr;  // |= 8 when a sort piece overflows its LDS buffer
-    // part 0 by in-bucket rank of a bucket-grouped segment (bstart) instead of the piece sort
-    const unsigned int* bstart = nullptr;
+    int* err = nullptr;
+    const unsigned int* bstart = nullptr;  // per-keypoint bucket starts of the bucket-grouped segment
     int max_blocks = 0;  // grid cap of the chunk kernels (0: one block per 4 chunks)
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
