@@ -155,7 +155,7 @@ __device__ __forceinline__ void rank_in_place(KnnLds* L, int tot, float sc0) {
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
+__device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
                            int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
                            unsigned long long ts1, const unsigned long long** sorted);
 
@@ -168,10 +168,10 @@ __device__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy,
 // a counting sort over LDS only -- no second pass over the candidates.
 // start_step: first ladder step tried (any step is exact; a later start only costs work);
 // *step_out: the step whose radius delivered the result; *total_out: in-radius count there.
-__device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
+__device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
                            int start_step, int* need_out, int* step_out, int* total_out, unsigned long long* kst,
                            const unsigned long long** sorted) {
-    unsigned long long chunks = 0;
+    unsigned long long chunks = 0, chunks_before = 0;
     const int lane = lane_id();
     const unsigned long long ts0 = kst ? cycle_stamp() : 0ull;
     const float r2 = (float)((double)r * (double)r);
@@ -205,6 +205,11 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
         if (!went && kst && lane == 0) atomicAdd(&kst[6], 1ull);
         total = cnt;
         if (total >= max_nn) break;
+        if (went && step < last && kst && lane == 0) {
+            atomicAdd(&kst[25], 1ull);
+            atomicAdd(&kst[26], chunks - chunks_before);
+        }
+        chunks_before = chunks;
     }
     if (step > last) step = last;
     *step_out = step;
@@ -223,7 +228,7 @@ __device__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy,
 // The selection once a ladder step has delivered (>= max_nn keys in radius, or the last step):
 // L->hist holds that step's level-0 d2 histogram over [0, rs^2) and L->list its first KNN_CAP
 // in-radius keys, in any candidate order (the result does not depend on it).
-__device__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
+__device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
                            int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
                            unsigned long long ts1, const unsigned long long** sorted) {
     const int lane = lane_id();

@@ -1,7 +1,8 @@
 """SR kNN work counters (bshot_debug_knn_stats): where k_seg_ratio's time goes per query.
 kst: 0 queries, 5 chunks streamed, 6 steps skipped unstreamed, 7 refine passes, 8 bitonic P,
 9 need, 10 in-radius total, 11 streaming-path queries, 12..15 cycles (ladder, fast select,
-slow select, finish), 16+s queries resolved at ladder step s."""
+slow select, finish), 16+s queries resolved at ladder step s, 25 streamed ladder steps that fell short of max_nn, 26 their
+chunks."""
 import json
 import os
 import sys
@@ -19,4 +20,5 @@ print(json.dumps({"queries": s[0], "chunks_per_q": s[5] / q, "skipped_steps_per_
                   "avg_need": s[9] / q, "avg_total": s[10] / q, "streamed_path": s[11],
                   "cycles_per_q": {"ladder": cyc[0] / q, "fast_sel": cyc[1] / q, "slow_sel": cyc[2] / q,
                                    "finish": cyc[3] / q},
-                  "resolved_at_step": s[16:16 + 9]}))
+                  "resolved_at_step": s[16:16 + 9], "failed_steps_per_q": s[25] / q,
+                  "failed_chunks_per_q": s[26] / q}))

@@ -37,5 +37,6 @@ for opts in variants:
                           "steps": s[16:25], "chunks_per_q": s[5] / q, "avg_total": s[10] / q, "streamed": s[11],
                           "refine": s[7], "skipped": s[6], "identical": bool(same),
                           "cyc_ladder": s[12] / q, "cyc_fastsel": s[13] / q, "cyc_streamsel": s[14] / q,
-                          "cyc_math": s[15] / q}))
+                          "cyc_math": s[15] / q,
+                          "failed_steps_per_q": s[25] / q, "failed_chunks_per_q": s[26] / q}))
         c.close()
