@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __r
                                                     int* __restrict__ counts, unsigned int* __restrict__ bh) {
     __shared__ CandLds lds[4];
     __shared__ unsigned int hist[4][SG_BUCKETS];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
     const float sc = (float)SG_BUCKETS / R2;
@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) k_shot_gather_b(GridView g, const float* 
                                                        const int* __restrict__ err) {
     __shared__ CandLds lds[4];
     __shared__ unsigned int cur[4][SG_BUCKETS];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
     const float sc = (float)SG_BUCKETS / R2;
@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
                                                    const unsigned long long* __restrict__ seg,
                                                    unsigned long long* __restrict__ out) {
     __shared__ unsigned long long stage[4][SR_STAGE];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
     for (int c = blockIdx.x * 4 + wave; c < cb[k]; c += gridDim.x * 4) [&]() {
         const int q = owner[c];

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ p
                                                     const unsigned long long* __restrict__ seg,
                                                     double* __restrict__ csum) {
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
+    for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
         const int q = owner[c];
         const long long o = offs[q];
         lrf_chunk_terms(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], R, seg + o, (int)(offs[q + 1] - o), c - cb[q],
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts
                                                   const double* __restrict__ eig, const int* __restrict__ okf,
                                                   int* __restrict__ csign) {
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
+    for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
         const int q = owner[c];
         if (!okf[q]) continue;
         const long long o = offs[q];
@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__
                                                       unsigned short* __restrict__ recS, float* __restrict__ recV) {
     const int lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
+    for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
         const int q = owner[c];
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         const long long o = offs[q];
@@ -605,7 +605,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     __shared__ unsigned int gcode[88];
     __shared__ __attribute__((aligned(16))) unsigned short sS[2][HF_B][320];  // [buffer][chunk][slot x 64 ranks]
     __shared__ __attribute__((aligned(16))) float sV[2][HF_B][320];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     if ((int)blockIdx.x >= k) return;
     const int q = perm[blockIdx.x];
     const long long o = offs[q];

@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(64 * ICPG_WAVES) k_icp_grid(const float* __res
         for (int q = 0; q < 16; ++q) T.m[q] = st->T[q];
     }
     __shared__ CandLds cl[ICPG_WAVES];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     CandLds* cs = &cl[wave];
     cand_init(cs);
     for (int i = blockIdx.x * ICPG_WAVES + wave; i < ns; i += gridDim.x * ICPG_WAVES) {

@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
                                                                 double g21, double g32, double* __restrict__ third,
                                                                 int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     IssLds* L = reinterpret_cast<IssLds*>(smem) + wave;
     cand_init(&L->cand);
     const float r2 = (float)((double)salient * (double)salient);

@@ -20,20 +20,22 @@
 
 namespace bsk {
 
-#define KNN_NB 256
-// LDS per wave sets k_seg_ratio's occupancy (its candidate streaming is latency-bound). The list
-// holds every in-radius key of the deciding ladder step; the counting sort of the selected
-// prefix (<= KNN_PRE keys) runs in place through registers, so there is no scatter buffer:
-// 768 keys + hist + offsets + candidate marks = 9.2 KB per wave -> 16 waves per CU, the VGPR
-// limit at <= 128 VGPRs (1024 keys + a 512-key scatter buffer gave 10 waves: 1.23 ms; 640 + 384
-// gave 14: 0.96 ms).
+#ifndef KNN_NB
+#define KNN_NB 192
+#endif
+// k_seg_ratio's candidate streaming is bound by dependent L2 round trips, so waves per CU set its
+// speed (3 -> 4 waves per SIMD: 1.05 -> 0.86 ms, profiles/ab_sr_stream.txt). Per wave: the key
+// list (KNN_CAP keys), hist, offsets (u16) and candidate marks = 7.8 KB, so 20 waves fit the
+// CU's 160 KB LDS, matched by <= 96 VGPRs (waves_per_eu 5). The list holds every in-radius key of
+// the deciding ladder step when they fit; the counting sort of the selected prefix (<= KNN_PRE keys)
+// runs in place through registers.
 #ifndef KNN_CAP
-#define KNN_CAP 768
+#define KNN_CAP 704
 #endif
 #define KNN_PRE 512  // largest prefix the counting sort handles (8 keys per lane)
 #define KNN_WAVES 2
 #ifndef SR_WPE
-#define SR_WPE 4  // VGPRs <= 128: 4 waves per SIMD
+#define SR_WPE 5  // VGPRs <= 96: 5 waves per SIMD
 #endif
 #if SR_WPE > 0
 #define SR_ATTR __attribute__((amdgpu_waves_per_eu(SR_WPE)))
@@ -41,18 +43,18 @@ namespace bsk {
 #define SR_ATTR
 #endif
 
-// list, hist and boff are contiguous: after the selection they double as the bitonic buffer of the
-// general path (P <= 1024 keys) and as the rank-order float arrays of the finishing math (3 x 512
-// coordinates, plus 512 CVS terms)
+// list, hist and boff are contiguous: after the selection they double as the rank-order float
+// arrays of the finishing math (3 x 512 coordinates; the CVS terms overwrite the x array)
 struct KnnLds {
     unsigned long long list[KNN_CAP];  // in-radius keys of the last ladder step; then the sorted result
     unsigned int hist[KNN_NB];
-    unsigned int boff[KNN_NB + 4];
+    unsigned short boff[KNN_NB + 4];   // counting-sort bucket starts (<= KNN_PRE)
     CandLds cand;
 };
-static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 4 * (KNN_NB + 4) >= 8192,
-              "list + hist + boff must hold 1024 keys");
-static_assert(KNN_CAP >= KNN_PRE, "the prefix must fit the list");
+static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 2 * (KNN_NB + 4) >= 3 * 512 * 4,
+              "list + hist + boff must hold 3 x 512 floats");
+static_assert(KNN_CAP >= KNN_PRE, "the prefix must fit the list (and the bitonic sort's 512 keys)");
+static_assert(KNN_CAP % 64 == 0 && KNN_NB % 64 == 0, "lane-strided loops");
 
 __device__ __forceinline__ int bucket_of(float d2, float lo, float sc) {
     const float v = (d2 - lo) * sc;
@@ -117,11 +119,11 @@ __device__ __forceinline__ int prefix_offsets(KnnLds* L, int Bmax) {
         for (int j = 0; j < KNN_NB / 64; ++j) {
             const int b = lane * (KNN_NB / 64) + j;
             const int h = b <= Bmax ? (int)L->hist[b] : 0;
-            L->boff[b] = (unsigned)run;
+            L->boff[b] = (unsigned short)run;
             L->hist[b] = (unsigned)run;
             run += h;
         }
-        if (lane == 63) L->boff[KNN_NB] = (unsigned)tot;
+        if (lane == 63) L->boff[KNN_NB] = (unsigned short)tot;
     }
     __builtin_amdgcn_wave_barrier();
     return tot;
@@ -380,10 +382,32 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
             atomicAdd(&kst[14], ts2 - ts1);
         }
     }
-    unsigned long long* buf = L->list;  // P <= 1024 keys: spans list, hist and boff (dead here)
-    for (int i = cnt + lane; i < P; i += 64) buf[i] = ~0ull;
-    __builtin_amdgcn_wave_barrier();
-    wave_bitonic(buf, P);
+    if (P <= KNN_PRE) {
+        unsigned long long* buf = L->list;
+        for (int i = cnt + lane; i < P; i += 64) buf[i] = ~0ull;
+        __builtin_amdgcn_wave_barrier();
+        wave_bitonic(buf, P);
+    } else {
+        // more keys than the bitonic buffer: every key's rank among all (keys are distinct), in place
+        unsigned long long kk[KNN_CAP / 64];
+        unsigned int dst[KNN_CAP / 64];
+#pragma unroll
+        for (int j = 0; j < KNN_CAP / 64; ++j) {
+            const int i = lane + 64 * j;
+            kk[j] = i < cnt ? L->list[i] : ~0ull;
+            dst[j] = 0;
+        }
+        for (int q = 0; q < cnt; ++q) {
+            const unsigned long long o = L->list[q];
+#pragma unroll
+            for (int j = 0; j < KNN_CAP / 64; ++j) dst[j] += o < kk[j] ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < KNN_CAP / 64; ++j)
+            if (lane + 64 * j < cnt) L->list[dst[j]] = kk[j];
+        __builtin_amdgcn_wave_barrier();
+    }
     *sorted = L->list;
     return true;
 }
@@ -494,8 +518,9 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
         // CVS / CVSN: per-neighbour terms in parallel, sequential float sum in rank order
         const float ctn = sqrtf(tx * tx + (ty * ty + tz * tz));
         // a skipped neighbour stores +0: sum + (+0) == sum, as sum starts at +0 and so
-        // is never -0 (the only value +0 changes)
-        float* term = fl + 1536;
+        // is never -0 (the only value +0 changes). Each term overwrites its own x coordinate
+        // (read first, by the same lane).
+        float* term = fl;
         for (int r0 = 0; r0 < need; r0 += 64) {
             const int r = r0 + lane;
             if (r < need) {
@@ -523,7 +548,8 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
                                                               float* __restrict__ ratio, int* __restrict__ err,
                                                               unsigned long long* __restrict__ kst) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    // the wave index in an SGPR: the wave's LDS base is then rematerialised, not held in a VGPR
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
     cand_init(&L->cand);
     // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD group a contiguous query range
@@ -811,7 +837,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(LadderGrids lg, cons
                                                             int max_nn, float4* __restrict__ normals,
                                                             int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
     cand_init(&L->cand);
     float* fl = reinterpret_cast<float*>(L->list);
@@ -864,7 +890,10 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(LadderGrids lg, cons
     }
 }
 
-size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES; }
+#ifndef KNN_LDS_PAD
+#define KNN_LDS_PAD 0  // diagnostic: extra LDS per workgroup (occupancy sensitivity)
+#endif
+size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES + KNN_LDS_PAD; }
 
 }  // namespace bsk
 

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score(const float* __r
                                                                 const int* __restrict__ hyp, int nhyp, double thr2,
                                                                 int* __restrict__ cnt) {
     __builtin_amdgcn_s_setprio(3);  // main-stream kernel on the odometry chain's critical path
-    const int h = blockIdx.x * RS_WAVES + (threadIdx.x >> 6);
+    const int h = blockIdx.x * RS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id();
     if (h >= nhyp) return;
     double sd[9], td[9];
@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score_zc(const float* 
     const float* cs = sp;
     const float* ct = sp + 3 * nidx;
     const int lane = lane_id();
-    for (int h = blockIdx.x * RS_WAVES + (threadIdx.x >> 6); h < nhyp; h += gridDim.x * RS_WAVES) {
+    for (int h = blockIdx.x * RS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); h < nhyp; h += gridDim.x * RS_WAVES) {
         double sd[9], td[9];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
