@@ -54,7 +54,7 @@ class FrameStats(ctypes.Structure):
 ABI_SYMBOLS = [
     "bshot_default_params", "bshot_create", "bshot_destroy", "bshot_last_error", "bshot_sync", "bshot_stream",
     "bshot_set_cloud", "bshot_set_cloud_device", "bshot_seg_ratio", "bshot_select_topk", "bshot_iss",
-    "bshot_describe", "bshot_get_normals", "bshot_match", "bshot_ransac", "bshot_ransac_dev", "bshot_icp", "bshot_odom_create",
+    "bshot_describe", "bshot_get_normals", "bshot_match", "bshot_ransac", "bshot_ransac_dev", "bshot_ransac_scores", "bshot_icp", "bshot_odom_create",
     "bshot_odom_destroy", "bshot_odom_last_error", "bshot_odom_process", "bshot_odom_process_device",
     "bshot_odom_get_keypoints", "bshot_odom_get_ratios", "bshot_odom_get_bits", "bshot_odom_get_target",
     "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
@@ -370,6 +370,21 @@ def ransac(src, tgt, cq, cm, max_iter=2000, thresh=1500.0):
     if rc < 0:
         raise BshotError("ransac failed")
     return rc, T.reshape(4, 4), iq[: ni.value].copy(), im[: ni.value].copy()
+
+
+def ransac_scores(cs, ct, hyp, thresh=1500.0, ctx=None):
+    """Inlier counts of RANSAC hypotheses (3 correspondence positions each) over the pairs cs[i] ->
+    ct[i]: on the GPU with a Context (csrc/ransac.hip k_ransac_score), on the host without."""
+    cs = _f32(cs).reshape(-1, 3)
+    ct = _f32(ct).reshape(-1, 3)
+    hyp = np.ascontiguousarray(hyp, np.int32).reshape(-1, 3)
+    cnt = np.zeros(max(len(hyp), 1), np.int32)
+    h = ctx.h if ctx is not None else None
+    rc = lib().bshot_ransac_scores(h, _ptr(cs), _ptr(ct), len(cs), _ptr(hyp), len(hyp), ctypes.c_double(thresh),
+                                   _ptr(cnt))
+    if rc < 0:
+        raise BshotError("ransac_scores failed: %d" % rc)
+    return cnt[: len(hyp)].copy()
 
 
 class Odometry:

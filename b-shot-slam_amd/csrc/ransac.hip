@@ -16,34 +16,60 @@ namespace bsk {
 
 #define RS_WAVES 4
 
-// wave per hypothesis. cs/ct: correspondence source/target points (3 floats each, correspondence
-// order); hyp: 3 correspondence positions per hypothesis
+// Workgroup per 64 hypotheses, lane per hypothesis. Wave 0 computes the 64 models (one double
+// umeyama per lane, not one per wave replicated over its 64 lanes: the FP64 work is 1/64 of a
+// wave-per-hypothesis kernel, which matters because this kernel runs on the main stream while the
+// lookahead's FP64-heavy SHOT producers hold the SIMDs), stores them component-major in LDS, then
+// each of the 4 waves scores the 64 models over its quarter of the correspondences: the
+// correspondence index is wave-uniform, so the point loads are uniform (scalar) loads and every
+// lane tests its own model. Partial counts are integers, summed in any order.
+// cs/ct: correspondence source/target points (3 floats each, correspondence order); hyp: 3
+// correspondence positions per hypothesis
+#define RS_HYP 64
 __global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score(const float* __restrict__ cs,
                                                                 const float* __restrict__ ct, int nidx,
                                                                 const int* __restrict__ hyp, int nhyp, double thr2,
                                                                 int* __restrict__ cnt) {
     __builtin_amdgcn_s_setprio(3);  // main-stream kernel on the odometry chain's critical path
-    const int h = blockIdx.x * RS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    __shared__ float Ts[12][RS_HYP];
+    __shared__ int part[RS_WAVES][RS_HYP];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id();
-    if (h >= nhyp) return;
-    double sd[9], td[9];
+    const int h = blockIdx.x * RS_HYP + lane;
+    if (w == 0) {
+        float T[12];
+        if (h < nhyp) {
+            double sd[9], td[9];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int p = hyp[3 * h + i];
+            for (int i = 0; i < 3; ++i) {
+                const int p = hyp[3 * h + i];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            sd[3 * i + d] = (double)cs[3 * p + d];
-            td[3 * i + d] = (double)ct[3 * p + d];
+                for (int d = 0; d < 3; ++d) {
+                    sd[3 * i + d] = (double)cs[3 * p + d];
+                    td[3 * i + d] = (double)ct[3 * p + d];
+                }
+            }
+            double md[16];
+            bm::umeyama_seq<double>(sd, td, 3, md);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) T[k] = (float)md[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) T[k] = 0.0f;
         }
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Ts[k][lane] = T[k];
     }
-    // every lane computes the (uniform) model: no divergence, no broadcast
-    double md[16];
-    bm::umeyama_seq<double>(sd, td, 3, md);
+    __syncthreads();
     float T[12];
 #pragma unroll
-    for (int i = 0; i < 12; ++i) T[i] = (float)md[i];
+    for (int k = 0; k < 12; ++k) T[k] = Ts[k][lane];
+    const int per = (nidx + RS_WAVES - 1) / RS_WAVES;
+    const int i0 = w * per;
+    const int i1 = min(nidx, i0 + per);
     int c = 0;
-    for (int i = lane; i < nidx; i += 64) {
+#pragma unroll 4
+    for (int i = i0; i < i1; ++i) {
         const float x = cs[3 * i], y = cs[3 * i + 1], z = cs[3 * i + 2];
         const float px = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
         const float py = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
@@ -52,10 +78,14 @@ __global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score(const float* __r
         const float d2 = (dx * dx + dz * dz) + (dy * dy + 0.0f);
         c += (double)d2 < thr2 ? 1 : 0;
     }
-    // integer sum: order-free
+    part[w][lane] = c;
+    __syncthreads();
+    if (w == 0 && h < nhyp) {
+        int s = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if (lane == 0) cnt[h] = c;
+        for (int v = 0; v < RS_WAVES; ++v) s += part[v][lane];
+        cnt[h] = s;
+    }
 }
 
 // Zero-copy variant for the odometry's main stream: the correspondence points and hypotheses are
@@ -123,7 +153,7 @@ hipError_t launch_ransac_score_zc(const float* h_pts, int nidx, const int* h_hyp
 hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,
                                int* cnt, hipStream_t s) {
     if (nhyp <= 0) return hipSuccess;
-    bsk::k_ransac_score<<<(nhyp + RS_WAVES - 1) / RS_WAVES, 64 * RS_WAVES, 0, s>>>(cs, ct, nidx, hyp, nhyp, thr2, cnt);
+    bsk::k_ransac_score<<<(nhyp + RS_HYP - 1) / RS_HYP, 64 * RS_WAVES, 0, s>>>(cs, ct, nidx, hyp, nhyp, thr2, cnt);
     return hipGetLastError();
 }
 

@@ -261,3 +261,45 @@ extern "C" int bshot_ransac_dev(bshot_ctx* c, const float* src_xyz, int ns, cons
     c->resolve_events();
     return rc;
 }
+
+extern "C" int bshot_ransac_scores(bshot_ctx* c, const float* cs, const float* ct, int nidx, const int32_t* hyp,
+                                   int nhyp, double thresh, int32_t* cnt) {
+    if (nidx < 0 || nhyp < 0 || (nhyp > 0 && (!hyp || !cnt)) || (nidx > 0 && (!cs || !ct))) return BSHOT_EINVAL;
+    for (int i = 0; i < 3 * nhyp; ++i)
+        if (hyp[i] < 0 || hyp[i] >= nidx) return BSHOT_EINVAL;
+    const double thr2 = thresh * thresh;
+    if (!c) {
+        for (int h = 0; h < nhyp; ++h) {
+            double sd[9], td[9];
+            for (int i = 0; i < 3; ++i)
+                for (int d = 0; d < 3; ++d) {
+                    sd[3 * i + d] = cs[3 * hyp[3 * h + i] + d];
+                    td[3 * i + d] = ct[3 * hyp[3 * h + i] + d];
+                }
+            const bg::Mat4f T = bg::umeyama<double>(sd, td, 3);
+            int n = 0;
+            for (int i = 0; i < nidx; ++i) {
+                float p[3];
+                bg::xform(T, cs + 3 * i, p);
+                const float dx = p[0] - ct[3 * i], dy = p[1] - ct[3 * i + 1], dz = p[2] - ct[3 * i + 2];
+                const float d2 = (dx * dx + dz * dz) + (dy * dy + 0.0f);
+                n += (double)d2 < thr2 ? 1 : 0;
+            }
+            cnt[h] = n;
+        }
+        return BSHOT_OK;
+    }
+    if (nhyp == 0) return BSHOT_OK;
+    (void)hipSetDevice(c->device);
+    const size_t np = 6 * (size_t)nidx;
+    if (c->rpts.ensure(np) || c->rhyp.ensure(3 * (size_t)nhyp) || c->rcnt.ensure(nhyp))
+        return c->fail("ransac_scores: alloc", BSHOT_EHIP);
+    if (hipMemcpyAsync(c->rpts.p, cs, sizeof(float) * 3 * nidx, hipMemcpyHostToDevice, c->stream) ||
+        hipMemcpyAsync(c->rpts.p + 3 * nidx, ct, sizeof(float) * 3 * nidx, hipMemcpyHostToDevice, c->stream) ||
+        hipMemcpyAsync(c->rhyp.p, hyp, sizeof(int) * 3 * nhyp, hipMemcpyHostToDevice, c->stream) ||
+        bsh::launch_ransac_score(c->rpts.p, c->rpts.p + 3 * nidx, nidx, c->rhyp.p, nhyp, thr2, c->rcnt.p, c->stream) ||
+        hipMemcpyAsync(cnt, c->rcnt.p, sizeof(int) * nhyp, hipMemcpyDeviceToHost, c->stream) ||
+        hipStreamSynchronize(c->stream))
+        return c->fail("ransac_scores: launch", BSHOT_EHIP);
+    return BSHOT_OK;
+}

@@ -108,6 +108,12 @@ int bshot_ransac_dev(bshot_ctx* c, const float* src, int ns, const float* tgt, i
                      const int32_t* corr_m, int n_corr, int max_iter, double thresh, float* T_out, int32_t* inl_q,
                      int32_t* inl_m, int* n_inl);
 
+/*      Kernel-level check of the scorer: inlier counts of nhyp hypotheses (3 correspondence
+ *      positions each, into the nidx correspondence pairs cs[i] -> ct[i], xyz floats) under
+ *      thresh; c == NULL scores on the host (the scorer bshot_ransac uses), else on the GPU. ---- */
+int bshot_ransac_scores(bshot_ctx* c, const float* cs, const float* ct, int nidx, const int32_t* hyp, int nhyp,
+                        double thresh, int32_t* cnt);
+
 /* ---- A11: point-to-point ICP (PCL IterativeClosestPoint defaults, src/lidar_odometry.cpp:291-297).
  *      src is already transformed by the initial guess; T_out = ICP final transformation. ---- */
 int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T_out,

@@ -52,6 +52,21 @@ def test_ransac_matches_oracle(seed, frac):
     assert np.array_equal(iq, oq) and np.array_equal(im, om)
 
 
+def test_ransac_scores_host_consistent():
+    """The host scorer behind bshot_ransac_scores (the GPU kernel's checker): the best-scoring
+    hypothesis's count equals the inlier count of the RANSAC result whose model it is."""
+    src, tgt, cq, cm = _corr_set(11, inlier_frac=0.6)
+    cs, ct = src[cq], tgt[cm]
+    hyp = np.arange(3 * 40, dtype=np.int32).reshape(40, 3) % len(cq)
+    cnt = bshot_py.ransac_scores(cs, ct, hyp)
+    assert cnt.shape == (40,) and cnt.min() >= 0 and cnt.max() <= len(cq)
+    # an exact-inlier triple (cm == cq) scores at least its own three correspondences
+    good = np.flatnonzero(cq == cm)[:3].astype(np.int32)
+    assert bshot_py.ransac_scores(cs, ct, good[None, :])[0] >= 3
+    with pytest.raises(bshot_py.BshotError):
+        bshot_py.ransac_scores(cs, ct, np.array([[0, 1, len(cq)]], np.int32))
+
+
 def test_ransac_degenerate():
     src, tgt, cq, cm = _corr_set(5, n_corr=2)
     for ncorr in (0, 1, 2):

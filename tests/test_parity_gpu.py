@@ -236,6 +236,22 @@ def test_ransac_dev_matches_host(ctx, seed, frac, zc):
         assert r2[0] == o2[0] and np.array_equal(r2[1], o2[1]) and np.array_equal(r2[2], o2[2])
 
 
+@pytest.mark.parametrize("nidx,nhyp", [(1, 1), (3, 63), (5, 64), (600, 65), (601, 2001), (2048, 130)])
+def test_ransac_scores_kernel(ctx, nidx, nhyp):
+    """k_ransac_score (workgroup per 64 hypotheses, lane per model, waves over correspondence
+    quarters) == the host scorer bshot_ransac uses, count for count, including workgroups with
+    fewer hypotheses than lanes and waves whose correspondence quarter is empty."""
+    from test_host import _corr_set
+    src, tgt, cq, cm = _corr_set(nidx + 7, n_src=max(nidx, 3), n_corr=nidx, inlier_frac=0.5)
+    cs, ct = src[cq], tgt[cm]
+    rng = np.random.default_rng(nhyp)
+    hyp = rng.integers(0, nidx, (nhyp, 3)).astype(np.int32)
+    g = bshot_py.ransac_scores(cs, ct, hyp, ctx=ctx)
+    h = bshot_py.ransac_scores(cs, ct, hyp)
+    assert np.array_equal(g, h)
+    assert g.min() >= 0 and g.max() <= nidx
+
+
 def test_config5_dense_large_radius_describe():
     """BASELINE config 5: VLP-128-style 256k-point sweep, K=4096 keypoints, SHOT radius 5000 mm
     (the large-neighbourhood stress case). The GPU describes all 4096 keypoints; the oracle checks
