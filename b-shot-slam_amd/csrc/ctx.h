@@ -3,12 +3,17 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/bshot_abi.h"
 #include "grid.h"
+#include "regrow.h"
 #include "kernels.h"
 
 template <typename T>
@@ -25,6 +30,7 @@ struct DBuf {
         size_t c = n * 2 > (size_t)65536 ? n * 2 : (size_t)65536;
         hipError_t e = hipMalloc(&p, sizeof(T) * c);
         if (e == hipSuccess) cap = c;
+        note_regrow("device", sizeof(T) * c);
         return e;
     }
     void release() {
@@ -49,6 +55,7 @@ struct PinBuf {
         size_t c = n * 2 > (size_t)65536 ? n * 2 : (size_t)65536;
         hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * c, hipHostMallocDefault);
         if (e == hipSuccess) cap = c;
+        note_regrow("pinned", sizeof(T) * c);
         return e;
     }
     void release() {

@@ -580,6 +580,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
 bool ctx_describe_replan(bshot_ctx* c, const int* err) {
     if (!(err[0] & 16)) return false;
     c->work[1]++;  // re-planned describes (bshot_work_counters)
+    note_regrow("describe replan", 0);
     long long total = 0;
     std::memcpy(&total, err + 2, sizeof(total));
     if (total > c->seg_hint) c->seg_hint = total;
@@ -1146,6 +1147,8 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
 
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n) {
     if (!c) return BSHOT_EINVAL;
+    c->work[6] = g_regrow_n.load();
+    c->work[7] = g_regrow_bytes.load();
     for (int i = 0; i < n && i < 8; ++i) out[i] = c->work[i];
     return 8;
 }

@@ -489,6 +489,7 @@ static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s)
     T* p = nullptr;
     hipError_t e = hipMalloc(&p, sizeof(T) * c);
     if (e != hipSuccess) return e;
+    note_regrow("gmap", sizeof(T) * c);
     if (used) {
         e = hipMemcpyAsync(p, b.p, sizeof(T) * used, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;

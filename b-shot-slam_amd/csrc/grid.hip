@@ -12,6 +12,7 @@
 
 #include "dev_common.h"
 #include "grid.h"
+#include "regrow.h"
 
 namespace bsk {
 
@@ -159,6 +160,7 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
     if (fresh) {
         for (int L = 0; L < 4; ++L) grid_free(*gp[L]);
         g0.cap = std::max(n + n / 4 + 1024, min_cap);
+        note_regrow("ladder grids", (size_t)g0.cap * 48);
         if ((e = hipMalloc(&g0.keys, sizeof(unsigned long long) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.keys2, sizeof(unsigned long long) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.vals, sizeof(unsigned int) * g0.cap))) return e;
@@ -212,6 +214,7 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
     if (n > g.cap || g.alias || !g.keys) {
         grid_free(g);
         g.cap = std::max(n + n / 4 + 1024, min_cap);
+        note_regrow("grid", (size_t)g.cap * 48);
         if ((e = hipMalloc(&g.keys, sizeof(unsigned long long) * g.cap))) return e;
         if ((e = hipMalloc(&g.keys2, sizeof(unsigned long long) * g.cap))) return e;
         if ((e = hipMalloc(&g.vals, sizeof(unsigned int) * g.cap))) return e;

@@ -313,7 +313,10 @@ def main():
             import ctypes
             wc = (ctypes.c_int64 * 8)()
             bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 8)
-            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": list(wc)}), file=sys.stderr)
+            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": list(wc),
+                              # CLOCK_MONOTONIC ms, the clock of BSHOT_GROW_TRACE's lines
+                              "t0_ms": round(t0 * 1e3, 3), "marks_ms": np.round(np.array(marks) * 1e3, 3).tolist()}),
+                  file=sys.stderr)
         if a.profile_stages:
             print(json.dumps({k: [round(v[0], 3), v[1]] for k, v in stages.items()}), file=sys.stderr)
             hm = np.mean([list(s.host_ms) for s in stats], axis=0)
