@@ -22,7 +22,7 @@ struct DBuf {
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
+        defer_free(p, DEFER_DEVICE);
         p = nullptr;
         cap = 0;
         // doubling with a 64 Ki-element floor: a sequence's sizes (targets M, neighbourhood totals)
@@ -47,7 +47,7 @@ struct PinBuf {
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
+        defer_free(p, DEFER_PINNED);
         p = nullptr;
         cap = 0;
         // doubling with a 64 Ki-element floor: a sequence's sizes (targets M, neighbourhood totals)

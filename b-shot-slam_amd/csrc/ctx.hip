@@ -518,7 +518,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(hipStreamSynchronize(st), "sync offs");
     const long long total = c->p_offs.p[k];
     c->work[0] = total;
-    if (total > c->seg_hint) c->seg_hint = total;
+    // the first total seen sets the device plan's capacities with 50% headroom on top of the
+    // plan's own +50%: a sequence's totals drift upwards over its first sweeps, and each overflow
+    // costs a re-planned describe plus a free + malloc of the neighbour-key buffers (hundreds of MB)
+    if (total > c->seg_hint) c->seg_hint = c->seg_hint == 0 ? total + total / 2 : total;
     HIPCHK(c->seg.ensure(total > 0 ? (size_t)total : 1), "alloc seg");
     HIPCHK(c->segtmp.ensure(total > 0 ? (size_t)total : 1), "alloc segtmp");
     const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
@@ -878,6 +881,7 @@ void bshot_destroy(bshot_ctx* c) {
         (void)hipStreamDestroy(c->iss);
         (void)hipStreamDestroy(c->pre);
     }
+    flush_deferred_frees();  // buffers parked by regrowths (regrow.h)
     delete c;
 }
 

@@ -496,7 +496,7 @@ static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s)
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
     }
-    if (b.p) (void)hipFree(b.p);
+    defer_free(b.p, DEFER_DEVICE);  // stream-ordered copy above; freed at context teardown
     b.p = p;
     b.cap = c;
     return hipSuccess;
@@ -733,6 +733,7 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
         any = any || m->q_active;
     }
     if (any) HIPCHK(hipStreamSynchronize(c->stream), "sync map query");
+    c->hmark("M_q_synced");
     int mtot = 0;
     for (GMap* m : maps) mtot += m->q_active ? m->p_ctr.p[GM_QTOT] : 0;
     const int nb = mtot + kref;
@@ -833,7 +834,9 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
                               c->stream),
                "D2H match");
     }
+    c->hmark("M_m_launched");
     HIPCHK(hipStreamSynchronize(c->stream), "sync match");
+    c->hmark("M_m_synced");
     c->resolve_events();
     if (nb > 0) std::memcpy(tgt.data(), g.p_tgt.p, sizeof(float) * 3 * nb);
     if (!run) return BSHOT_OK;

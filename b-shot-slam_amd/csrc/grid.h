@@ -39,7 +39,8 @@ struct DevGrid {
 // targets), so that regrowth, a device-wide stall (hipFree), is rare
 hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4* d_pts4, hipStream_t s,
                       bool write_pts4 = true, int min_cap = 0);
-void grid_free(DevGrid& g);
+// defer: park the buffers until context teardown (regrowth inside the sweep loop; regrow.h)
+void grid_free(DevGrid& g, bool defer = false);
 // four nested grids (cells c0, 2c0, 4c0, 8c0) from one sort; g[1..3].spts alias g[0].spts.
 // level_mask: the levels whose hash tables are built (the sorted points are always written);
 // min_cap as grid_build's

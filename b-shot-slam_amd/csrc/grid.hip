@@ -158,7 +158,7 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
     bool fresh = n > g0.cap || !g0.keys || g0.alias;
     for (int L = 1; L < 4; ++L) fresh = fresh || !gp[L]->alias || gp[L]->spts != g0.spts || !gp[L]->table;
     if (fresh) {
-        for (int L = 0; L < 4; ++L) grid_free(*gp[L]);
+        for (int L = 0; L < 4; ++L) grid_free(*gp[L], true);
         g0.cap = std::max(n + n / 4 + 1024, min_cap);
         note_regrow("ladder grids", (size_t)g0.cap * 48);
         if ((e = hipMalloc(&g0.keys, sizeof(unsigned long long) * g0.cap))) return e;
@@ -212,7 +212,7 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
                       bool write_pts4, int min_cap) {
     hipError_t e;
     if (n > g.cap || g.alias || !g.keys) {
-        grid_free(g);
+        grid_free(g, true);
         g.cap = std::max(n + n / 4 + 1024, min_cap);
         note_regrow("grid", (size_t)g.cap * 48);
         if ((e = hipMalloc(&g.keys, sizeof(unsigned long long) * g.cap))) return e;
@@ -240,19 +240,28 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
     return hipGetLastError();
 }
 
-void grid_free(DevGrid& g) {
+void grid_free(DevGrid& g, bool defer) {
     if (g.alias) g.spts = nullptr;  // owned by the ladder's level-0 grid
-    if (g.keys) (void)hipFree(g.keys);
-    if (g.keys2) (void)hipFree(g.keys2);
-    if (g.vals) (void)hipFree(g.vals);
-    if (g.vals2) (void)hipFree(g.vals2);
-    if (g.spts) (void)hipFree(g.spts);
-    if (g.table) (void)hipFree(g.table);
-    if (g.ncells) (void)hipFree(g.ncells);
-    if (g.tiles) (void)hipFree(g.tiles);
-    if (g.tctr) (void)hipFree(g.tctr);
-    if (g.tmp) (void)hipFree(g.tmp);
+    for (void* p : {(void*)g.keys, (void*)g.keys2, (void*)g.vals, (void*)g.vals2, (void*)g.spts, (void*)g.table,
+                    (void*)g.ncells, (void*)g.tiles, (void*)g.tctr, (void*)g.tmp}) {
+        if (!p) continue;
+        if (defer) defer_free(p, DEFER_DEVICE);  // a regrowth inside the sweep loop
+        else (void)hipFree(p);
+    }
     g = DevGrid();
 }
 
+
 }  // namespace bsh
+
+void flush_deferred_frees() {
+    std::vector<std::pair<void*, int>> v;
+    {
+        std::lock_guard<std::mutex> lk(g_defer_mu);
+        v.swap(g_deferred);
+    }
+    for (auto& e : v) {
+        if (e.second == DEFER_PINNED) (void)hipHostFree(e.first);
+        else (void)hipFree(e.first);
+    }
+}

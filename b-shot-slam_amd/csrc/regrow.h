@@ -6,6 +6,9 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 // process-wide regrowth events of the grow-only pools (bshot_work_counters [6] count, [7] bytes);
 // BSHOT_GROW_TRACE=1 prints each one (kind, bytes) to stderr
@@ -21,3 +24,19 @@ inline void note_regrow(const char* kind, size_t bytes) {
     }
 }
 
+
+// Buffers replaced by a regrowth are not freed in the sweep loop: hipFree waits for the whole
+// device and unmaps memory from the GPU, and measured stalls of 6-7 ms of the odometry chain
+// followed such frees (profiles/r02h_stalls.txt). They are parked here and freed when a context is
+// destroyed (after its streams are synchronised); growth is geometric, so at most about as much
+// memory as the live pools is parked.
+enum DeferKind { DEFER_DEVICE = 0, DEFER_PINNED = 1 };
+inline std::mutex g_defer_mu;
+inline std::vector<std::pair<void*, int>> g_deferred;
+inline void defer_free(void* p, int kind) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_defer_mu);
+    g_deferred.emplace_back(p, kind);
+}
+// frees every parked buffer (bshot_destroy; hipFree synchronises the device first)
+void flush_deferred_frees();
