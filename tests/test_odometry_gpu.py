@@ -104,17 +104,19 @@ def test_odometry_lookahead_device_frames(depth, opts):
         od.close()
 
 
-def test_kp_test_config1_kp_evaluation():
-    """BASELINE config 1 / kp_test (test/kp_test.cpp:159-181): ground-free HDL-64 sweeps (N ~ 61k in
-    the synthetic scene, whose returns are half ground; ~120k in the reference's recordings),
-    K=600, kpEvaluation every frame (src/lidar_odometry.cpp:392-445): the SR and ISS 1-NN
-    repeatability rates equal the oracle's bit for bit, on top of the whole-frame parity."""
+@pytest.mark.parametrize("sensor,frames,lo,hi", [(0, 3, 40000, 130000), (1, 2, 120000, 160000)])
+def test_kp_test_config1_kp_evaluation(sensor, frames, lo, hi):
+    """BASELINE config 1 / kp_test (test/kp_test.cpp:159-181): ground-free sweeps, K=600,
+    kpEvaluation every frame (src/lidar_odometry.cpp:392-445): the SR and ISS 1-NN repeatability
+    rates equal the oracle's bit for bit, on top of the whole-frame parity. Sensor 0 (HDL-64 scene,
+    half of whose returns are ground) leaves ~61k points; sensor 1 (the 128-laser scene) leaves
+    ~140k, at and above the ~120k of the reference's ground-removed recordings."""
     od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=600, run_kp_eval=1))
     oo = orc.Odometry(orc.params(num_keypoints=600))
     try:
-        for f in range(3):
-            xyz, _ = bshot_py.synth_sweep(f, no_ground=True)
-            assert 40000 < len(xyz) < 130000
+        for f in range(frames):
+            xyz, _ = bshot_py.synth_sweep(f, sensor=sensor, no_ground=True)
+            assert lo < len(xyz) < hi
             st = od.process(xyz)
             so = oo.process(xyz)
             assert st.n_keypoints == so.n_keypoints and st.n_iss == so.n_iss and st.n_inliers == so.n_inliers
