@@ -737,7 +737,9 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             return BSHOT_OK;
         }
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
-        const unsigned long long* best = c->p_best.p;
+        // the NN keys land in pinned host memory (no copy), double-buffered by iteration parity so
+        // the next iteration's kernel can be in flight while the host finishes this one
+        HIPCHK(c->p_best.ensure(2 * (size_t)ns), "alloc pinned best");
         const int splits = icp_tile_splits(ns, nt);
         const bool use_grid = c->opt_icp_grid != 0;
         if (use_grid) {
@@ -750,32 +752,43 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
             HIPCHK(hipMemsetAsync(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
         }
-        double prev_mse = 1.7976931348623157e308;
-        bg::Mat4f Ts = bg::Mat4f::identity();
-        while (true) {
-            const int b = it & 1;
+        // one launch per iteration: iteration j moves the source by the previous step's transform
+        // (j > 0) and writes its NN keys to p_best[j & 1]
+        auto launch_it = [&](int j, const bg::Mat4f& Tj) -> int {
+            const int b = j & 1;
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-            // one launch per iteration; the NN keys land in pinned host memory (no copy)
-            const float* s_in = it == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
+            const float* s_in = j == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
+            unsigned long long* bo = c->p_best.p + (size_t)ns * b;
             if (use_grid)
-                HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->icp_lad[0], c->icp_lad[2],
-                                       c->itgt.p, nt, c->p_best.p, c->stream),
+                HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Tj.m, j > 0, ns, c->icp_lad[0],
+                                       c->icp_lad[2], c->itgt.p, nt, bo, c->stream),
                        "icp iteration");
             else
-                HIPCHK(launch_icp_tile(s_in, c->isrc.p + 3 * (size_t)ns * b, Ts.m, it > 0, ns, c->itgt3.p, nt,
-                                       c->ipart.p, (int)std::min<size_t>(c->ipart.cap, 0x7FFFFFFF), c->icnt.p,
-                                       c->p_best.p, c->stream),
+                HIPCHK(launch_icp_tile(s_in, c->isrc.p + 3 * (size_t)ns * b, Tj.m, j > 0, ns, c->itgt3.p, nt,
+                                       c->ipart.p, (int)std::min<size_t>(c->ipart.cap, 0x7FFFFFFF), c->icnt.p, bo,
+                                       c->stream),
                        "icp iteration");
             c->stage_end(sg14);
+            return BSHOT_OK;
+        };
+        double prev_mse = 1.7976931348623157e308;
+        bg::Mat4f Ts = bg::Mat4f::identity();
+        if (int e = launch_it(0, Ts)) return e;
+        while (true) {
+            const unsigned long long* best = c->p_best.p + (size_t)ns * (it & 1);
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
             for (int i = 0; i < ns; ++i) {
                 const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);
                 tb[3 * i] = tgt[3 * j]; tb[3 * i + 1] = tgt[3 * j + 1]; tb[3 * i + 2] = tgt[3 * j + 2];
             }
             Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
-            for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);  // the device applies Ts next launch
-            fin = bg::mul(Ts, fin);
             ++it;
+            // the next iteration goes out before this one's bookkeeping and convergence test (PCL
+            // decides after the step); if the test stops the loop, that launch is never read
+            if (it < max_iter)
+                if (int e = launch_it(it, Ts)) return e;
+            for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);  // the device applies Ts too
+            fin = bg::mul(Ts, fin);
             if (it >= max_iter) break;
             const double cos_angle = 0.5 * (double)(((Ts.m[0] + Ts.m[5]) + Ts.m[10]) - 1.0f);
             const double tsq = (double)((Ts.m[3] * Ts.m[3] + Ts.m[7] * Ts.m[7]) + Ts.m[11] * Ts.m[11]);
