@@ -23,6 +23,9 @@ import time
 
 import numpy as np
 
+# the library's copy-engine setting (b-shot-slam_amd/bshot_py.py), before anything initialises HIP
+os.environ.setdefault("GPU_FORCE_BLIT_COPY_SIZE", "256")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "b-shot-slam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
