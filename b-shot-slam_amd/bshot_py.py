@@ -9,13 +9,6 @@ import os
 
 import numpy as np
 
-# Host<->device copies up to 256 KB by blit kernels instead of the SDMA copy engines (read by the
-# HIP runtime when it initialises, so before the first GPU call): the per-sweep copies are small,
-# and on the SDMA path about half of the 20-sweep runs caught a 6-18 ms GPU-wide stall
-# (profiles/r02h_stalls.txt: 0 of 6 runs stalled with blit copies, 4 of 6 by default; 468 vs 452
-# sweeps/s over 200 sweeps). An explicit setting in the environment wins.
-os.environ.setdefault("GPU_FORCE_BLIT_COPY_SIZE", "256")
-
 HERE = os.path.dirname(os.path.abspath(__file__))
 # BSHOT_LIB: diagnostic override (timing experiments on `make variant` builds)
 LIB_PATH = os.environ.get("BSHOT_LIB") or os.path.join(HERE, "lib", "libbshot_amd.so")

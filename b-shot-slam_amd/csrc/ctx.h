@@ -134,15 +134,9 @@ struct bshot_ctx {
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
     int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
-    int opt_ransac_zc = 0;      // RANSAC scores read/written in pinned host memory (one queue entry; A/B even)
     int opt_side_prio = 0;      // describe (side) stream priority: 0 low (as SR/ISS ahead), 1 middle, 2 the main stream's
-    int opt_hist_fused = 8;     // SHOT records computed and applied in one kernel: waves per workgroup (0: contrib + apply)
-    int opt_sr_tile = 0;        // SR cell tiles: ladder level of a tile's cell (0: one query per wave; tiled measured slower)
-    int opt_sr_tile_q = 128;    // tiled SR: queries a workgroup takes before it retires
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
-    int opt_side_reserve = 0;   // CUs the side stream may not use (0: plain low-priority stream)
-    bool side_shared = false;   // side/pre/iss streams from the process-wide CU-masked pool (never destroyed)
 
     DBuf<int> errw;  // describe-stage error bits (normals)
 
@@ -167,8 +161,6 @@ struct bshot_ctx {
     DBuf<int4> plan;
     DBuf<int> cb, owner, okf, signs, perm;
     DBuf<double> csum, eig;
-    DBuf<unsigned short> recS;
-    DBuf<float> recV;
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)
     bsh::PreState* prep = nullptr;  // GPU preprocessor state (csrc/preprocess.hip), created on first use
@@ -179,7 +171,6 @@ struct bshot_ctx {
     PinBuf<int> p_kidx;
     PinBuf<float> p_kps3;
     int opt_chunk_blocks = 0;  // grid cap of the 64-rank chunk kernels (0: one block per 4 chunks)
-    int opt_dev_plan = 1;      // describe planned on the device (no mid-describe host sync) once sizes are known
     bool plan_on_host = false;  // next describe: plan on the host (after a device-plan overflow)
     long long seg_hint = 0;     // largest neighbourhood total seen (device-plan capacities)
     int ladder_mode(const CloudState& s) const { return s.fine_ladder ? (opt_ladder_front ? 2 : 1) : 0; }
@@ -209,7 +200,6 @@ struct bshot_ctx {
     PinBuf<bsh::IcpState> p_istate;
     int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
     int opt_topk_thread = 1;   // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
-    int opt_queue_thread = 0;  // LidarOdometry: the queued sweep's grids/SR/ISS launches issued from their own host thread
     int opt_pre_fast = 1;  // preprocessor: one 32-bit sort for azimuth-ordered lasers with tabled verticals
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
     int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
@@ -236,7 +226,8 @@ struct bshot_ctx {
     // streams' work)
     PinBuf<uint32_t> p_a, p_bits;
     PinBuf<int> p_left, p_gidx, p_err;
-    PinBuf<float> p_g3, p_src, p_tgt;
+    PinBuf<float> p_g3, p_src, p_tgt, p_xyz;
+    hipEvent_t ev_xyz = nullptr;  // the staged host cloud (p_xyz) has been copied
     PinBuf<unsigned long long> p_best;
     PinBuf<long long> p_i64;
 

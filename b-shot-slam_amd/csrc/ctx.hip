@@ -122,52 +122,18 @@ void bshot_ctx::resolve_events(bool wait) {
 
 namespace bsh {
 
-// The three low-priority streams (side: lookahead describe, pre: queued grids + SR, iss) are
-// restricted to all but opt_side_reserve CUs, which stay free for the main stream's short
-// latency-critical kernels (match, RANSAC, ICP). The reserved CUs are i = 33 m mod ncu,
-// m < reserve: that covers every residue mod 8 and every block of 32, so every XCD keeps some
-// whichever way the CU mask is numbered. CU-masked streams are created once per (device, reserve,
-// role) and shared for the process lifetime: destroying one was seen to hang intermittently
-// (ROCm 7.2), so they are never destroyed.
-static hipStream_t masked_stream(int device, int ncu, int reserve, int role) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, int>, hipStream_t> pool;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = pool.find({device, reserve, role});
-    if (it != pool.end()) return it->second;
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
-    for (int m = 0; m < reserve; ++m) {
-        const int i = (33 * m) % ncu;
-        mask[i / 32] &= ~(1u << (i % 32));
-    }
-    hipStream_t st = nullptr;
-    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
-    pool[{device, reserve, role}] = st;
-    return st;
-}
-
+// The three low-priority streams (side: lookahead describe, pre: queued grids + SR, iss) run
+// beside the high-priority main stream, whose short kernels (match, RANSAC, ICP) are the odometry
+// chain's critical path. (Reserving CUs for the main stream with CU-masked side streams measured
+// slower, 288 vs 380 sweeps/s, and its pruned code is in experiments/r03_pruned_variants.patch.)
 int ctx_make_side_stream(bshot_ctx* c) {
     hipStream_t* sts[3] = {&c->side, &c->pre, &c->iss};
     for (hipStream_t* p : sts) {
-        if (*p && !c->side_shared) {
+        if (*p) {
             (void)hipStreamSynchronize(*p);
             (void)hipStreamDestroy(*p);
         }
         *p = nullptr;
-    }
-    c->side_shared = false;
-    hipDeviceProp_t prop;
-    int ncu = 0;
-    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) ncu = prop.multiProcessorCount;
-    if (c->opt_side_reserve > 0 && ncu > 0 && ncu - c->opt_side_reserve >= 8) {
-        bool ok = true;
-        for (int r = 0; r < 3; ++r) ok = ok && (*sts[r] = masked_stream(c->device, ncu, c->opt_side_reserve, r)) != nullptr;
-        if (ok) {
-            c->side_shared = true;
-            return BSHOT_OK;
-        }
-        for (hipStream_t* p : sts) *p = nullptr;
     }
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
@@ -226,17 +192,16 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.ratio.ensure(n > 0 ? n : 1), "alloc ratio");
     HIPCHK(s.h_ratio.ensure(n > 0 ? n : 1), "alloc pinned ratio");
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
-    HIPCHK(hipMemsetAsync(s.errw.p, 0, sizeof(int), st), "memset err");
+    HIPCHK(kfill(s.errw.p, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks, c->opt_sr_tile,
-                                c->opt_sr_tile_q),
+                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks),
                "seg_ratio launch");
         c->stage_end(sg2, st);
-        HIPCHK(hipMemcpyAsync(s.h_ratio.p, s.ratio.p, sizeof(float) * n, hipMemcpyDeviceToHost, st), "D2H ratio");
+        HIPCHK(kcopy(s.h_ratio.p, s.ratio.p, sizeof(float) * n, st), "D2H ratio");
     }
-    HIPCHK(hipMemcpyAsync(s.h_err.p, s.errw.p, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
+    HIPCHK(kcopy(s.h_err.p, s.errw.p, sizeof(int), st), "D2H err");
     HIPCHK(hipEventRecord(s.ev_sr, st), "record sr");
     s.sr_state = 1;
     return BSHOT_OK;
@@ -252,7 +217,7 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.issnmc.ensure(n > 0 ? n : 1), "alloc iss nms counts");
     HIPCHK(s.h_flag.ensure(n > 0 ? n : 1), "alloc pinned flags");
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
-    HIPCHK(hipMemsetAsync(s.errw.p + 1, 0, sizeof(int), st), "memset err");
+    HIPCHK(kfill(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
         HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient * (float)c->opt_iss_cell, s.pts4.p, st, false),
@@ -264,9 +229,9 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
                "iss launch");
         c->stage_end(sg3, st);
         c->hmark("Q_iss_k");
-        HIPCHK(hipMemcpyAsync(s.h_flag.p, s.issflag.p, n, hipMemcpyDeviceToHost, st), "D2H iss");
+        HIPCHK(kcopy(s.h_flag.p, s.issflag.p, n, st), "D2H iss");
     }
-    HIPCHK(hipMemcpyAsync(s.h_err.p + 1, s.errw.p + 1, sizeof(int), hipMemcpyDeviceToHost, st), "D2H err");
+    HIPCHK(kcopy(s.h_err.p + 1, s.errw.p + 1, sizeof(int), st), "D2H err");
     HIPCHK(hipEventRecord(s.ev_iss, st), "record iss");
     s.iss_state = 1;
     return BSHOT_OK;
@@ -406,7 +371,7 @@ int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k) {
     c->normals_snap_n = m;
     if (m > 0) {
         HIPCHK(c->normals_snap.ensure(m), "alloc normals snapshot");
-        HIPCHK(hipMemcpyAsync(c->normals_snap.p, c->normals.p, sizeof(float4) * m, hipMemcpyDeviceToDevice, st),
+        HIPCHK(kcopy(c->normals_snap.p, c->normals.p, sizeof(float4) * m, st),
                "snapshot normals");
     }
     return BSHOT_OK;
@@ -415,8 +380,7 @@ int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k) {
 int ctx_normals_restore(bshot_ctx* c) {
     if (c->normals_snap_size < 0) return BSHOT_OK;
     if (c->normals_snap_n > 0)
-        HIPCHK(hipMemcpyAsync(c->normals.p, c->normals_snap.p, sizeof(float4) * c->normals_snap_n,
-                              hipMemcpyDeviceToDevice, c->stream),
+        HIPCHK(kcopy(c->normals.p, c->normals_snap.p, sizeof(float4) * c->normals_snap_n, c->stream),
                "restore normals");
     c->normals_size = c->normals_snap_size;
     c->normals_snap_size = -1;
@@ -433,14 +397,14 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     // persistent normals array: resize(n) keeps [0, min) and value-initialises new slots
     HIPCHK(c->normals.ensure(std::max(n, std::max(k, 1))), "alloc normals");
     if (n > c->normals_size)
-        HIPCHK(hipMemsetAsync(c->normals.p + c->normals_size, 0, sizeof(float4) * (n - c->normals_size), st),
+        HIPCHK(kfill(c->normals.p + c->normals_size, 0, sizeof(float4) * (n - c->normals_size), st),
                "zero normals");
     c->normals_size = n;
     if (k <= 0) return BSHOT_OK;
     // errw: [0] error bits (2 normals overflow, 8 sort piece overflow, 16 device plan over
     // capacity), [2..3] the neighbourhood total as planned on the device
     HIPCHK(c->errw.ensure(4), "alloc err");
-    HIPCHK(hipMemsetAsync(c->errw.p, 0, 4 * sizeof(int), st), "memset err");
+    HIPCHK(kfill(c->errw.p, 0, 4 * sizeof(int), st), "memset err");
     HIPCHK(c->counts.ensure(k), "alloc counts");
     HIPCHK(c->offs.ensure(k + 1), "alloc offs");
     HIPCHK(c->rf.ensure(9 * (size_t)k), "alloc rf");
@@ -456,7 +420,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     const int sg5 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
     HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
     HIPCHK(c->sbst.ensure(1024 * (size_t)k), "alloc bucket starts");
-    if (c->opt_dev_plan && !c->plan_on_host && k <= 8192 && c->seg_hint > 0) {
+    if (!c->plan_on_host && k <= 8192 && c->seg_hint > 0) {
         // the whole describe queued without a host round trip: the plan (segment offsets, chunk
         // bases, LPT order) is computed on the device against capacities sized from the largest
         // neighbourhood total seen so far (+25%); an overflow (errw bit 16) makes the caller
@@ -474,10 +438,6 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
         HIPCHK(c->okf.ensure(k), "alloc okf");
         HIPCHK(c->signs.ensure(2 * (size_t)chunk_cap), "alloc signs");
-        if (!c->opt_hist_fused) {  // the fused SHOT kernel keeps its records in LDS
-            HIPCHK(c->recS.ensure(320 * (size_t)chunk_cap), "alloc records");
-            HIPCHK(c->recV.ensure(320 * (size_t)chunk_cap), "alloc records");
-        }
         HIPCHK(launch_shot_count_plan(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->sbh.p, seg_cap, chunk_cap,
                                       c->offs.p, c->cb.p, c->perm.p, c->errw.p, st),
                "shot count + plan");
@@ -492,11 +452,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p;
         A.pts4 = S.pts4.p; A.normals = c->normals.p;
         A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
-        A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
+        A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p;
         A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
         A.bstart = c->sbst.p;
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
-        A.hist_fused = c->opt_hist_fused;
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
@@ -512,7 +471,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(launch_shot_count(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->offs.p, st, c->sbh.p), "shot count");
     c->stage_end(sg5, st);
     HIPCHK(c->p_offs.ensure((size_t)k + 1), "alloc pinned offs");
-    HIPCHK(hipMemcpyAsync(c->p_offs.p, c->offs.p, sizeof(long long) * ((size_t)k + 1), hipMemcpyDeviceToHost,
+    HIPCHK(kcopy(c->p_offs.p, c->offs.p, sizeof(long long) * ((size_t)k + 1),
                           st),
            "D2H offs");
     HIPCHK(hipStreamSynchronize(st), "sync offs");
@@ -552,22 +511,17 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
     HIPCHK(c->okf.ensure(k), "alloc okf");
     HIPCHK(c->signs.ensure(2 * (size_t)(cbr > 0 ? cbr : 1)), "alloc signs");  // per-chunk sign counts
-    if (!c->opt_hist_fused) {
-        HIPCHK(c->recS.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
-        HIPCHK(c->recV.ensure(320 * (size_t)(cbr > 0 ? cbr : 1)), "alloc records");
-    }
     HIPCHK(c->perm.ensure(k), "alloc perm");
-    HIPCHK(hipMemcpyAsync(c->cb.p, hcb, sizeof(int) * ((size_t)k + 1), hipMemcpyHostToDevice, st), "H2D cb");
-    HIPCHK(hipMemcpyAsync(c->perm.p, hperm, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D perm");
+    HIPCHK(kcopy(c->cb.p, hcb, sizeof(int) * ((size_t)k + 1), st), "H2D cb");
+    HIPCHK(kcopy(c->perm.p, hperm, sizeof(int) * k, st), "H2D perm");
     Describe2Args A;
     A.k = k; A.n_plan = n_plan; A.n_chunks = cbr; A.R = R;
     A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p; A.pts4 = S.pts4.p; A.normals = c->normals.p;
     A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
-    A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p; A.recS = c->recS.p; A.recV = c->recV.p;
+    A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p;
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
     A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
-    A.hist_fused = c->opt_hist_fused;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -608,7 +562,7 @@ int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx,
     if (k <= 0) return BSHOT_OK;
     HIPCHK(c->p_gidx.ensure(k), "alloc pinned idx");
     std::memcpy(c->p_gidx.p, h_idx, sizeof(int) * k);
-    HIPCHK(hipMemcpyAsync(c->gidx.p, c->p_gidx.p, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D idx");
+    HIPCHK(kcopy(c->gidx.p, c->p_gidx.p, sizeof(int) * k, st), "H2D idx");
     HIPCHK(launch_gather(S.pts4.p, c->gidx.p, k, dst.p, st), "gather");
     return BSHOT_OK;
 }
@@ -622,7 +576,7 @@ int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h
     int rc = ctx_gather_on(c, S, st, h_idx, k, dst);
     if (rc || k <= 0) return rc;
     HIPCHK(c->p_g3.ensure(3 * (size_t)k), "alloc pinned gather");
-    HIPCHK(hipMemcpyAsync(c->p_g3.p, dst.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, st), "D2H gather");
+    HIPCHK(kcopy(c->p_g3.p, dst.p, sizeof(float) * 3 * k, st), "D2H gather");
     HIPCHK(hipStreamSynchronize(st), "sync gather");
     std::memcpy(out, c->p_g3.p, sizeof(float) * 3 * k);
     return BSHOT_OK;
@@ -638,9 +592,9 @@ int ctx_gather_kps_async(bshot_ctx* c, CloudState& S, hipStream_t st, const int*
     HIPCHK(c->p_kidx.ensure(k), "alloc pinned kidx");
     HIPCHK(c->p_kps3.ensure(3 * (size_t)k), "alloc pinned kps");
     std::memcpy(c->p_kidx.p, h_idx, sizeof(int) * k);
-    HIPCHK(hipMemcpyAsync(c->kidx.p, c->p_kidx.p, sizeof(int) * k, hipMemcpyHostToDevice, st), "H2D kidx");
+    HIPCHK(kcopy(c->kidx.p, c->p_kidx.p, sizeof(int) * k, st), "H2D kidx");
     HIPCHK(launch_gather(S.pts4.p, c->kidx.p, k, c->kps.p, st), "gather kps");
-    HIPCHK(hipMemcpyAsync(c->p_kps3.p, c->kps.p, sizeof(float) * 3 * k, hipMemcpyDeviceToHost, st), "D2H kps");
+    HIPCHK(kcopy(c->p_kps3.p, c->kps.p, sizeof(float) * 3 * k, st), "D2H kps");
     return BSHOT_OK;
 }
 
@@ -673,15 +627,14 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         HIPCHK(c->p_best.ensure(ns), "alloc pinned best");
         if (d_tgt) {
             std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
-            HIPCHK(hipMemcpyAsync(c->itgt3.p, d_tgt, sizeof(float) * 3 * (size_t)nt, hipMemcpyDeviceToDevice, c->stream),
+            HIPCHK(kcopy(c->itgt3.p, d_tgt, sizeof(float) * 3 * (size_t)nt, c->stream),
                    "icp targets");
-            HIPCHK(hipMemcpyAsync(c->itgt3.p + 3 * (size_t)nt, c->p_tgt.p + 3 * (size_t)nt, sizeof(float) * 3 * ns,
-                                  hipMemcpyHostToDevice, c->stream),
+            HIPCHK(kcopy(c->itgt3.p + 3 * (size_t)nt, c->p_tgt.p + 3 * (size_t)nt, sizeof(float) * 3 * ns, c->stream),
                    "H2D icp source");
         } else {
             std::memcpy(c->p_tgt.p, tgt, sizeof(float) * 3 * nt);
             std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
-            HIPCHK(hipMemcpyAsync(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * ((size_t)nt + ns), hipMemcpyHostToDevice,
+            HIPCHK(kcopy(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * ((size_t)nt + ns),
                                   c->stream),
                    "H2D icp points");
         }
@@ -689,9 +642,9 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         if (c->opt_icp_dev) {
             HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
             HIPCHK(c->ibest.ensure(2 * (size_t)ns), "alloc icp best");
-            HIPCHK(hipMemcpyAsync(c->isrc.p, d_src0, sizeof(float) * 3 * ns, hipMemcpyDeviceToDevice, c->stream),
+            HIPCHK(kcopy(c->isrc.p, d_src0, sizeof(float) * 3 * ns, c->stream),
                    "icp src");
-            HIPCHK(hipMemsetAsync(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
+            HIPCHK(kfill(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
             const bool use_grid = c->opt_icp_grid != 0;
             if (use_grid) {
                 const int mc = std::max(65536, 2 * nt);
@@ -711,7 +664,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             h.done = 0;
             h.max_iter = max_iter;
             h.pad = 0;
-            HIPCHK(hipMemcpyAsync(c->istate.p, c->p_istate.p, sizeof(IcpState), hipMemcpyHostToDevice, c->stream),
+            HIPCHK(kcopy(c->istate.p, c->p_istate.p, sizeof(IcpState), c->stream),
                    "H2D icp state");
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
             const int n_it = max_iter > 1 ? max_iter : 1;
@@ -729,7 +682,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                            "icp iteration");
             }
             c->stage_end(sg14);
-            HIPCHK(hipMemcpyAsync(c->p_istate.p, c->istate.p, sizeof(IcpState), hipMemcpyDeviceToHost, c->stream),
+            HIPCHK(kcopy(c->p_istate.p, c->istate.p, sizeof(IcpState), c->stream),
                    "D2H icp state");
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
             std::memcpy(T, h.fin, sizeof(float) * 16);
@@ -750,7 +703,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         } else {
             HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
             HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
-            HIPCHK(hipMemsetAsync(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
+            HIPCHK(kfill(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
         }
         // one launch per iteration: iteration j moves the source by the previous step's transform
         // (j > 0) and writes its NN keys to p_best[j & 1]
@@ -878,7 +831,8 @@ void bshot_destroy(bshot_ctx* c) {
     c->seg.release(); c->segtmp.release(); c->rf.release(); c->shot.release(); c->ok.release(); c->bits.release();
     c->ma.release(); c->lbest.release(); c->left.release();
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
-    c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release();
+    c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release(); c->p_xyz.release();
+    if (c->ev_xyz) (void)hipEventDestroy(c->ev_xyz);
     c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
     c->sbh.release(); c->sbst.release(); c->kidx.release(); c->p_kidx.release(); c->p_kps3.release();
     bsh::pre_free(c->prep);
@@ -889,11 +843,9 @@ void bshot_destroy(bshot_ctx* c) {
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
-    if (!c->side_shared) {
-        (void)hipStreamDestroy(c->side);
-        (void)hipStreamDestroy(c->iss);
-        (void)hipStreamDestroy(c->pre);
-    }
+    (void)hipStreamDestroy(c->side);
+    (void)hipStreamDestroy(c->iss);
+    (void)hipStreamDestroy(c->pre);
     flush_deferred_frees();  // buffers parked by regrowths (regrow.h)
     delete c;
 }
@@ -918,8 +870,16 @@ int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n) {
     // the current cloud's buffers may still be read by the side stream (its ISS)
     if (c->cs.iss_state == 1) HIPCHK(hipStreamWaitEvent(c->stream, c->cs.ev_iss, 0), "wait iss");
     HIPCHK(c->cs.xyz.ensure(3 * (size_t)(n > 0 ? n : 1)), "alloc xyz");
-    if (n > 0)
-        HIPCHK(hipMemcpyAsync(c->cs.xyz.p, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, c->stream), "H2D xyz");
+    if (n > 0) {
+        // staged through pinned memory and moved by a kernel (no copy engine); the staging buffer is
+        // refilled only after the previous cloud's copy has run
+        if (c->ev_xyz) HIPCHK(hipEventSynchronize(c->ev_xyz), "wait staged cloud");
+        else HIPCHK(hipEventCreateWithFlags(&c->ev_xyz, hipEventDisableTiming), "event");
+        HIPCHK(c->p_xyz.ensure(3 * (size_t)n), "alloc pinned xyz");
+        std::memcpy(c->p_xyz.p, xyz, sizeof(float) * 3 * n);
+        HIPCHK(kcopy(c->cs.xyz.p, c->p_xyz.p, sizeof(float) * 3 * n, c->stream), "H2D xyz");
+        HIPCHK(hipEventRecord(c->ev_xyz, c->stream), "record staged cloud");
+    }
     return ctx_set_cloud_dev(c, c->cs.xyz.p, n);
 }
 
@@ -1035,12 +995,12 @@ int bshot_match(bshot_ctx* c, const uint32_t* a, int na, const uint32_t* b, int 
     HIPCHK(c->p_left.ensure(2 * (size_t)na + nb), "alloc pinned match out");
     std::memcpy(c->p_a.p, a, sizeof(uint32_t) * 11 * na);
     std::memcpy(c->p_a.p + 11 * (size_t)na, b, sizeof(uint32_t) * 11 * nb);
-    HIPCHK(hipMemcpyAsync(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * ((size_t)na + nb), hipMemcpyHostToDevice,
+    HIPCHK(kcopy(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * ((size_t)na + nb),
                           c->stream),
            "H2D descriptors");
     int rc = ctx_match_dev(c, na, nb);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb), hipMemcpyDeviceToHost,
+    HIPCHK(kcopy(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb),
                           c->stream),
            "D2H match");
     HIPCHK(hipStreamSynchronize(c->stream), "sync match");
@@ -1133,29 +1093,20 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
-    else if (k == "ransac_zc") c->opt_ransac_zc = value ? 1 : 0;
-    else if (k == "hist_fused") c->opt_hist_fused = value < 0 ? 0 : (value == 1 ? 8 : value);  // 1: default width
-    else if (k == "sr_tile") c->opt_sr_tile = value < 0 ? 0 : (value > 3 ? 3 : value);
-    else if (k == "sr_tile_q") c->opt_sr_tile_q = value < 64 ? 64 : value;
     else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
     else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
-    else if (k == "queue_thread") c->opt_queue_thread = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
     else if (k == "pre_fast") c->opt_pre_fast = value ? 1 : 0;
     else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;
     else if (k == "chunk_blocks") c->opt_chunk_blocks = value < 0 ? 0 : value;
-    else if (k == "dev_plan") c->opt_dev_plan = value ? 1 : 0;
     else if (k == "timing_mask") c->timing_mask = (unsigned)value;
     else if (k == "dev_plan_hint") c->seg_hint = value < 0 ? 0 : value;  // tests: force / avoid a re-plan
     else if (k == "side_prio") {
         c->opt_side_prio = value < 0 ? 0 : (value > 2 ? 2 : value);
-        return bsh::ctx_make_side_stream(c);
-    } else if (k == "side_cu_reserve") {
-        c->opt_side_reserve = value < 0 ? 0 : value;
         return bsh::ctx_make_side_stream(c);
     }
     else return c->fail("bshot_set_option: unknown option " + k, BSHOT_EINVAL);

@@ -12,7 +12,6 @@
 //                 interpolation records of every neighbour into a double-buffered LDS batch while
 //                 one wave applies them in rank order to the LDS histogram (in-order ds_add_f32),
 //                 then L2 normalisation and B-SHOT bits
-//   k_hist_contrib + k_hist_apply: the same as two kernels, records through HBM (hist_fused=0)
 // Chunk c of keypoint q covers ranks [64 (c - cb[q]), ...) where cb is the exclusive scan of
 // ceil(n_q / 64) (k_desc_plan, or the host plan after an overflow).
 #include <hip/hip_runtime.h>
@@ -351,72 +350,6 @@ __device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, co
         }
 }
 
-// records of chunk c (64 ranks): recS[320 c + 64 j + r] = bin of slot j of rank r (u16),
-// recV[...] = its value; slot order = PCL's add order per neighbour (cos neighbour, radius,
-// inclination, azimuth, main bin); unused slots and padding ranks -> bin 360 with value +0
-__global__ void __launch_bounds__(256) k_hist_contrib(const float4* __restrict__ pts4,
-                                                      const float4* __restrict__ normals,
-                                                      const float* __restrict__ kps, int k, float R,
-                                                      const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                      const int* __restrict__ owner,
-                                                      const unsigned long long* __restrict__ seg,
-                                                      const float* __restrict__ rf_in, const int* __restrict__ ok_in,
-                                                      unsigned short* __restrict__ recS, float* __restrict__ recV) {
-    const int lane = lane_id();
-    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) [&]() {
-        const int q = owner[c];
-        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-        const long long o = offs[q];
-        const int n = (int)(offs[q + 1] - o);
-        const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
-        if (!(fin && ok_in[q] && n >= 5)) return;
-        const int i = (c - cb[q]) * 64 + lane;
-        unsigned short* rs = recS + (size_t)c * 320 + lane;  // slot-major chunk rows: [slot][64 ranks]
-        float* rv = recV + (size_t)c * 320 + lane;
-        if (i >= n) {
-            // padding ranks of the keypoint's last chunk: no-op records
-    #pragma unroll
-            for (int j = 0; j < 5; ++j) { rs[64 * j] = (unsigned short)360; rv[64 * j] = 0.f; }
-            return;
-        }
-        float rf[9];
-    #pragma unroll
-        for (int j = 0; j < 9; ++j) rf[j] = rf_in[9 * (size_t)q + j];
-        int bins[5];
-        float vals[5];
-        shot_records(pts4, normals, kx, ky, kz, R, rf, seg[o + i], bins, vals);
-        unsigned int bb[5];
-        float vv[5];
-    #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            bb[j] = bins[j] < 0 ? 360u : (unsigned)bins[j];
-            vv[j] = bins[j] < 0 ? 0.f : vals[j];
-        }
-    #pragma unroll
-        for (int j = 0; j < 5; ++j) { rs[64 * j] = (unsigned short)bb[j]; rv[64 * j] = vv[j]; }
-    }();
-}
-
-// wave per keypoint: records applied in rank order to the LDS histogram (lanes 0..4 own record
-// slots; one in-order ds_add_f32 per neighbour), then normalisation and binarisation. The LDS
-// float-atomic unit of a CU is the limiter (~3 cycles per lane-op), so blocks are launched in
-// descending neighbourhood size (perm, host-sorted) and the LDS reservation caps residency at
-// 4 keypoints per CU: the largest start first and smaller ones fill in as CUs free up.
-#ifndef HA_LDS_PAD
-#define HA_LDS_PAD 8192
-#endif
-#ifndef HA_SKIP
-#define HA_SKIP 0
-#endif
-// keypoints per wave: group g owns lanes 5g..5g+4 and its own LDS histogram, so one in-order
-// ds_add_f32 carries the records of HA_G keypoints (their adds never share an address). HA_G > 1
-// measured slower (the atomic unit, not instruction issue, is the limit)
-#ifndef HA_G
-#define HA_G 1
-#endif
-static_assert(5 * HA_G <= 64, "HA_G groups of 5 lanes must fit a wave");
-
 // normalizeHistogram + B-SHOT of one keypoint's histogram h (wave-uniform q, good)
 __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q, bool good, int lane,
                                             float* __restrict__ shot_out, unsigned int* __restrict__ bits_out) {
@@ -502,93 +435,12 @@ __device__ __forceinline__ bool apply_good(const float* __restrict__ kps, const 
     return fin && ok_in[q] && n >= 5;
 }
 
-// HA_G keypoints per wave (perm[HA_G * blockIdx.x + g]); launched with ceil(k / HA_G) blocks
-__global__ void __launch_bounds__(64) k_hist_apply(const float* __restrict__ kps, int k, const int* __restrict__ perm,
-                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                   const int* __restrict__ ok_in,
-                                                   const unsigned short* __restrict__ recS,
-                                                   const float* __restrict__ recV, float* __restrict__ shot_out,
-                                                   unsigned int* __restrict__ bits_out) {
-    __shared__ float hist[HA_G * 384];
-    __shared__ unsigned int gcode[88];
-    __shared__ float pad_[HA_LDS_PAD];  // residency cap (see above)
-    const int lane = lane_id();
-    const int g = lane / 5, slot = lane - 5 * g;
-    const int p0 = HA_G * blockIdx.x;
-    if (lane == 0 && perm[p0] < 0) pad_[0] = 0.f;
-    for (int j = lane; j < HA_G * 384; j += 64) hist[j] = 0.0f;
-    __builtin_amdgcn_wave_barrier();
-    // lane (g, slot) applies record slot `slot` of every rank of keypoint g, in rank order: one
-    // ds_add_f32 per rank with the 5 lanes of each group (distinct bins within a rank), so every
-    // bin sees its adds in PCL's order. A lane reads its slot's chunk rows straight from memory
-    // (64 bins as 32 dwords, 64 values), the next chunk's rows in flight while this one is applied.
-    int c0 = 0, nch = 0;
-    if (g < HA_G && p0 + g < k) {
-        const int q = perm[p0 + g];
-        if (apply_good(kps, offs, ok_in, q)) {
-            c0 = cb[q];
-            nch = cb[q + 1] - c0;
-        }
-    }
-    int tmax = nch;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) tmax = max(tmax, __shfl_xor(tmax, m, 64));
-    if (tmax > 0) {
-        float* hg = hist + 384 * (g < HA_G ? g : 0);
-        auto load = [&](int c, uint4* bw, float4* vw) {
-            const uint4* b4 = reinterpret_cast<const uint4*>(recS + (size_t)c * 320 + 64 * slot);
-            const float4* v4 = reinterpret_cast<const float4*>(recV + (size_t)c * 320 + 64 * slot);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) bw[u] = b4[u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) vw[u] = v4[u];
-        };
-        uint4 bw[8], nbw[8];
-        float4 vw[16], nvw[16];
-        if (nch > 0) load(c0, bw, vw);
-        for (int t = 0; t < tmax; ++t) {
-            const bool act = t < nch;
-            if (t + 1 < nch) load(c0 + t + 1, nbw, nvw);
-            if (act) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const unsigned int w[4] = {bw[u].x, bw[u].y, bw[u].z, bw[u].w};
-#pragma unroll
-                    for (int h = 0; h < 4; ++h) {
-                        const int r = 8 * u + 2 * h;  // ranks r, r + 1 of the chunk
-                        const float4 va = vw[r >> 2];
-                        const float v0 = (r & 3) == 0 ? va.x : va.z;
-                        const float v1 = (r & 3) == 0 ? va.y : va.w;
-#if HA_SKIP
-                        // no-op records (bin 360, +0) issue no LDS atomic
-                        if ((w[h] & 0xFFFFu) < 352u) atomicAdd(&hg[w[h] & 0xFFFFu], v0);
-                        if ((w[h] >> 16) < 352u) atomicAdd(&hg[w[h] >> 16], v1);
-#else
-                        atomicAdd(&hg[w[h] & 0xFFFFu], v0);
-                        atomicAdd(&hg[w[h] >> 16], v1);
-#endif
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) bw[u] = nbw[u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) vw[u] = nvw[u];
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_wave_barrier();
-    for (int gg = 0; gg < HA_G; ++gg) {
-        if (p0 + gg >= k) break;
-        const int q = perm[p0 + gg];
-        hist_finish(hist + 384 * gg, gcode, q, apply_good(kps, offs, ok_in, q), lane, shot_out, bits_out);
-    }
-}
-
-// Records and ordered apply fused (knob hist_fused): a workgroup per keypoint (LPT order); waves
-// 1..HF_B compute the interpolation records of HF_B chunks into an LDS batch (shot_records, as
-// k_hist_contrib) while wave 0 applies the previous batch in rank order (as k_hist_apply: one
-// in-order ds_add_f32 per rank on lanes 0..4), double-buffered, so the records never leave LDS.
+// Records and ordered apply fused: a workgroup per keypoint (LPT order); waves 1..HF_B compute the
+// interpolation records of HF_B chunks into an LDS batch (shot_records) while wave 0 applies the
+// previous batch in rank order (one in-order ds_add_f32 per rank on lanes 0..4: every bin sees its
+// adds in PCL's order), double-buffered, so the records never leave LDS. The CU's LDS float-atomic
+// unit (~3 cycles per lane-op) bounds the applying wave; keypoints launch in descending
+// neighbourhood size so the largest start first.
 template <int HF_WAVES>
 __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __restrict__ pts4,
                                                               const float4* __restrict__ normals,
@@ -702,21 +554,9 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
                                                       A.signs, A.rf, A.ok);
         return hipGetLastError();
     }
-    if (A.hist_fused) {
-        // hist_fused = waves per workgroup (1 applies, the rest produce records)
-#define HF_LAUNCH(W)                                                                                               \
-    bsk::k_hist_fused<W><<<A.k, 64 * W, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,    \
-                                                A.rf, A.ok, A.shot, A.bits)
-        if (A.hist_fused <= 4) HF_LAUNCH(4);
-        else if (A.hist_fused <= 8) HF_LAUNCH(8);
-        else HF_LAUNCH(16);
-#undef HF_LAUNCH
-        return hipGetLastError();
-    }
-    if (A.n_chunks > 0)
-        bsk::k_hist_contrib<<<cblocks, 256, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.offs, A.cb, A.owner,
-                                                     A.sorted, A.rf, A.ok, A.recS, A.recV);
-    bsk::k_hist_apply<<<(A.k + HA_G - 1) / HA_G, 64, 0, s>>>(A.kps, A.k, A.perm, A.offs, A.cb, A.ok, A.recS, A.recV, A.shot, A.bits);
+    // 8 waves per workgroup: 1 applies, 7 produce records
+    bsk::k_hist_fused<8><<<A.k, 64 * 8, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
+                                                 A.rf, A.ok, A.shot, A.bits);
     return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "kernels.h"
 #include "dev_common.h"
 #include "gmap.h"
 #include "umap_order.h"
@@ -491,7 +492,7 @@ static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s)
     if (e != hipSuccess) return e;
     note_regrow("gmap", sizeof(T) * c);
     if (used) {
-        e = hipMemcpyAsync(p, b.p, sizeof(T) * used, hipMemcpyDeviceToDevice, s);
+        e = kcopy(p, b.p, sizeof(T) * used, s);
         if (e != hipSuccess) return e;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
@@ -507,7 +508,7 @@ static int gmap_init(bshot_ctx* c, GMap& g) {
     g.tsize = 1u << 16;
     HIPCHK(g.tkey.ensure(g.tsize), "gmap table");
     HIPCHK(g.tval.ensure(g.tsize), "gmap table");
-    HIPCHK(hipMemsetAsync(g.tkey.p, 0xFF, sizeof(unsigned long long) * g.tsize, c->stream), "gmap table clear");
+    HIPCHK(kfill(g.tkey.p, 0xFF, sizeof(unsigned long long) * g.tsize, c->stream), "gmap table clear");
     g.blk_cap = 1 << 14;
     HIPCHK(g.blk.ensure(g.blk_cap), "gmap blocks");
     g.ipool_cap = (size_t)1 << 24;
@@ -517,7 +518,7 @@ static int gmap_init(bshot_ctx* c, GMap& g) {
     g.ipool_cap = g.ipool.cap;
     g.cpool_cap = g.cpool.cap;
     HIPCHK(g.ctr.ensure(GM_NCTR), "gmap counters");
-    HIPCHK(hipMemsetAsync(g.ctr.p, 0, sizeof(int) * GM_NCTR, c->stream), "gmap counters");
+    HIPCHK(kfill(g.ctr.p, 0, sizeof(int) * GM_NCTR, c->stream), "gmap counters");
     HIPCHK(g.p_ctr.ensure(GM_NCTR), "gmap pinned counters");
     std::memset(g.p_ctr.p, 0, sizeof(int) * GM_NCTR);
     g.slots = 0;
@@ -589,12 +590,12 @@ static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync) {
     HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
     HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
                                      c->stream), "gmap sort");
-    HIPCHK(hipMemsetAsync(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
+    HIPCHK(kfill(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
     bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, c->stream>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
     bsk::k_gmap_insert<<<std::min(k, 1024), GM_INS_T, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
     HIPCHK(hipGetLastError(), "gmap insert launch");
     g.slots += k;
-    HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");
+    HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, c->stream), "D2H map counters");
     if (sync) {
         HIPCHK(hipStreamSynchronize(c->stream), "sync map");
         if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > LDS image or pool)", BSHOT_ECAP);
@@ -621,12 +622,12 @@ int gmap_insert(bshot_ctx* c, const float* kps_host, const float* ratio_host, co
         HIPCHK(g.p_kin.ensure(4 * (size_t)k), "gmap pinned in");
         std::memcpy(g.p_kin.p, kps_host, sizeof(float) * 3 * k);
         std::memcpy(g.p_kin.p + 3 * (size_t)k, ratio_host, sizeof(float) * k);
-        HIPCHK(hipMemcpyAsync(g.kin.p, g.p_kin.p, sizeof(float) * 4 * k, hipMemcpyHostToDevice, c->stream), "H2D map in");
+        HIPCHK(kcopy(g.kin.p, g.p_kin.p, sizeof(float) * 4 * k, c->stream), "H2D map in");
         bsk::k_gmap_prep<<<(k + 255) / 256, 256, 0, c->stream>>>(g.kin.p, g.kin.p + 3 * (size_t)k, d_bits, k, xf(T),
                                                                  g.slots, dev_view(g), g.keys.p, g.vals.p);
         if ((rc = gmap_run_insert(c, g, k, true))) return rc;
     } else {
-        HIPCHK(hipMemcpyAsync(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, hipMemcpyDeviceToHost, c->stream), "D2H map counters");
+        HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, c->stream), "D2H map counters");
         HIPCHK(hipStreamSynchronize(c->stream), "sync map");
     }
     *map_size = g.p_ctr.p[GM_MEMBERS];
@@ -664,7 +665,7 @@ int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n)
     std::memset(g.p_hrec.p, 0, sizeof(float) * GM_REC_HDR);
     std::memcpy(g.p_hrec.p, &n, sizeof(int));
     if (n > 0) std::memcpy(g.p_hrec.p + GM_REC_HDR, rec, sizeof(float) * GM_REC_W * n);
-    HIPCHK(hipMemcpyAsync(g.hrec.p, g.p_hrec.p, sizeof(float) * per, hipMemcpyHostToDevice, c->stream), "H2D batch");
+    HIPCHK(kcopy(g.hrec.p, g.p_hrec.p, sizeof(float) * per, c->stream), "H2D batch");
     return gmap_insert_records(c, replica, g.hrec.p, n, true);
 }
 
@@ -688,7 +689,7 @@ static int query_count(bshot_ctx* c, GMap& g, const QueryBox& q) {
     bsk::k_gmap_qcount<<<(q.npos + 255) / 256, 256, 0, c->stream>>>(dev_view(g), q.x0, q.y0, q.z0, q.ny, q.nz, q.npos, cnt,
                                                                     cnt + q.npos);
     bsk::k_gmap_scan<<<1, 1024, 0, c->stream>>>(cnt, q.npos, cnt + 2 * q.npos, cnt + 3 * q.npos);
-    HIPCHK(hipMemcpyAsync(g.p_ctr.p + GM_QTOT, cnt + 3 * q.npos, sizeof(int), hipMemcpyDeviceToHost, c->stream),
+    HIPCHK(kcopy(g.p_ctr.p + GM_QTOT, cnt + 3 * q.npos, sizeof(int), c->stream),
            "D2H map total");
     g.q_active = true;
     return BSHOT_OK;
@@ -760,7 +761,7 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
         HIPCHK(g.p_refin.ensure(14 * (size_t)kref), "gmap pinned ref");
         std::memcpy(g.p_refin.p, ref_kps, sizeof(float) * 3 * kref);
         std::memcpy(g.p_refin.p + 3 * (size_t)kref, ref_bits, sizeof(unsigned int) * 11 * kref);
-        HIPCHK(hipMemcpyAsync(g.refin.p, g.p_refin.p, sizeof(float) * 14 * kref, hipMemcpyHostToDevice, c->stream),
+        HIPCHK(kcopy(g.refin.p, g.p_refin.p, sizeof(float) * 14 * kref, c->stream),
                "H2D ref");
         bsk::k_gmap_ref<<<(kref + 255) / 256, 256, 0, c->stream>>>(
             g.refin.p, reinterpret_cast<const unsigned int*>(g.refin.p + 3 * (size_t)kref), kref, xf(ref_pose),
@@ -809,7 +810,7 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
     if (na > 0) {
         HIPCHK(c->p_a.ensure(11 * (size_t)na), "alloc pinned descriptors");
         std::memcpy(c->p_a.p, a, sizeof(uint32_t) * 11 * na);
-        HIPCHK(hipMemcpyAsync(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * na, hipMemcpyHostToDevice, c->stream),
+        HIPCHK(kcopy(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * na, c->stream),
                "H2D descriptors");
     }
     int nb = 0;
@@ -823,14 +824,14 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
     GMap& g = *c->gmap;
     HIPCHK(g.p_tgt.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc pinned targets");
     if (nb > 0)
-        HIPCHK(hipMemcpyAsync(g.p_tgt.p, c->gtgt.p, sizeof(float) * 3 * nb, hipMemcpyDeviceToHost, c->stream),
+        HIPCHK(kcopy(g.p_tgt.p, c->gtgt.p, sizeof(float) * 3 * nb, c->stream),
                "D2H targets");
     const bool run = na > 0 && nb > 0;
     if (run) {
         HIPCHK(c->p_left.ensure(2 * (size_t)na + nb), "alloc pinned match out");
         rc = ctx_match_dev(c, na, nb);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb), hipMemcpyDeviceToHost,
+        HIPCHK(kcopy(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb),
                               c->stream),
                "D2H match");
     }

@@ -18,8 +18,6 @@ struct DevGrid {
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     bool alias = false;  // spts borrowed from another grid (nested ladder build)
-    int2* tiles = nullptr;  // ladder level-0 grid: SR tiles (start, count) of the sorted cloud
-    int* tctr = nullptr;    // [0] tile count, [1] tile fetch counter
 
     GridView view() const {
         GridView v;

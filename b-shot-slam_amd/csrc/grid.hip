@@ -12,6 +12,7 @@
 
 #include "dev_common.h"
 #include "grid.h"
+#include "kernels.h"
 #include "regrow.h"
 
 namespace bsk {
@@ -166,8 +167,6 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
         if ((e = hipMalloc(&g0.vals, sizeof(unsigned int) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.vals2, sizeof(unsigned int) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.spts, sizeof(float4) * g0.cap))) return e;
-        if ((e = hipMalloc(&g0.tiles, sizeof(int2) * g0.cap))) return e;
-        if ((e = hipMalloc(&g0.tctr, sizeof(int) * 2))) return e;
         size_t tb = 0;
         if ((e = rocprim::radix_sort_pairs(nullptr, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)g0.cap, 0, 63,
                                            s)))
@@ -235,7 +234,7 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
     size_t tb = g.tmp_bytes;
     if ((e = rocprim::radix_sort_pairs(g.tmp, tb, g.keys, g.keys2, g.vals, g.vals2, (unsigned)n, 0, 64, s))) return e;
     bsk::k_grid_clear<<<(g.H + B - 1) / B, B, 0, s>>>(g.table, g.H);
-    if ((e = hipMemsetAsync(g.ncells, 0, sizeof(int), s))) return e;
+    if ((e = kfill(g.ncells, 0, sizeof(int), s))) return e;
     bsk::k_grid_cells<<<(n + B - 1) / B, B, 0, s>>>(g.keys2, g.vals2, d_pts4, n, g.table, g.H - 1, g.spts, g.ncells);
     return hipGetLastError();
 }
@@ -243,7 +242,7 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
 void grid_free(DevGrid& g, bool defer) {
     if (g.alias) g.spts = nullptr;  // owned by the ladder's level-0 grid
     for (void* p : {(void*)g.keys, (void*)g.keys2, (void*)g.vals, (void*)g.vals2, (void*)g.spts, (void*)g.table,
-                    (void*)g.ncells, (void*)g.tiles, (void*)g.tctr, (void*)g.tmp}) {
+                    (void*)g.ncells, (void*)g.tmp}) {
         if (!p) continue;
         if (defer) defer_free(p, DEFER_DEVICE);  // a regrowth inside the sweep loop
         else (void)hipFree(p);

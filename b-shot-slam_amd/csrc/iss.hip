@@ -334,7 +334,7 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc, int* err,
                       hipStream_t s, int ovf_blocks, int nms_blocks) {
     if (n <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), s);
+    hipError_t e = kfill(ovf, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn,
                                                                              g21, g32, third, ovf, nml, nmc);

@@ -1,0 +1,102 @@
+// kcopy.hip -- copies and fills issued as kernels on the caller's stream.
+//
+// Every per-sweep transfer of the odometry loop is device<->device or between device memory and
+// the context's pinned staging buffers (hipHostMalloc: mapped into the GPU's address space), so a
+// kernel can move it with plain vector loads and stores. Doing so keeps the sweep loop off the
+// copy engines: with SDMA copies in the loop, about half of the 20-sweep runs carried one 6-18 ms
+// GPU-wide stall, gone whenever no copy engine was used (profiles/r02h_stalls.txt).
+// Kernel completion orders the data as a copy would: a stream wait, an event or a later kernel on
+// the same stream sees it, and host memory written here is visible to the host once it has
+// synchronised with the stream.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace bsk {
+
+#define KC_THREADS 256
+#define KC_MAX_BLOCKS 1024
+
+// dst/src 16-B aligned: uint4 body; the tail (bytes % 16) byte by byte
+__global__ void __launch_bounds__(KC_THREADS) k_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16,
+                                                       unsigned char* __restrict__ dtail,
+                                                       const unsigned char* __restrict__ stail, int ntail) {
+    const size_t stride = (size_t)gridDim.x * KC_THREADS;
+    for (size_t i = (size_t)blockIdx.x * KC_THREADS + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(KC_THREADS) k_copy4(unsigned int* __restrict__ dst, const unsigned int* __restrict__ src,
+                                                      size_t n4, unsigned char* __restrict__ dtail,
+                                                      const unsigned char* __restrict__ stail, int ntail) {
+    const size_t stride = (size_t)gridDim.x * KC_THREADS;
+    for (size_t i = (size_t)blockIdx.x * KC_THREADS + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(KC_THREADS) k_copy1(unsigned char* __restrict__ dst, const unsigned char* __restrict__ src,
+                                                      size_t n) {
+    const size_t stride = (size_t)gridDim.x * KC_THREADS;
+    for (size_t i = (size_t)blockIdx.x * KC_THREADS + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(KC_THREADS) k_fill16(uint4* __restrict__ dst, uint4 v, size_t n16,
+                                                       unsigned char* __restrict__ dtail, unsigned char b, int ntail) {
+    const size_t stride = (size_t)gridDim.x * KC_THREADS;
+    for (size_t i = (size_t)blockIdx.x * KC_THREADS + threadIdx.x; i < n16; i += stride) dst[i] = v;
+    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = b;
+}
+
+__global__ void __launch_bounds__(KC_THREADS) k_fill1(unsigned char* __restrict__ dst, unsigned char b, size_t n) {
+    const size_t stride = (size_t)gridDim.x * KC_THREADS;
+    for (size_t i = (size_t)blockIdx.x * KC_THREADS + threadIdx.x; i < n; i += stride) dst[i] = b;
+}
+
+}  // namespace bsk
+
+namespace bsh {
+
+static inline int kc_blocks(size_t units) {
+    const size_t b = (units + KC_THREADS - 1) / KC_THREADS;
+    return (int)(b < 1 ? 1 : (b > KC_MAX_BLOCKS ? KC_MAX_BLOCKS : b));
+}
+
+hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0 || dst == src) return hipSuccess;
+    if (!dst || !src) return hipErrorInvalidValue;
+    const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
+    unsigned char* d = static_cast<unsigned char*>(dst);
+    const unsigned char* p = static_cast<const unsigned char*>(src);
+    if ((a & 15) == 0) {
+        const size_t n16 = bytes / 16;
+        const int tail = (int)(bytes % 16);
+        bsk::k_copy16<<<kc_blocks(n16), KC_THREADS, 0, s>>>(reinterpret_cast<uint4*>(d), reinterpret_cast<const uint4*>(p),
+                                                            n16, d + 16 * n16, p + 16 * n16, tail);
+    } else if ((a & 3) == 0) {
+        const size_t n4 = bytes / 4;
+        const int tail = (int)(bytes % 4);
+        bsk::k_copy4<<<kc_blocks(n4), KC_THREADS, 0, s>>>(reinterpret_cast<unsigned int*>(d),
+                                                          reinterpret_cast<const unsigned int*>(p), n4, d + 4 * n4,
+                                                          p + 4 * n4, tail);
+    } else {
+        bsk::k_copy1<<<kc_blocks(bytes), KC_THREADS, 0, s>>>(d, p, bytes);
+    }
+    return hipGetLastError();
+}
+
+hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (!dst) return hipErrorInvalidValue;
+    unsigned char* d = static_cast<unsigned char*>(dst);
+    if (((uintptr_t)dst & 15) == 0) {
+        const unsigned int w = 0x01010101u * value;
+        const size_t n16 = bytes / 16;
+        bsk::k_fill16<<<kc_blocks(n16), KC_THREADS, 0, s>>>(reinterpret_cast<uint4*>(d), make_uint4(w, w, w, w), n16,
+                                                            d + 16 * n16, value, (int)(bytes % 16));
+    } else {
+        bsk::k_fill1<<<kc_blocks(bytes), KC_THREADS, 0, s>>>(d, value, bytes);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace bsh

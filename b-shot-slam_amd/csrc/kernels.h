@@ -6,12 +6,16 @@
 
 namespace bsh {
 
+// copies / fills as kernels on stream s (csrc/kcopy.hip): device memory and the pinned staging
+// buffers only (never pageable host memory). The sweep loop issues no copy-engine transfer.
+hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s);
+hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s);
+
 // g4: the radius-ladder grids (cells r/16, r/8, r/4, r/2 for ladder modes 1, 2; r/8, r/8, r/2, r/2
 // for mode 0), see ladder() in knn.hip
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst = nullptr, int max_blocks = 8192, int tile_level = 0,
-                            int tile_q = 128);
+                            unsigned long long* kst = nullptr, int max_blocks = 8192);
 hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float4* pts4, const float* kps, int k,
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
@@ -63,7 +67,6 @@ hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int
 // load-balanced SHOT (describe2.hip): in-bucket rank, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;
-    int hist_fused = 0;                    // records + ordered apply in one kernel (k_hist_fused): waves
     float R = 0.f;
     const int* cb = nullptr;               // k + 1 chunk offsets
     int* owner = nullptr;                  // keypoint of every chunk
@@ -80,8 +83,6 @@ struct Describe2Args {
     int* signs = nullptr;                     // 2 per chunk: sign counts (k_lrf_sign)
     float* rf = nullptr;
     int* ok = nullptr;
-    unsigned short* recS = nullptr;  // histogram records, slot-major per 64-rank chunk (320 per chunk)
-    float* recV = nullptr;
     float* shot = nullptr;
     unsigned int* bits = nullptr;
     int* err = nullptr;
@@ -91,10 +92,6 @@ struct Describe2Args {
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 
 // A10 RANSAC: score (inlier count) of every hypothesis (csrc/ransac.hip)
-// the scores from / into pinned host memory (one queue entry); nidx <= RANSAC_ZC_MAXN (LDS stage)
-#define RANSAC_ZC_MAXN 768
-hipError_t launch_ransac_score_zc(const float* h_pts, int nidx, const int* h_hyp, int nhyp, double thr2, int* h_cnt,
-                                  hipStream_t s);
 hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,
                                int* cnt, hipStream_t s);
 

@@ -191,12 +191,9 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
         // a step whose cube holds fewer than max_nn candidates cannot deliver: skipped unstreamed
         const bool went = for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             ++chunks;
-#ifndef SR_EXP
-#define SR_EXP 0
-#endif
-            if (!(SR_EXP & 4) && v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
+            if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
             const unsigned long long m = __ballot(v);
-            if (!(SR_EXP & 8) && v) {
+            if (v) {
                 const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
                 if (slot < KNN_CAP) L->list[slot] = knn_key(d2, idx);
@@ -244,7 +241,6 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
     if (need == 0) return true;
     const float sc0 = (float)KNN_NB / rs2;
 
-    if (SR_EXP & 2) { *sorted = L->list; return true; }
     // ---- fast path: every in-radius key is in L->list
     if (total <= KNN_CAP) {
         int Bmax = KNN_NB - 1;
@@ -571,8 +567,6 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
             const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
             if (!ok) {
                 if (lane == 0) atomicOr(err, 1);
-            } else if (SR_EXP & 1) {
-                out = (float)need;
             } else if (need > 0) {
                 out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
             }
@@ -583,250 +577,6 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
         }
         if (lane == 0) ratio[q] = out;
         __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// A1, cell-tiled: the queries of one level-L ladder cell (a tile: <= ST_T consecutive points of the
-// hierarchically sorted cloud) share each ladder step's candidates. Per step the workgroup looks up
-// the cells of grid gi[s] that can hold a point within rs of the tile's participating queries (the
-// tile's bounding box dilated by rs, cells pruned by box distance), stages their points in LDS, and
-// every query sweeps the staged set linearly -- no per-query hash lookups or L2 round trips. The
-// staged set contains every cell each query's own cube would stream (a superset,
-// and every point outside a query's cube fails d2 < rs^2 in float), so the in-radius keys, the
-// histogram and hence the selection are those of k_seg_ratio. A step whose region exceeds the LDS
-// capacity streams per query from the global grid as k_seg_ratio does.
-#define ST_WAVES 4
-#define ST_T 64
-#define ST_SCAP 2048
-#define ST_CCAP 512
-
-struct SrTileLds {
-    float4 stage[ST_SCAP];
-    unsigned int cst[ST_CCAP];
-    unsigned int coff[ST_CCAP + 1];
-    float4 qp[ST_T];
-    int qstart[ST_T];  // first ladder step of the query; -1 once its ratio is written
-    int plist[ST_T];   // queries taking part in the current step
-    float bb[6];       // their bounding box (lo xyz, hi xyz)
-    int wtot[ST_WAVES];
-    int np, nleft, pctr, tile, ntot;
-    KnnLds wl[ST_WAVES];
-};
-
-// cell cidx of the region [x0, x0 + nx) x ... on grid G: its spts run, or cnt = 0 when its box lies
-// farther than rs + 1 mm from the bounding box (double, as cand_lookup)
-__device__ __forceinline__ void region_cell(const GridView& G, double c, int x0, int y0, int z0, int ny, int nz,
-                                            int ncell, int cidx, const float* bb, double lim, unsigned int& st,
-                                            unsigned int& cnt) {
-    st = 0;
-    cnt = 0;
-    if (cidx >= ncell) return;
-    const int iz = cidx % nz, t = cidx / nz, iy = t % ny, ix = t / ny;
-    const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
-    const double bx0 = cx * c, by0 = cy * c, bz0 = cz * c;
-    double dx = 0, dy = 0, dz = 0;
-    if ((double)bb[3] < bx0) dx = bx0 - bb[3]; else if ((double)bb[0] > bx0 + c) dx = bb[0] - (bx0 + c);
-    if ((double)bb[4] < by0) dy = by0 - bb[4]; else if ((double)bb[1] > by0 + c) dy = bb[1] - (by0 + c);
-    if ((double)bb[5] < bz0) dz = bz0 - bb[5]; else if ((double)bb[2] > bz0 + c) dz = bb[2] - (bz0 + c);
-    if (dx * dx + dy * dy + dz * dz <= lim * lim) {
-        if (!grid_lookup(G, cell_key(cx, cy, cz), st, cnt)) cnt = 0;
-    }
-}
-
-__device__ __forceinline__ float wave_min_f(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
-}
-__device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    return v;
-}
-
-// tiles of the sorted cloud: runs of one level-L cell cut into chunks of <= T points. Points without a
-// ladder key (non-finite, or beyond the key range) are no query: their ratio is NaN, as k_seg_ratio's
-__global__ void k_sr_tiles(const unsigned long long* __restrict__ keys, const unsigned int* __restrict__ vals, int n,
-                           int L, int T, int2* __restrict__ tiles, int* __restrict__ tctr, float* __restrict__ ratio) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const unsigned long long k = keys[j];
-    if (k == BS_EMPTY_KEY) {
-        ratio[vals[j]] = __builtin_nanf("");
-        return;
-    }
-    const unsigned long long pk = k >> (3 * L);
-    if (j > 0 && (keys[j - 1] >> (3 * L)) == pk) return;
-    int lo = j + 1, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((keys[mid] >> (3 * L)) == pk) lo = mid + 1;
-        else hi = mid;
-    }
-    const int len = lo - j, m = (len + T - 1) / T;
-    const int base = atomicAdd(&tctr[0], m);
-    for (int i = 0; i < m; ++i) tiles[base + i] = make_int2(j + i * T, min(T, len - i * T));
-}
-
-// qmax: a workgroup takes tiles until it has handled qmax queries (short-lived workgroups let the
-// high-priority main stream's kernels onto the CUs); the grid covers n / qmax + 1 workgroups
-__global__ void __launch_bounds__(64 * ST_WAVES) k_seg_ratio_tiled(LadderGrids lg, const float4* __restrict__ spts,
-                                                                    const float4* __restrict__ pts4,
-                                                                    const int2* __restrict__ tiles, int* __restrict__ tctr,
-                                                                    int qmax, float radius, int max_nn, int sr_type,
-                                                                    int hint, float* __restrict__ ratio,
-                                                                    int* __restrict__ err) {
-    __shared__ SrTileLds S;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
-    KnnLds* L = &S.wl[wave];
-    float* fl = reinterpret_cast<float*>(L->list);
-    cand_init(&L->cand);
-    const int last = lg.nsteps - 1;
-    const float r2 = (float)((double)radius * (double)radius);
-    const int ntiles = tctr[0];
-    const float qnan = __builtin_nanf("");
-    int done_q = 0;
-    while (done_q < qmax) {
-        if (tid == 0) S.tile = atomicAdd(&tctr[1], 1);
-        __syncthreads();
-        const int t = S.tile;
-        if (t >= ntiles) break;
-        const int2 tl = tiles[t];
-        done_q += tl.y;
-        if (tid < tl.y) S.qp[tid] = spts[tl.x + tid];
-        __syncthreads();
-        for (int i = wave; i < tl.y; i += ST_WAVES) {
-            const float4 sp = S.qp[i];
-            const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
-            int st = -1;
-            if (!origin) st = hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
-            else if (lane == 0) ratio[__float_as_uint(sp.w)] = qnan;
-            if (lane == 0) S.qstart[i] = st;
-        }
-        __syncthreads();
-        for (int s = 0; s <= last; ++s) {
-            if (wave == 0) {
-                const int st = lane < tl.y ? S.qstart[lane] : -1;
-                const bool part = st >= 0 && st <= s;
-                const unsigned long long pm = __ballot(part);
-                if (part) S.plist[__builtin_amdgcn_mbcnt_hi((unsigned)(pm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)pm, 0u))] = lane;
-                const float4 q = lane < tl.y ? S.qp[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float inf = __builtin_inff();
-                const float lx = wave_min_f(part ? q.x : inf), ly = wave_min_f(part ? q.y : inf), lz = wave_min_f(part ? q.z : inf);
-                const float hx = wave_max_f(part ? q.x : -inf), hy = wave_max_f(part ? q.y : -inf), hz = wave_max_f(part ? q.z : -inf);
-                const int nleft = __popcll(__ballot(st >= 0));
-                if (lane == 0) {
-                    S.np = __popcll(pm);
-                    S.nleft = nleft;
-                    S.pctr = 0;
-                    S.bb[0] = lx; S.bb[1] = ly; S.bb[2] = lz; S.bb[3] = hx; S.bb[4] = hy; S.bb[5] = hz;
-                }
-            }
-            __syncthreads();
-            if (S.nleft == 0) break;
-            const int np = S.np;
-            if (np > 0) {
-                const float rs = s == last ? radius : radius * lg.frac[s];
-                const float rs2 = s == last ? r2 : (float)((double)rs * (double)rs);
-                const GridView& G = lg.g[lg.gi[s]];
-                const double c = (double)G.cell;
-                const int x0 = (int)floor(((double)S.bb[0] - rs) / c), x1 = (int)floor(((double)S.bb[3] + rs) / c);
-                const int y0 = (int)floor(((double)S.bb[1] - rs) / c), y1 = (int)floor(((double)S.bb[4] + rs) / c);
-                const int z0 = (int)floor(((double)S.bb[2] - rs) / c), z1 = (int)floor(((double)S.bb[5] + rs) / c);
-                const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
-                const long long ncl = (long long)nx * ny * nz;
-                bool staged = ncl <= ST_CCAP;
-                if (staged) {
-                    const int ncell = (int)ncl;
-                    const double lim = (double)rs + 1.0;
-                    unsigned int st0, cn0, st1, cn1;
-                    region_cell(G, c, x0, y0, z0, ny, nz, ncell, 2 * tid, S.bb, lim, st0, cn0);
-                    region_cell(G, c, x0, y0, z0, ny, nz, ncell, 2 * tid + 1, S.bb, lim, st1, cn1);
-                    int wt;
-                    const int ex = wave_excl_scan((int)(cn0 + cn1), wt);
-                    if (lane == 63) S.wtot[wave] = wt;
-                    __syncthreads();
-                    int base = 0, total = 0;
-#pragma unroll
-                    for (int w = 0; w < ST_WAVES; ++w) {
-                        base += w < wave ? S.wtot[w] : 0;
-                        total += S.wtot[w];
-                    }
-                    S.cst[2 * tid] = st0;
-                    S.cst[2 * tid + 1] = st1;
-                    S.coff[2 * tid] = (unsigned)(base + ex);
-                    S.coff[2 * tid + 1] = (unsigned)(base + ex + (int)cn0);
-                    if (tid == 0) S.coff[ST_CCAP] = (unsigned)total;
-                    __syncthreads();
-                    staged = total <= ST_SCAP;
-                    if (staged) {
-                        for (int f = tid; f < total; f += 64 * ST_WAVES) {
-                            // last cell k with coff[k] <= f (a non-empty one)
-                            int a = 0, b = ST_CCAP;
-                            while (b - a > 1) {
-                                const int m = (a + b) >> 1;
-                                if (S.coff[m] <= (unsigned)f) a = m;
-                                else b = m;
-                            }
-                            S.stage[f] = G.spts[S.cst[a] + ((unsigned)f - S.coff[a])];
-                        }
-                        if (tid == 0) S.ntot = total;
-                    }
-                    __syncthreads();
-                }
-                const int ntot = staged ? S.ntot : 0;
-                const float sc = (float)KNN_NB / rs2;
-                while (true) {
-                    int k = 0;
-                    if (lane == 0) k = atomicAdd(&S.pctr, 1);
-                    k = __shfl(k, 0, 64);
-                    if (k >= np) break;
-                    const int i = S.plist[k];
-                    const float4 sp = S.qp[i];
-                    hist_clear(L);
-                    int cnt = 0;
-                    auto cb = [&](bool v, float d2, unsigned int idx) {
-                        if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
-                        const unsigned long long m = __ballot(v);
-                        if (v) {
-                            const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                            if (slot < KNN_CAP) L->list[slot] = knn_key(d2, idx);
-                        }
-                        cnt += __popcll(m);
-                    };
-                    if (staged) {
-#pragma unroll 4
-                        for (int f0 = 0; f0 < ntot; f0 += 64) {
-                            const int f = f0 + lane;
-                            const float4 p = f < ntot ? S.stage[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-                            const float d2 = d2_flann(sp.x, sp.y, sp.z, p.x, p.y, p.z);
-                            cb(f < ntot && d2 < rs2, d2, __float_as_uint(p.w));
-                        }
-                    } else {
-                        for_candidates(G, &L->cand, sp.x, sp.y, sp.z, rs, rs2, cb, s == last ? 0 : max_nn);
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (cnt >= max_nn || s == last) {
-                        int need = 0;
-                        const unsigned long long* sorted = nullptr;
-                        float out = qnan;
-                        if (!knn_finish(lg, L, sp.x, sp.y, sp.z, radius, max_nn, s, cnt, &need, nullptr, 0ull, 0ull, &sorted)) {
-                            if (lane == 0) atomicOr(err, 1);
-                        } else if (need > 0) {
-                            out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
-                        }
-                        if (lane == 0) {
-                            ratio[__float_as_uint(sp.w)] = out;
-                            S.qstart[i] = -1;
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            __syncthreads();
-        }
     }
 }
 
@@ -923,20 +673,7 @@ static LadderGrids ladder(const DevGrid* const* g4, int mode) {
 
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst, int max_blocks, int tile_level, int tile_q) {
-    // cell-tiled kernel on the nested ladder grids (level-0 grid holds the sorted keys and tiles)
-    if (tile_level > 0 && ladder_mode >= 1 && !kst && g4[0]->tiles && n > 0) {
-        const DevGrid& g0 = *g4[0];
-        hipError_t e = hipMemsetAsync(g0.tctr, 0, sizeof(int) * 2, s);
-        if (e) return e;
-        const int L = tile_level > 3 ? 3 : tile_level;
-        bsk::k_sr_tiles<<<(n + 255) / 256, 256, 0, s>>>(g0.keys2, g0.vals2, n, L, ST_T, g0.tiles, g0.tctr, ratio);
-        const int q = tile_q < ST_T ? ST_T : tile_q;
-        const int blocks = n / q + 1;
-        bsk::k_seg_ratio_tiled<<<blocks, 64 * ST_WAVES, 0, s>>>(ladder(g4, ladder_mode), g0.spts, pts4, g0.tiles, g0.tctr, q,
-                                                                 radius, max_nn, sr_type, hint, ratio, err);
-        return hipGetLastError();
-    }
+                            unsigned long long* kst, int max_blocks) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     // fewer, longer-lived waves cost less dispatch; more, short-lived ones let high-priority

@@ -106,7 +106,7 @@ static bsk::HamDir ham_dir(const unsigned int* q, int nq, const unsigned int* r,
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s) {
     if (na <= 0 || nb <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(best, 0xFF, sizeof(unsigned long long) * ((size_t)na + nb), s);
+    hipError_t e = kfill(best, 0xFF, sizeof(unsigned long long) * ((size_t)na + nb), s);
     if (e != hipSuccess) return e;
     const bsk::HamDir d0 = ham_dir(a, na, b, nb, best), d1 = ham_dir(b, nb, a, na, best + na);
     dim3 grid(d0.qb > d1.qb ? d0.qb : d1.qb, d0.splits > d1.splits ? d0.splits : d1.splits, 2);

@@ -439,7 +439,7 @@ int pre_stage_lasers(bshot_ctx* c, const bshot_laser* lasers, int n, const bshot
     PCHK(P.lasers.ensure(n), "pre alloc lasers");
     PCHK(P.p_lasers.ensure(n), "pre alloc lasers");
     std::memcpy(P.p_lasers.p, lasers, sizeof(bshot_laser) * (size_t)n);
-    PCHK(hipMemcpyAsync(P.lasers.p, P.p_lasers.p, sizeof(bshot_laser) * (size_t)n, hipMemcpyHostToDevice, c->stream),
+    PCHK(kcopy(P.lasers.p, P.p_lasers.p, sizeof(bshot_laser) * (size_t)n, c->stream),
          "pre H2D lasers");
     *d_out = P.lasers.p;
     return BSHOT_OK;
@@ -520,13 +520,13 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
         PCHK(P.selm.ensure(n), "pre alloc sel");
         PCHK(P.p_sel.ensure(n), "pre alloc sel");
         std::memcpy(P.p_sel.p, P.h_sel.data(), (size_t)n);
-        PCHK(hipMemcpyAsync(P.selm.p, P.p_sel.p, (size_t)n, hipMemcpyHostToDevice, st), "pre H2D sel");
+        PCHK(kcopy(P.selm.p, P.p_sel.p, (size_t)n, st), "pre H2D sel");
         selm = P.selm.p;
     }
     if (J > 0) {
         PCHK(P.p_vj.ensure(J), "pre alloc");
         std::memcpy(P.p_vj.p, P.vj.data(), sizeof(double) * J);
-        PCHK(hipMemcpyAsync(P.d_vj.p, P.p_vj.p, sizeof(double) * J, hipMemcpyHostToDevice, st), "pre H2D vj");
+        PCHK(kcopy(P.d_vj.p, P.p_vj.p, sizeof(double) * J, st), "pre H2D vj");
     }
     const int sg = c->stage_begin(BSHOT_STAGE_PRE, st);
     const int B = 256, G = (n2 + B - 1) / B;
@@ -539,10 +539,10 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
         PCHK(P.fbad.ensure(1), "pre alloc"); PCHK(P.p_fbad.ensure(1), "pre alloc");
         PCHK(P.d_rtab.ensure(nr), "pre alloc"); PCHK(P.p_rtab.ensure(nr), "pre alloc");
         std::memcpy(P.p_rtab.p, P.rtab.data(), sizeof(double) * nr);
-        PCHK(hipMemcpyAsync(P.d_rtab.p, P.p_rtab.p, sizeof(double) * nr, hipMemcpyHostToDevice, st), "pre H2D ranks");
-        PCHK(hipMemsetAsync(P.fbad.p, 0, sizeof(int), st), "pre memset");
+        PCHK(kcopy(P.d_rtab.p, P.p_rtab.p, sizeof(double) * nr, st), "pre H2D ranks");
+        PCHK(kfill(P.fbad.p, 0, sizeof(int), st), "pre memset");
         bpk::k_pre_check<<<(n + B - 1) / B, B, 0, st>>>(d_lasers, n, P.d_rtab.p, nr, P.colflag.p, P.vrank.p, P.fbad.p);
-        PCHK(hipMemcpyAsync(P.p_fbad.p, P.fbad.p, sizeof(int), hipMemcpyDeviceToHost, st), "pre D2H check");
+        PCHK(kcopy(P.p_fbad.p, P.fbad.p, sizeof(int), st), "pre D2H check");
         PCHK(hipStreamSynchronize(st), "pre sync check");
         fast = P.p_fbad.p[0] == 0;
     }
@@ -579,7 +579,7 @@ int pre_read(bshot_ctx* c, const bshot_laser* d_lasers, int n, const double* ver
                                       P.colmin.p);
     bpk::k_pre_colaz<<<G, B, 0, st>>>(d_lasers, P.colmin.p, P.tot.p, n2, P.col_az.p);
     bpk::k_pre_pts<<<G, B, 0, st>>>(P.c_vr.p, P.c_dist.p, P.c_col.p, P.col_az.p, P.tot.p, n2, P.pts.p);
-    if (J > 0) PCHK(hipMemsetAsync(P.ph0.p, 0, sizeof(int) * J, st), "pre memset");
+    if (J > 0) PCHK(kfill(P.ph0.p, 0, sizeof(int) * J, st), "pre memset");
     c->stage_end(sg, st);
     PCHK(hipGetLastError(), "pre read launch");
     return BSHOT_OK;
@@ -636,7 +636,7 @@ int pre_write(bshot_ctx* c, float* d_xyz, int cap, int* n_out) {
     bpk::k_pre_write<<<G, B, 0, st>>>(P.pts.p, P.keep.p, P.offs.p, P.tot.p, n2, cap, d_xyz, P.tot.p + 2);
     c->stage_end(sg, st);
     PCHK(hipGetLastError(), "pre write launch");
-    PCHK(hipMemcpyAsync(P.p_tot.p, P.tot.p, sizeof(int) * 4, hipMemcpyDeviceToHost, st), "pre D2H count");
+    PCHK(kcopy(P.p_tot.p, P.tot.p, sizeof(int) * 4, st), "pre D2H count");
     PCHK(hipStreamSynchronize(st), "pre sync");
     c->resolve_events();
     P.cells = P.p_tot.p[0];
@@ -675,7 +675,7 @@ int pre_cells(bshot_ctx* c, std::vector<bshot_pre_cell>& out) {
     if (!c->prep) return BSHOT_OK;
     PreState& P = *c->prep;
     if (!P.counts_ok) {
-        PCHK(hipMemcpyAsync(P.p_tot.p, P.tot.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream), "pre D2H count");
+        PCHK(kcopy(P.p_tot.p, P.tot.p, sizeof(int) * 4, c->stream), "pre D2H count");
         PCHK(hipStreamSynchronize(c->stream), "pre sync");
         P.cells = P.p_tot.p[0];
         P.cols = P.p_tot.p[1];

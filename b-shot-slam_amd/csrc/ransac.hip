@@ -88,67 +88,9 @@ __global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score(const float* __r
     }
 }
 
-// Zero-copy variant for the odometry's main stream: the correspondence points and hypotheses are
-// read straight from the host's pinned staging buffers and the counts written back into pinned
-// memory, so the scoring is one queue entry instead of two uploads, the kernel and a download
-// (each of which waits for CUs behind the lookahead streams). A workgroup stages the points in LDS
-// once (one PCIe read of them per workgroup) and its waves stride over the hypotheses.
-__global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score_zc(const float* __restrict__ pts, int nidx,
-                                                                   const int* __restrict__ hyp, int nhyp,
-                                                                   double thr2, int* __restrict__ cnt) {
-    __builtin_amdgcn_s_setprio(3);  // main-stream kernel on the odometry chain's critical path
-    extern __shared__ float sp[];   // cs[3 nidx] then ct[3 nidx]
-    for (int i = threadIdx.x; i < 6 * nidx; i += 64 * RS_WAVES) sp[i] = pts[i];
-    __syncthreads();
-    const float* cs = sp;
-    const float* ct = sp + 3 * nidx;
-    const int lane = lane_id();
-    for (int h = blockIdx.x * RS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); h < nhyp; h += gridDim.x * RS_WAVES) {
-        double sd[9], td[9];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int p = hyp[3 * h + i];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                sd[3 * i + d] = (double)cs[3 * p + d];
-                td[3 * i + d] = (double)ct[3 * p + d];
-            }
-        }
-        double md[16];
-        bm::umeyama_seq<double>(sd, td, 3, md);
-        float T[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) T[i] = (float)md[i];
-        int c = 0;
-        for (int i = lane; i < nidx; i += 64) {
-            const float x = cs[3 * i], y = cs[3 * i + 1], z = cs[3 * i + 2];
-            const float px = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
-            const float py = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
-            const float pz = ((T[8] * x + T[9] * y) + T[10] * z) + T[11];
-            const float dx = px - ct[3 * i], dy = py - ct[3 * i + 1], dz = pz - ct[3 * i + 2];
-            const float d2 = (dx * dx + dz * dz) + (dy * dy + 0.0f);
-            c += (double)d2 < thr2 ? 1 : 0;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) cnt[h] = c;
-    }
-}
-
 }  // namespace bsk
 
 namespace bsh {
-
-hipError_t launch_ransac_score_zc(const float* h_pts, int nidx, const int* h_hyp, int nhyp, double thr2, int* h_cnt,
-                                  hipStream_t s) {
-    if (nhyp <= 0) return hipSuccess;
-    if (nidx > RANSAC_ZC_MAXN) return hipErrorInvalidValue;
-    int blocks = (nhyp + RS_WAVES - 1) / RS_WAVES;
-    if (blocks > 128) blocks = 128;
-    bsk::k_ransac_score_zc<<<blocks, 64 * RS_WAVES, sizeof(float) * 6 * (size_t)nidx, s>>>(h_pts, nidx, h_hyp, nhyp,
-                                                                                         thr2, h_cnt);
-    return hipGetLastError();
-}
 
 hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,
                                int* cnt, hipStream_t s) {

@@ -120,7 +120,7 @@ int velo_decode(bshot_ctx* c, const unsigned char* d_pk, const long long* d_ut, 
     size_t tb = 0;
     VCHK(rocprim::inclusive_scan(nullptr, tb, V.flag.p, V.scan.p, (size_t)nrec, rocprim::plus<int>(), st), "velo scan size");
     VCHK(V.tmp.ensure(tb), "velo alloc");
-    VCHK(hipMemsetAsync(V.tot.p, 0, sizeof(int) * 4, st), "velo memset");
+    VCHK(kfill(V.tot.p, 0, sizeof(int) * 4, st), "velo memset");
     const int B = 256, G = (nrec + B - 1) / B;
     const int sg = c->stage_begin(BSHOT_STAGE_PRE, st);
     bvk::k_velo_decode<<<G, B, 0, st>>>(d_pk, d_ut, nrec, max_lasers, V.az.p, d_rec, V.tot.p + 1);
@@ -130,7 +130,7 @@ int velo_decode(bshot_ctx* c, const unsigned char* d_pk, const long long* d_ut, 
     bvk::k_velo_starts<<<G, B, 0, st>>>(V.flag.p, V.scan.p, nrec, V.starts.p, V.tot.p);
     c->stage_end(sg, st);
     VCHK(hipGetLastError(), "velo launch");
-    VCHK(hipMemcpyAsync(V.p_starts.p, V.tot.p, sizeof(int) * 2, hipMemcpyDeviceToHost, st), "velo D2H");
+    VCHK(kcopy(V.p_starts.p, V.tot.p, sizeof(int) * 2, st), "velo D2H");
     VCHK(hipStreamSynchronize(st), "velo sync");
     const int splits = V.p_starts.p[0];
     if (V.p_starts.p[1]) return c->fail("velodyne decode: packet with a sensor type other than 0x21/0x22", BSHOT_EINVAL);
@@ -201,8 +201,8 @@ int bshot_velodyne_decode(bshot_ctx* c, const uint8_t* payloads, const int64_t* 
         return c->fail("velodyne decode: alloc", BSHOT_EHIP);
     std::memcpy(V.p_pk.p, payloads, nb);
     std::memcpy(V.p_ut.p, unixtime, sizeof(int64_t) * npk);
-    if (hipMemcpyAsync(V.pk.p, V.p_pk.p, nb, hipMemcpyHostToDevice, c->stream) ||
-        hipMemcpyAsync(V.ut.p, V.p_ut.p, sizeof(int64_t) * npk, hipMemcpyHostToDevice, c->stream))
+    if (bsh::kcopy(V.pk.p, V.p_pk.p, nb, c->stream) ||
+        bsh::kcopy(V.ut.p, V.p_ut.p, sizeof(int64_t) * npk, c->stream))
         return c->fail("velodyne decode: H2D", BSHOT_EHIP);
     std::vector<int> rs, rc;
     int e = bsh::velo_decode(c, V.pk.p, V.ut.p, npk, max_lasers, specified_frame, V.rec.p, rs, rc);

@@ -58,12 +58,6 @@ static int select_from_ratios(const float* h_ratio, int n, int k_want, std::vect
     return BSHOT_OK;
 }
 
-struct LidarOdometry::QueueAhead {
-    std::thread th;
-    std::string err;
-    std::shared_ptr<TopkAhead> topk;
-};
-
 struct LidarOdometry::Lookahead {
     const float* d_xyz = nullptr;
     int n = 0;
@@ -97,28 +91,11 @@ LidarOdometry::LidarOdometry(const bshot_params& p, int device)
 
 LidarOdometry::~LidarOdometry() {
     if (ahead_ && ahead_->th.joinable()) ahead_->th.join();
-    if (queue_ahead_ && queue_ahead_->th.joinable()) queue_ahead_->th.join();
-    if (queue_ahead_ && queue_ahead_->topk && queue_ahead_->topk->th.joinable()) queue_ahead_->topk->th.join();
     dropTopkAhead();
     bshot_destroy(ctx_);
 }
 
-// the queue thread (launches of the sweep after next) has to be done before the main thread looks
-// at the queue slot again; its top-K thread, if any, becomes topk_ahead_
-void LidarOdometry::joinQueue() {
-    if (!queue_ahead_) return;
-    if (queue_ahead_->th.joinable()) queue_ahead_->th.join();
-    auto q = queue_ahead_;
-    queue_ahead_.reset();
-    if (q->topk) topk_ahead_ = q->topk;
-    if (!q->err.empty()) {
-        err_ = q->err;
-        throw std::runtime_error(err_);
-    }
-}
-
 void LidarOdometry::drainLookahead() {
-    joinQueue();
     joinAhead();
     if (topk_ahead_ && topk_ahead_->th.joinable()) topk_ahead_->th.join();
 }
@@ -157,7 +134,6 @@ void LidarOdometry::check(int rc, const char* where) {
 void LidarOdometry::setSRType(std::string sr_type) {
     // a type change takes effect at the next extractKeypoints (as in the reference): sweeps already
     // prefetched or queued with the old type are dropped, after their threads are done
-    joinQueue();
     joinAhead();
     dropReady();
     dropTopkAhead();
@@ -174,7 +150,6 @@ void LidarOdometry::setRefFrame(Frame::Ptr ref) {
 }
 
 void LidarOdometry::setSrcFrame(Frame::Ptr src) {
-    joinQueue();
     joinAhead();
     dropReady();
     src_ = src;
@@ -186,7 +161,6 @@ void LidarOdometry::setSrcFrame(Frame::Ptr src) {
 
 void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n) {
     ctx_->hmark("M_frame");
-    joinQueue();
     joinAhead();
     ctx_->hmark("M_joined");
     if (ready_ && !(ready_->d_xyz == d_xyz && ready_->n == n)) dropReady();
@@ -198,7 +172,6 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
 }
 
 void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
-    joinQueue();
     joinAhead();
     dropReady();
     // grids + SR + ISS on the side stream (after everything already queued on the main stream,
@@ -226,9 +199,8 @@ void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
 
 void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
     // issued from the worker (after its describe) it started the sweep after next's SR too late and
-    // slowed the describe it then overlapped (measured 260 -> 237 sweeps/s); the main thread records
-    // the ordering event and a thread of its own issues the launches
-    joinQueue();
+    // slowed the describe it then overlapped (measured 260 -> 237 sweeps/s): the main thread issues
+    // the launches (a thread of their own only moved the wait, profiles/ab_queue_at.txt)
     dropTopkAhead();
     bshot_ctx* c = ctx_;
     const int kwant = prm_.num_keypoints;
@@ -258,27 +230,9 @@ void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
         });
         return tk;
     };
-    if (!c->opt_queue_thread) {
-        check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
-        ctx_->hmark("M_queued");
-        topk_ahead_ = start_topk();
-        return;
-    }
-    const int go = bsh::ctx_queue_begin(c, d_xyz, n);
-    check(go, "queueFrameDevice");
-    if (go == 0) return;
-    auto q = std::make_shared<QueueAhead>();
-    QueueAhead* p = q.get();
-    p->th = std::thread([p, c, d_xyz, n, start_topk]() {
-        if (bsh::ctx_queue_rest(c, d_xyz, n) != BSHOT_OK) {
-            p->err = std::string("queueFrameDevice: ") + c->err;
-            return;
-        }
-        c->hmark("Q_queued");
-        p->topk = start_topk();
-    });
-    queue_ahead_ = q;
+    check(bshot_queue_cloud_device(ctx_, d_xyz, n), "queueFrameDevice");
     ctx_->hmark("M_queued");
+    topk_ahead_ = start_topk();
 }
 
 // worker thread: the extract + describe half of the frame for the prefetched cloud (ctx->pf) on
@@ -337,9 +291,9 @@ void LidarOdometry::runAhead(Lookahead& la) {
         fail("alloc pinned");
     for (int attempt = 0; attempt < 3; ++attempt) {
         c->p_err.p[0] = 0;
-        if (k > 0 && (hipMemcpyAsync(c->p_bits.p, c->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
+        if (k > 0 && (bsh::kcopy(c->p_bits.p, c->bits.p, sizeof(uint32_t) * 11 * k,
                                      c->side) != hipSuccess ||
-                      hipMemcpyAsync(c->p_err.p, c->errw.p, 4 * sizeof(int), hipMemcpyDeviceToHost, c->side) !=
+                      bsh::kcopy(c->p_err.p, c->errw.p, 4 * sizeof(int), c->side) !=
                           hipSuccess))
             fail("D2H bits");
         if (hipStreamSynchronize(c->side) != hipSuccess) fail("lookahead sync");
@@ -458,9 +412,9 @@ void LidarOdometry::computeDescriptors() {
     for (int attempt = 0; attempt < 3; ++attempt) {
         ctx_->p_err.p[0] = 0;
         if (k > 0) {
-            if (hipMemcpyAsync(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k, hipMemcpyDeviceToHost,
+            if (bsh::kcopy(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k,
                                ctx_->stream) != hipSuccess ||
-                hipMemcpyAsync(ctx_->p_err.p, ctx_->errw.p, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx_->stream) !=
+                bsh::kcopy(ctx_->p_err.p, ctx_->errw.p, 4 * sizeof(int), ctx_->stream) !=
                     hipSuccess)
                 check(BSHOT_EHIP, "D2H bits");
         }
@@ -725,7 +679,6 @@ void LidarOdometry::kpEvaluation() {
 PointCloudXYZ LidarOdometry::issKpDetection(const PointCloudXYZ& kps) {
     // standalone ISS over an arbitrary cloud (src/lidar_odometry.cpp:447-461); the lookahead threads
     // finish first (they issue on the context's streams), their prefetched results stay valid
-    joinQueue();
     joinAhead();
     const int n = (int)kps.size();
     check(bshot_set_cloud(ctx_, n ? kps.data()->v : nullptr, n), "iss set cloud");

@@ -164,14 +164,12 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
         std::memcpy(c->p_rpts.p + 3 * nidx, ct.data(), sizeof(float) * 3 * nidx);
         std::memcpy(c->p_rhyp.p, spos.data(), sizeof(int) * 3 * nhyp);
         const int sg = c->stage_begin(BSHOT_STAGE_RANSAC);
-        if (c->opt_ransac_zc && nidx <= RANSAC_ZC_MAXN) {
-            if (bsh::launch_ransac_score_zc(c->p_rpts.p, nidx, c->p_rhyp.p, nhyp, thr2, c->p_rcnt.p, c->stream))
-                return c->fail("ransac: launch", BSHOT_EHIP);
-        } else if (hipMemcpyAsync(c->rpts.p, c->p_rpts.p, sizeof(float) * np, hipMemcpyHostToDevice, c->stream) ||
-            hipMemcpyAsync(c->rhyp.p, c->p_rhyp.p, sizeof(int) * 3 * nhyp, hipMemcpyHostToDevice, c->stream) ||
+        // kernel copies from / into the pinned staging buffers (csrc/kcopy.hip): no copy engine
+        if (bsh::kcopy(c->rpts.p, c->p_rpts.p, sizeof(float) * np, c->stream) ||
+            bsh::kcopy(c->rhyp.p, c->p_rhyp.p, sizeof(int) * 3 * nhyp, c->stream) ||
             bsh::launch_ransac_score(c->rpts.p, c->rpts.p + 3 * nidx, nidx, c->rhyp.p, nhyp, thr2, c->rcnt.p,
                                      c->stream) ||
-            hipMemcpyAsync(c->p_rcnt.p, c->rcnt.p, sizeof(int) * nhyp, hipMemcpyDeviceToHost, c->stream))
+            bsh::kcopy(c->p_rcnt.p, c->rcnt.p, sizeof(int) * nhyp, c->stream))
             return c->fail("ransac: launch", BSHOT_EHIP);
         c->stage_end(sg);
         gpu_launched = true;

@@ -4,7 +4,9 @@
 // Scene (world frame, mm): ground z=-1730; facade rows at x=+-9000 in segments separated by cross
 // streets, with recessed windows (300 mm) and doors (500 mm); a back row of buildings at
 // x=+-35000; poles r=150 every 12 m at x=+-7000; parked cars (1800x4500x1500 boxes) at x=+-3600;
-// trees (spheres r~1500) at x=+-6000. Sensor pose at frame t: yaw_t = 0.5deg*sin(2*pi*t/200),
+// trees (spheres r~1500) at x=+-6000. Scene seeds with bit 31 set select an aperiodic variant
+// (diagnostic, tests/diag/config3_diag.py): pole spacing 6-18 m instead of 12 m, and each 4 m
+// facade cell draws its own window presence, width and height from a hash. Sensor pose at frame t: yaw_t = 0.5deg*sin(2*pi*t/200),
 // position (0, 800*t, 0). Returns: nearest hit, range < max_range, range noise N(0, 20 mm)
 // quantised to 2 mm (src/preprocess.cpp:45-46 uses 2 mm ticks). Output order: azimuth-major,
 // vertical-ascending (mimics src/preprocess.cpp:201-215). Points are in the sensor frame.
@@ -35,7 +37,9 @@ static inline double u01(uint64_t h) { return ((h >> 11) + 0.5) * (1.0 / 9007199
 
 struct Scene {
     std::vector<Prim> prims;  // sorted by ymin
+    bool aperiodic = false;
     explicit Scene(uint32_t seed) {
+        aperiodic = (seed & 0x80000000u) != 0;
         uint64_t st = seed * 0x1234567ull + 99;
         auto rnd = [&]() { st = splitmix(st); return u01(st); };
         const double Y0 = -200000, Y1 = 1300000;
@@ -49,6 +53,7 @@ struct Scene {
                 p.kind = 0;
                 p.a[0] = side * 9000.0; p.a[1] = y; p.a[2] = y + len; p.a[3] = -1730 + h; p.a[4] = side;
                 p.a[5] = 4000 * rnd();  // window phase
+                p.a[6] = (double)(splitmix(st) >> 12);  // per-facade salt of the aperiodic variant
                 p.ymin = y; p.ymax = y + len;
                 prims.push_back(p);
                 y += len + 12000 + 8000 * rnd();
@@ -58,7 +63,7 @@ struct Scene {
             bp.a[0] = side * 35000.0; bp.a[3] = -1730 + 20000;
             bp.ymin = Y0 - 200000; bp.ymax = Y1 + 200000;
             prims.push_back(bp);
-            for (double py = Y0 + 3000 * (side + 2); py < Y1; py += 12000) {
+            for (double py = Y0 + 3000 * (side + 2); py < Y1; py += aperiodic ? 6000 + 12000 * rnd() : 12000) {
                 Prim p{};
                 p.kind = 1;
                 p.a[0] = side * 7000.0; p.a[1] = py; p.a[2] = 150; p.a[3] = -1730; p.a[4] = 3270;
@@ -97,7 +102,7 @@ static std::shared_ptr<Scene> get_scene(uint32_t seed) {
 }
 
 // nearest positive ray parameter of one primitive (inf if none); ray o + t d, |d| = 1
-static double hit(const Prim& p, const double o[3], const double d[3], bool& is_ground) {
+static double hit(const Prim& p, const double o[3], const double d[3], bool& is_ground, bool aperiodic) {
     const double INF = 1e300;
     is_ground = false;
     switch (p.kind) {
@@ -111,8 +116,21 @@ static double hit(const Prim& p, const double o[3], const double d[3], bool& is_
             const double u = std::fmod(y - p.a[1] + p.a[5], 4000.0);
             const double fz = z + 1730;
             double recess = 0;
+            if (aperiodic) {
+                // every 4 m x 3.5 m facade cell draws its window (present, x-extent, height) from a hash
+                const int64_t cx = (int64_t)std::floor((y - p.a[1] + p.a[5]) / 4000.0);
+                const int64_t cz = fz > 1000 ? (int64_t)std::floor((fz - 1000) / 3500.0) : -1;
+                const uint64_t hw = splitmix((uint64_t)p.a[6] ^ ((uint64_t)cx << 8) ^ (uint64_t)(cz + 1));
+                const double w0 = 300 + 1500 * u01(hw), w1 = w0 + 700 + 1300 * u01(splitmix(hw + 1));
+                const double hh = 1000 + 1500 * u01(splitmix(hw + 2));
+                if (cz >= 0 && (hw & 7) < 5 && std::fmod(fz - 1000, 3500.0) < hh && u > w0 && u < w1 &&
+                    fz < p.a[3] + 1730 - 800)
+                    recess = 300;
+                if (fz < 2200 && u > 200 && u < 1400 && (splitmix(hw + 3) & 3) == 0) recess = 500;
+            } else {
             if (fz > 1000 && std::fmod(fz - 1000, 3500.0) < 1800 && u > 1200 && u < 2700 && fz < p.a[3] + 1730 - 800) recess = 300;
             if (fz < 2200 && u > 200 && u < 1400 && std::fmod(y - p.a[1], 12000.0) < 4000) recess = 500;
+            }
             if (recess > 0) {
                 const double t2 = (X + p.a[4] * recess - o[0]) / d[0];
                 if (t2 > 0) return t2;
@@ -220,7 +238,7 @@ int synth_sweep(int sensor, uint32_t scene_seed, int frame, int no_ground, float
             }
             for (const Prim* p : near) {
                 bool g;
-                const double t = hit(*p, o, d, g);
+                const double t = hit(*p, o, d, g, sc->aperiodic);
                 if (t < best) { best = t; ground = false; }
             }
             if (best >= 1e299 || (no_ground && ground)) continue;
@@ -303,7 +321,7 @@ int synth_lasers(int sensor, uint32_t scene_seed, int frame, float max_range, fl
             if (d[2] < -1e-12) best = (-1730.0 - o[2]) / d[2];
             for (const Prim* p : near) {
                 bool g;
-                const double t = hit(*p, o, d, g);
+                const double t = hit(*p, o, d, g, sc->aperiodic);
                 if (t < best) best = t;
             }
             const uint64_t h = splitmix(((uint64_t)scene_seed << 40) ^ ((uint64_t)(frame + 1000) << 20) ^ (uint64_t)(j * V + b));

@@ -23,9 +23,6 @@ import time
 
 import numpy as np
 
-# the library's copy-engine setting (b-shot-slam_amd/bshot_py.py), before anything initialises HIP
-os.environ.setdefault("GPU_FORCE_BLIT_COPY_SIZE", "256")
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "b-shot-slam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -73,7 +70,6 @@ def parse():
     ap.add_argument("--no-prefetch", action="store_true",
                     help="process sweeps strictly one after another (no lookahead of the next sweep's SR/ISS)")
     ap.add_argument("--ladder-grids", type=int, default=None, help="tuning knob: 2 or 4 kNN ladder grids")
-    ap.add_argument("--side-cu-reserve", type=int, default=None, help="tuning knob: CUs kept from the side stream")
     ap.add_argument("--opt", action="append", default=[], help="tuning knob name=value (bshot_odom_set_option)")
     ap.add_argument("--from-lasers", action="store_true",
                     help="each sweep starts as HBM-resident laser returns and runs the GPU preprocessor "
@@ -133,9 +129,8 @@ def main():
         pre_done[j] = True
 
     odo = bshot_py.Odometry(device=local, params=params)
-    for name, val in (("ladder_grids", a.ladder_grids), ("side_cu_reserve", a.side_cu_reserve)):
-        if val is not None:
-            odo.set_option(name, val)
+    if a.ladder_grids is not None:
+        odo.set_option("ladder_grids", a.ladder_grids)
     for kv in a.opt:
         name, val = kv.split("=")
         odo.set_option(name, int(val))

@@ -95,9 +95,6 @@ class LidarOdometry {
     void joinAhead();
     void dropTopkAhead();
     void dropReady();
-    struct QueueAhead;
-    void joinQueue();
-    std::shared_ptr<QueueAhead> queue_ahead_;  // sweep after next: its launches issued on their own thread
     std::shared_ptr<TopkAhead> topk_ahead_;  // sweep after next: top-K on its own thread once its SR lands
     std::shared_ptr<Lookahead> ahead_;  // next sweep, in flight on the worker thread
     std::shared_ptr<Lookahead> ready_;  // adopted for the current sweep

@@ -185,6 +185,17 @@ class OOdom {
     std::vector<P3> iss_src, iss_ref;
     float ransac_T[16];
     float T_best[16];
+#ifdef ORACLE_DIAG
+    // diagnostic-only build (oracle/Makefile diag, never the product, never the parity oracle):
+    // fix_normals computes the normal of every surface point (the evident intent of
+    // include/bshot_bits.h:59-86, whose loop writes keypoint k's normal into surface slot k);
+    // pose_override replaces the frame's estimated pose (kept in the stats) by a given one for
+    // the pose and the map update, so a sequence can be replayed under ground-truth poses.
+    int diag_fix_normals = 0;
+    int diag_have_override = 0;
+    float diag_override[16];
+    std::vector<int32_t> mut_q, mut_m;
+#endif
 
     explicit OOdom(const oracle_params& pp) : p(pp) {
         map.canonical = pp.map_canonical != 0;
@@ -224,6 +235,11 @@ class OOdom {
         if (initial) iss_ref = iss_src;
         // ---- computeDescriptors (:173-184)
         normals.resize(4 * (size_t)n, 0.0f);  // std::vector::resize keeps [0, min) (persistent)
+#ifdef ORACLE_DIAG
+        if (diag_fix_normals)
+            oracle_normals(xyz, n, xyz, n, p.normal_radius, p.normal_max_nn, normals.data());
+        else
+#endif
         oracle_normals(xyz, n, reinterpret_cast<const float*>(src->kps.data()), k, p.normal_radius, p.normal_max_nn,
                        normals.data());
         std::vector<float> shot(352 * (size_t)std::max(k, 1));
@@ -250,6 +266,10 @@ class OOdom {
                      reinterpret_cast<const uint32_t*>(c2bits.data()), m, left.data(), right.data(), cq.data(),
                      cm.data(), &nc);
         st->n_mutual = nc;
+#ifdef ORACLE_DIAG
+        mut_q.assign(cq.begin(), cq.begin() + nc);
+        mut_m.assign(cm.begin(), cm.begin() + nc);
+#endif
         inl_q.assign(std::max(nc, 1), 0);
         inl_m.assign(std::max(nc, 1), 0);
         int ni = 0;
@@ -287,6 +307,13 @@ class OOdom {
         st->repeat_sr = repeat_rate(src->kps, ref->kps);
         st->repeat_iss = repeat_rate(iss_src, iss_ref);
         // ---- poseEstimation (:333-342)
+        std::memcpy(st->pose, T_best, sizeof(T_best));
+#ifdef ORACLE_DIAG
+        if (diag_have_override) {
+            std::memcpy(T_best, diag_override, sizeof(T_best));
+            diag_have_override = 0;
+        }
+#endif
         std::memcpy(src->pose, T_best, sizeof(T_best));
         // ---- updateMap (:344-376) with Keypoint::createKeypoint (src/keypoint.cpp:23-32)
         for (int i = 0; i < k; ++i) {
@@ -301,7 +328,6 @@ class OOdom {
         }
         initial = false;
         std::memcpy(st->T_ransac, ransac_T, sizeof(ransac_T));
-        std::memcpy(st->pose, T_best, sizeof(T_best));
         st->map_size = map.size();
         return 0;
     }
@@ -369,5 +395,22 @@ int oracle_odom_get_iss(void* h, float* xyz, int cap) {
     std::memcpy(xyz, o->iss_src.data(), sizeof(P3) * c);
     return c;
 }
+
+#ifdef ORACLE_DIAG
+void oracle_diag_fix_normals(void* h, int on) { static_cast<OOdom*>(h)->diag_fix_normals = on; }
+void oracle_diag_pose_override(void* h, const float* T16) {
+    auto* o = static_cast<OOdom*>(h);
+    std::memcpy(o->diag_override, T16, sizeof(o->diag_override));
+    o->diag_have_override = 1;
+}
+int oracle_diag_get_mutual(void* h, int32_t* q, int32_t* m, int cap) {
+    auto* o = static_cast<OOdom*>(h);
+    const int c = (int)o->mut_q.size();
+    if (c > cap) return -c;
+    std::memcpy(q, o->mut_q.data(), sizeof(int32_t) * c);
+    std::memcpy(m, o->mut_m.data(), sizeof(int32_t) * c);
+    return c;
+}
+#endif
 
 }  // extern "C"

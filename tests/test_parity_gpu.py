@@ -44,22 +44,10 @@ def test_seg_ratio_bit_exact(ctx, cloud, sr_ref, ladder):
     ctx.set_option("ladder_grids", 4)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 0])
-def test_seg_ratio_tiles_bit_exact(ctx, cloud, sr_ref, tile):
-    """Cell-tiled SR (tiles = runs of one ladder level-`tile` cell; 0 = one query per wave, the default)."""
-    ctx.set_option("sr_tile", tile)
-    ctx.set_cloud(cloud)
-    idx, rat = ctx.seg_ratio()
-    ctx.set_option("sr_tile", 0)
-    ridx, rrat = sr_ref
-    np.testing.assert_array_equal(idx, ridx)
-    np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32))
-
-
 def _edge_cloud():
-    """Sparse far points, a dense clump whose neighbourhoods overflow the LDS stage (> 2048
-    candidates: the per-query fallback), exact duplicates, origin points, NaN/inf rows and points
-    beyond the ladder keys' range (no grid cell: ratio NaN)."""
+    """Sparse far points, a dense clump whose neighbourhoods overflow the kNN list (> KNN_CAP keys:
+    the streaming selection), exact duplicates, origin points, NaN/inf rows and points beyond the
+    ladder keys' range (no grid cell: ratio NaN)."""
     rng = np.random.default_rng(11)
     far = rng.uniform(-90000, 90000, (3000, 3))
     clump = np.array([2000.0, -1000.0, 300.0]) + rng.normal(0, 250, (6000, 3))
@@ -71,17 +59,15 @@ def _edge_cloud():
 
 
 @pytest.mark.parametrize("sr_type", [0, 1, 2])
-def test_seg_ratio_tiles_edge_cases(sr_type):
+def test_seg_ratio_edge_cases(sr_type):
     xyz = _edge_cloud()
     ridx, rrat = orc.seg_ratio(xyz, sr_type=sr_type)
     c = bshot_py.Context(0, bshot_py.default_params(sr_type=sr_type))
     try:
-        for tile in (1, 3, 0):
-            c.set_option("sr_tile", tile)
-            c.set_cloud(xyz)
-            idx, rat = c.seg_ratio()
-            np.testing.assert_array_equal(idx, ridx, err_msg=f"tile {tile}")
-            np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32), err_msg=f"tile {tile}")
+        c.set_cloud(xyz)
+        idx, rat = c.seg_ratio()
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32))
     finally:
         c.close()
 
@@ -101,12 +87,10 @@ def test_iss_exact(ctx, cloud):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("k,fused", [(600, 0), (600, 8), (2048, 0), (2048, 4), (2048, 8), (2048, 16)])  # k ascending: the module context's persistent normals array must not hold stale slots from a larger K
-def test_describe_parity(ctx, cloud, sr_ref, k, fused):
+@pytest.mark.parametrize("k", [600, 2048])  # k ascending: the module context's persistent normals array must not hold stale slots from a larger K
+def test_describe_parity(ctx, cloud, sr_ref, k):
     """Load-balanced SHOT: bucketed gather + in-bucket rank, chunked LRF, records + ordered apply
-    (fused = W > 0, the default 8: records computed by W - 1 waves and applied by one, in one
-    workgroup per keypoint, k_hist_fused; 0: k_hist_contrib + k_hist_apply)."""
-    ctx.set_option("hist_fused", fused)
+    (7 waves compute the records and one applies them, in one workgroup per keypoint: k_hist_fused)."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, k)
     kps = cloud[kidx]
@@ -127,20 +111,19 @@ def test_describe_parity(ctx, cloud, sr_ref, k, fused):
     np.testing.assert_array_equal(rf.view(np.uint32)[~np.isnan(rf)], rrf.view(np.uint32)[~np.isnan(rrf)])
     np.testing.assert_array_equal(shot.view(np.uint32)[~np.isnan(shot)], rs.view(np.uint32)[~np.isnan(rs)])
     np.testing.assert_array_equal(bits, rb)
-    ctx.set_option("hist_fused", 8)
 
 
 @pytest.mark.parametrize("hint", [1 << 26, 1])
 def test_describe_device_plan(ctx, cloud, sr_ref, hint):
     """Describe planned on the device (capacity hint ample) and the re-plan after a device plan
-    overflows its capacity (hint 1): both give the host-planned bits."""
+    overflows its capacity (hint 1): both give the host-planned bits (hint 0: no size seen yet, the
+    plan is made on the host, as for a context's first describe)."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 2048)
     kps = cloud[kidx]
     ctx.set_cloud(cloud)
-    ctx.set_option("dev_plan", 0)
+    ctx.set_option("dev_plan_hint", 0)
     ref_bits, ref_shot, _ = ctx.describe(kps)
-    ctx.set_option("dev_plan", 1)
     ctx.set_option("dev_plan_hint", hint)
     bits, shot, _ = ctx.describe(kps)
     np.testing.assert_array_equal(bits, ref_bits)
@@ -214,16 +197,13 @@ def test_icp_grid_edge_cases(icp_grid, icp_dev):
         c.close()
 
 
-@pytest.mark.parametrize("seed,frac,zc", [(1, 0.6, 0), (2, 0.3, 0), (3, 0.9, 0), (4, 0.05, 0), (6, 0.15, 0),
-                                          (1, 0.6, 1), (4, 0.05, 1)])
-def test_ransac_dev_matches_host(ctx, seed, frac, zc):
-    """A10 with the hypotheses scored on the GPU (bshot_ransac_dev; zc = 1: read from / written to
-    pinned host memory by one kernel) == host RANSAC == oracle, bit for bit."""
+@pytest.mark.parametrize("seed,frac", [(1, 0.6), (2, 0.3), (3, 0.9), (4, 0.05), (6, 0.15)])
+def test_ransac_dev_matches_host(ctx, seed, frac):
+    """A10 with the hypotheses scored on the GPU (bshot_ransac_dev) == host RANSAC == oracle, bit
+    for bit."""
     from test_host import _corr_set
     src, tgt, cq, cm = _corr_set(seed, inlier_frac=frac)
-    ctx.set_option("ransac_zc", zc)
     rc, T, iq, im = ctx.ransac(src, tgt, cq, cm)
-    ctx.set_option("ransac_zc", 0)
     hrc, hT, hq, hm = bshot_py.ransac(src, tgt, cq, cm)
     orc_rc, oT, oq, om = orc.ransac(src, tgt, cq, cm)
     assert rc == hrc == orc_rc
