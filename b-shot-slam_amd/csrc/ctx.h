@@ -196,18 +196,13 @@ struct bshot_ctx {
     void hmark(const char* name);
 
     // icp
-    DBuf<bsh::IcpState> istate;
-    PinBuf<bsh::IcpState> p_istate;
+    PinBuf<bsh::IcpResult> p_icp;  // k_icp_loop's result (final transform, iterations)
     int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
     int opt_topk_thread = 1;   // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
     int opt_pre_fast = 1;  // preprocessor: one 32-bit sort for azimuth-ordered lasers with tabled verticals
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
     int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
-    DBuf<unsigned long long> ipart;  // k_icp_tile span minima
-    DBuf<unsigned int> icnt;         // k_icp_tile per-block arrival counters
-    int opt_icp_grid = 1;  // 1: exact 1-NN on hashed grids of the targets (k_icp_grid); 0: LDS-tiled brute force (k_icp_tile)
-    bsh::DevGrid icp_lad[4];  // ICP target grids: nested cells 1000 .. 8000 mm (levels 0 and 2 used), one sort per ICP call
-    int opt_icp_dev = 0;  // 1: ICP loop resident on the device (one sync); 0: host Umeyama per iteration (faster under load)
+    bsh::DevGrid icp_lad[4];  // ICP target grids: nested cells 1000 .. 8000 mm, one sort per ICP call
     DBuf<float> isrc, itgt3;
     DBuf<float4> itgt;
     DBuf<unsigned long long> ibest;

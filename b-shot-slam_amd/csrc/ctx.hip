@@ -607,11 +607,11 @@ int ctx_sync_main(bshot_ctx* c) {
     return BSHOT_OK;
 }
 
-// the ICP targets' grids (cells 1000 and 4000 mm) from one nested-key sort of itgt3; float4 targets
-// in index order -> itgt
-static hipError_t icp_grids(bshot_ctx* c, int nt, int min_cap) {
+// the ICP targets' nested grids (cells 1000, 2000, 4000, 8000 mm, all hashed) from one
+// nested-key sort of d_tgt; float4 targets in index order -> itgt
+static hipError_t icp_grids(bshot_ctx* c, const float* d_tgt, int nt, int min_cap) {
     DevGrid* lad[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
-    return grid_build_ladder(lad, c->itgt3.p, nt, 1000.f, c->itgt.p, c->stream, 0x5u, min_cap);
+    return grid_build_ladder(lad, d_tgt, nt, 1000.f, c->itgt.p, c->stream, 0xFu, min_cap);
 }
 
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
@@ -619,120 +619,74 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
     bg::Mat4f fin = bg::Mat4f::identity();
     int it = 0;
     if (ns >= 3 && nt > 0) {
-        // device: target then source in one staging buffer (one H2D copy), src double buffer
-        // (moved by each iteration's kernel)
-        HIPCHK(c->isrc.ensure(6 * (size_t)ns), "alloc icp src");
-        HIPCHK(c->itgt3.ensure(3 * ((size_t)nt + ns)), "alloc icp staging");
-        HIPCHK(c->p_tgt.ensure(3 * ((size_t)nt + ns)), "alloc pinned tgt");
-        HIPCHK(c->p_best.ensure(ns), "alloc pinned best");
-        if (d_tgt) {
-            std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
-            HIPCHK(kcopy(c->itgt3.p, d_tgt, sizeof(float) * 3 * (size_t)nt, c->stream),
-                   "icp targets");
-            HIPCHK(kcopy(c->itgt3.p + 3 * (size_t)nt, c->p_tgt.p + 3 * (size_t)nt, sizeof(float) * 3 * ns, c->stream),
-                   "H2D icp source");
-        } else {
+        // the source (host, already moved by T_est) through pinned staging; the targets are in HBM
+        // already (gmap) or go the same way
+        HIPCHK(c->isrc.ensure(9 * (size_t)ns), "alloc icp src");
+        HIPCHK(c->p_src.ensure(3 * (size_t)ns), "alloc pinned src");
+        HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
+        std::memcpy(c->p_src.p, src, sizeof(float) * 3 * ns);
+        HIPCHK(kcopy(c->isrc.p, c->p_src.p, sizeof(float) * 3 * ns, c->stream), "H2D icp source");
+        if (!d_tgt) {
+            HIPCHK(c->itgt3.ensure(3 * (size_t)nt), "alloc icp staging");
+            HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
             std::memcpy(c->p_tgt.p, tgt, sizeof(float) * 3 * nt);
-            std::memcpy(c->p_tgt.p + 3 * (size_t)nt, src, sizeof(float) * 3 * ns);
-            HIPCHK(kcopy(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * ((size_t)nt + ns),
-                                  c->stream),
-                   "H2D icp points");
+            HIPCHK(kcopy(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * nt, c->stream), "H2D icp targets");
+            d_tgt = c->itgt3.p;
         }
-        const float* d_src0 = c->itgt3.p + 3 * (size_t)nt;
-        if (c->opt_icp_dev) {
-            HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
-            HIPCHK(c->ibest.ensure(2 * (size_t)ns), "alloc icp best");
-            HIPCHK(kcopy(c->isrc.p, d_src0, sizeof(float) * 3 * ns, c->stream),
-                   "icp src");
-            HIPCHK(kfill(c->ibest.p, 0xFF, sizeof(unsigned long long) * ns, c->stream), "init best");
-            const bool use_grid = c->opt_icp_grid != 0;
-            if (use_grid) {
-                const int mc = std::max(65536, 2 * nt);
-                HIPCHK(icp_grids(c, nt, mc), "icp grids");
-            } else {
-                HIPCHK(launch_pack_points(c->itgt3.p, nt, c->itgt.p, c->stream), "pack tgt");
-            }
-            // max_iter (NN, update) pairs queued at once; converged iterations return immediately
-            HIPCHK(c->istate.ensure(1), "alloc icp state");
-            HIPCHK(c->p_istate.ensure(1), "alloc pinned icp state");
-            IcpState& h = *c->p_istate.p;
-            const bg::Mat4f I = bg::Mat4f::identity();
-            std::memcpy(h.T, I.m, sizeof(h.T));
-            std::memcpy(h.fin, I.m, sizeof(h.fin));
-            h.prev_mse = 1.7976931348623157e308;
-            h.it = 0;
-            h.done = 0;
-            h.max_iter = max_iter;
-            h.pad = 0;
-            HIPCHK(kcopy(c->istate.p, c->p_istate.p, sizeof(IcpState), c->stream),
-                   "H2D icp state");
+        // the targets are fixed for the whole ICP call: their grids are built once
+        const int mc = std::max(65536, 2 * nt);
+        HIPCHK(icp_grids(c, d_tgt, nt, mc), "icp grids");
+        if (ns <= ICP_LOOP_MAXN) {
+            // the whole loop in one launch; the result lands in pinned memory
+            HIPCHK(c->p_icp.ensure(1), "alloc pinned icp result");
+            const DevGrid* g4[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-            const int n_it = max_iter > 1 ? max_iter : 1;
-            for (int j = 0; j < n_it; ++j) {
-                const int b = j & 1;
-                if (use_grid)
-                    HIPCHK(launch_icp_grid_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
-                                               c->istate.p, ns, c->icp_lad[0], c->icp_lad[2], c->itgt.p, nt, c->ibest.p,
-                                               c->stream),
-                           "icp iteration");
-                else
-                    HIPCHK(launch_icp_dev(c->isrc.p + 3 * (size_t)ns * b, c->isrc.p + 3 * (size_t)ns * (b ^ 1),
-                                          c->istate.p, ns, c->itgt.p, nt, c->ibest.p + (size_t)ns * b,
-                                          c->ibest.p + (size_t)ns * (b ^ 1), c->stream),
-                           "icp iteration");
-            }
+            HIPCHK(launch_icp_loop(c->isrc.p, ns, g4, c->itgt.p, nt, max_iter, c->p_icp.p, c->stream), "icp loop");
             c->stage_end(sg14);
-            HIPCHK(kcopy(c->p_istate.p, c->istate.p, sizeof(IcpState), c->stream),
-                   "D2H icp state");
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
-            std::memcpy(T, h.fin, sizeof(float) * 16);
-            *iters = h.it;
+            std::memcpy(T, c->p_icp.p->fin, sizeof(float) * 16);
+            *iters = c->p_icp.p->iters;
             return BSHOT_OK;
         }
+        // more sources than the loop kernel's LDS holds: one NN launch per iteration, the Umeyama
+        // step on the host (the same arithmetic). The NN keys land in pinned host memory (no
+        // copy), double-buffered by iteration parity so the next iteration's kernel can be in
+        // flight while the host finishes this one.
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
-        // the NN keys land in pinned host memory (no copy), double-buffered by iteration parity so
-        // the next iteration's kernel can be in flight while the host finishes this one
         HIPCHK(c->p_best.ensure(2 * (size_t)ns), "alloc pinned best");
-        const int splits = icp_tile_splits(ns, nt);
-        const bool use_grid = c->opt_icp_grid != 0;
-        if (use_grid) {
-            // the targets are fixed for the whole ICP call: two hashed grids of them, built once
-            HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
-            const int mc = std::max(65536, 2 * nt);
-            HIPCHK(icp_grids(c, nt, mc), "icp grids");
-        } else {
-            HIPCHK(c->ipart.ensure((size_t)splits * ns), "alloc icp spans");
-            HIPCHK(c->icnt.ensure((size_t)(ns + 255) / 256), "alloc icp counters");
-            HIPCHK(kfill(c->icnt.p, 0, sizeof(unsigned int) * ((ns + 255) / 256), c->stream), "icp counters");
-        }
-        // one launch per iteration: iteration j moves the source by the previous step's transform
-        // (j > 0) and writes its NN keys to p_best[j & 1]
+        const float* d_src0 = c->isrc.p;
+        // iteration j moves the source by the previous step's transform (j > 0) and writes its NN
+        // keys to p_best[j & 1]
         auto launch_it = [&](int j, const bg::Mat4f& Tj) -> int {
             const int b = j & 1;
             const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-            const float* s_in = j == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (b ^ 1);
+            const float* s_in = j == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (1 + (b ^ 1));
             unsigned long long* bo = c->p_best.p + (size_t)ns * b;
-            if (use_grid)
-                HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * b, Tj.m, j > 0, ns, c->icp_lad[0],
-                                       c->icp_lad[2], c->itgt.p, nt, bo, c->stream),
-                       "icp iteration");
-            else
-                HIPCHK(launch_icp_tile(s_in, c->isrc.p + 3 * (size_t)ns * b, Tj.m, j > 0, ns, c->itgt3.p, nt,
-                                       c->ipart.p, (int)std::min<size_t>(c->ipart.cap, 0x7FFFFFFF), c->icnt.p, bo,
-                                       c->stream),
-                       "icp iteration");
+            HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * (1 + b), Tj.m, j > 0, ns, c->icp_lad[0],
+                                   c->icp_lad[2], c->itgt.p, nt, bo, c->stream),
+                   "icp iteration");
             c->stage_end(sg14);
             return BSHOT_OK;
         };
         double prev_mse = 1.7976931348623157e308;
         bg::Mat4f Ts = bg::Mat4f::identity();
         if (int e = launch_it(0, Ts)) return e;
+        std::vector<float> h_tgt;
+        const float* tg = tgt;
+        if (!tg) {
+            h_tgt.resize(3 * (size_t)nt);
+            HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
+            HIPCHK(kcopy(c->p_tgt.p, d_tgt, sizeof(float) * 3 * nt, c->stream), "D2H icp targets");
+            HIPCHK(hipStreamSynchronize(c->stream), "sync icp targets");
+            std::memcpy(h_tgt.data(), c->p_tgt.p, sizeof(float) * 3 * nt);
+            tg = h_tgt.data();
+        }
         while (true) {
             const unsigned long long* best = c->p_best.p + (size_t)ns * (it & 1);
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
             for (int i = 0; i < ns; ++i) {
                 const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);
-                tb[3 * i] = tgt[3 * j]; tb[3 * i + 1] = tgt[3 * j + 1]; tb[3 * i + 2] = tgt[3 * j + 2];
+                tb[3 * i] = tg[3 * j]; tb[3 * i + 1] = tg[3 * j + 1]; tb[3 * i + 2] = tg[3 * j + 2];
             }
             Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
             ++it;
@@ -752,6 +706,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             if (__builtin_fabs(mse - prev_mse) < 1e-12) break;
             prev_mse = mse;
         }
+        HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
     }
     std::memcpy(T, fin.m, sizeof(float) * 16);
     *iters = it;
@@ -839,7 +794,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->prep = nullptr;
     bsh::velo_free(c->velo);
     c->velo = nullptr;
-    c->gidx.release(); c->gout.release(); c->istate.release(); c->p_istate.release(); c->isrc.release(); c->ipart.release(); c->icnt.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gidx.release(); c->gout.release(); c->p_icp.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
@@ -1093,8 +1048,6 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
-    else if (k == "icp_dev") c->opt_icp_dev = value ? 1 : 0;
-    else if (k == "icp_grid") c->opt_icp_grid = value ? 1 : 0;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;

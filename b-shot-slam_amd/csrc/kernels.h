@@ -40,30 +40,21 @@ hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, in
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
-// LDS-tiled NN pass over target spans (k_icp_tile); part: icp_tile_splits(ns, nt) x ns keys, cnt:
-// ceil(ns / 256) zeroed counters
-int icp_tile_splits(int ns, int nt);
-hipError_t launch_icp_tile(const float* src_in, float* src_out, const float* T16, int apply, int ns, const float* tgt,
-                           int nt, unsigned long long* part, int part_cap, unsigned int* cnt,
-                           unsigned long long* best_out, hipStream_t s);
-// exact 1-NN on two hashed grids of the targets (cells r1 < r2; k_icp_grid), brute force past them
+// exact 1-NN on two hashed grids of the targets (cells r1 < r2; k_icp_grid), brute force past them:
+// one NN pass of the host-driven ICP loop (source sets larger than ICP_LOOP_MAXN)
 hipError_t launch_icp_grid(const float* src_in, float* src_out, const float* T16, int apply, int ns, const DevGrid& g1,
                            const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best_out, hipStream_t s);
-// device-resident ICP loop state (ctx_icp with opt icp_dev): step T, accumulated fin, PCL
-// convergence bookkeeping
-struct IcpState {
-    float T[16];
-    float fin[16];
-    double prev_mse;
-    int it, done, max_iter, pad;
+// the whole ICP loop in one launch (k_icp_loop): g4 = the targets' nested grids, cells 1000, 2000,
+// 4000, 8000 mm (all four hashed); tgt4 = the targets in index order; out (pinned host memory) =
+// the final transform and the iteration count. 3 <= ns <= ICP_LOOP_MAXN (32 B of LDS per source).
+#define ICP_LOOP_MAXN 5000
+struct IcpResult {
+    float fin[16];  // row-major 4x4
+    int iters;
+    int pad[3];
 };
-// one (NN, update) iteration pair; no-ops once st->done
-// one device-resident ICP iteration on the target grids: k_icp_grid with the loop state's step,
-// then k_icp_update (returns at once when the loop has converged)
-hipError_t launch_icp_grid_dev(const float* src_in, float* src_out, IcpState* st, int ns, const DevGrid& g1,
-                               const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best, hipStream_t s);
-hipError_t launch_icp_dev(const float* src_in, float* src_out, IcpState* st, int ns, const float4* tgt, int nt,
-                          unsigned long long* best, unsigned long long* best_next, hipStream_t s);
+hipError_t launch_icp_loop(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int max_iter,
+                           IcpResult* out, hipStream_t s);
 // load-balanced SHOT (describe2.hip): in-bucket rank, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;

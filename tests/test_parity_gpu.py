@@ -145,10 +145,8 @@ def test_match_exact_random_and_ties(ctx):
             np.testing.assert_array_equal(g, r)
 
 
-@pytest.mark.parametrize("icp_dev", [0, 1])
-def test_icp_exact(ctx, cloud, sr_ref, icp_dev):
-    """A11 with the host Umeyama per iteration (icp_dev 0) and the device-resident loop (1)."""
-    ctx.set_option("icp_dev", icp_dev)
+def test_icp_exact(ctx, cloud, sr_ref):
+    """A11: the whole ICP loop in one launch (k_icp_loop) vs the oracle, bit for bit."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 600)
     tgt = cloud[kidx]
@@ -156,17 +154,18 @@ def test_icp_exact(ctx, cloud, sr_ref, icp_dev):
     src = (tgt @ np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], np.float32).T + np.array([300, -200, 50], np.float32))
     src = src.astype(np.float32)
     T, it = ctx.icp(src, tgt)
-    ctx.set_option("icp_dev", 0)
     Tr, itr = orc.icp(src, tgt)
     assert it == itr
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
 
 
-@pytest.mark.parametrize("icp_grid,icp_dev", [(1, 0), (0, 0), (1, 1), (0, 1)])
-def test_icp_grid_edge_cases(icp_grid, icp_dev):
-    """A11 1-NN on the target grids (k_icp_grid) vs the oracle's brute force: sources far beyond
-    every ball (brute-force fallback), exact-duplicate targets (index tie), targets exactly on a
-    ball radius (d2 == rs^2 is outside the ball), a non-finite source, sparse and dense targets."""
+@pytest.mark.parametrize("big", [False, True])
+def test_icp_grid_edge_cases(big):
+    """A11 1-NN on the target grids vs the oracle's brute force: sources far beyond every ball
+    (the brute-force scan), exact-duplicate targets (index tie), targets exactly on a ball radius
+    (d2 == rs^2 is outside the ball), a non-finite source, sparse and dense targets. big: more
+    sources than the one-launch loop holds in LDS (ICP_LOOP_MAXN), i.e. the host-driven loop of
+    k_icp_grid launches."""
     rng = np.random.default_rng(11)
     tgt = (rng.random((5000, 3)) * [80000, 80000, 4000] - [40000, 40000, 2000]).astype(np.float32)
     tgt[100:110] = tgt[90]  # duplicates
@@ -175,11 +174,12 @@ def test_icp_grid_edge_cases(icp_grid, icp_dev):
     src = np.concatenate([tgt[:1500] + rng.normal(0, 300, (1500, 3)), tgt[1500:1600] + 7000.0,
                           [[0, 0, 0], [1000, 0, 0], [500, 0, 0], [2e6, 2e6, 0], [-9e5, 0, 3e5]],
                           tgt[90:91] + 1.0]).astype(np.float32)
+    if big:
+        src = np.concatenate([src, tgt[:3600] + rng.normal(0, 500, (3600, 3))]).astype(np.float32)
+        assert len(src) > 5000
     c = bshot_py.Context(0)
     try:
-        c.set_option("icp_grid", icp_grid)
-        c.set_option("icp_dev", icp_dev)
-        for s2 in (src, src[:64]):
+        for s2 in ((src,) if big else (src, src[:64], src[:3])):
             T, it = c.icp(s2, tgt)
             Tr, itr = orc.icp(s2, tgt)
             assert it == itr
