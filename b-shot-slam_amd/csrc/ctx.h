@@ -40,11 +40,13 @@ struct DBuf {
     }
 };
 
-// pinned host staging (async D2H), grow-only
+// pinned host staging (async D2H), grow-only; coherent: fine-grained memory, for hand-over with a
+// running kernel (system-scope atomics, csrc/icp.hip)
 template <typename T>
 struct PinBuf {
     T* p = nullptr;
     size_t cap = 0;
+    bool coherent = false;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         defer_free(p, DEFER_PINNED);
@@ -53,7 +55,7 @@ struct PinBuf {
         // doubling with a 64 Ki-element floor: a sequence's sizes (targets M, neighbourhood totals)
         // grow for many sweeps, and every regrowth is a free + malloc that stalls the device
         size_t c = n * 2 > (size_t)65536 ? n * 2 : (size_t)65536;
-        hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * c, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * c, coherent ? hipHostMallocCoherent : hipHostMallocDefault);
         if (e == hipSuccess) cap = c;
         note_regrow("pinned", sizeof(T) * c);
         return e;
@@ -196,14 +198,22 @@ struct bshot_ctx {
     void hmark(const char* name);
 
     // icp
-    PinBuf<bsh::IcpResult> p_icp;  // k_icp_loop's result (final transform, iterations)
+    PinBuf<bsh::IcpSync> p_isync;  // ICP host <-> kernel hand-over (coherent)
+    PinBuf<unsigned long long> p_ibest;  // ICP NN keys, two iterations' worth (coherent)
+    PinBuf<int> p_idone;  // ICP per-workgroup completion flags (coherent)
+    DBuf<float4> ilst;  // ICP candidate lists (ICP_LIST_CAP per source)
+    DBuf<float> ilsd;   // their entries' distances from the list centre (ascending)
+    DBuf<int> ilcnt;    // their counts (-1: none)
+    DBuf<float> ilrad;  // their radii
     int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
     int opt_topk_thread = 1;   // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
     int opt_pre_fast = 1;  // preprocessor: one 32-bit sort for azimuth-ordered lasers with tabled verticals
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
     int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
     bsh::DevGrid icp_lad[4];  // ICP target grids: nested cells 1000 .. 8000 mm, one sort per ICP call
-    DBuf<float> isrc, itgt3;
+    DBuf<float> itgt3;
+    const float* icp_prep_tgt = nullptr;  // device targets whose ICP grids ctx_icp_prepare has queued
+    int icp_prep_nt = 0;
     DBuf<float4> itgt;
     DBuf<unsigned long long> ibest;
 
@@ -281,4 +291,6 @@ int ctx_gather_kps_async(bshot_ctx* c, CloudState& S, hipStream_t st, const int*
 // d_tgt (nullable): the same targets already on the device (gmap), copied D2D instead of uploaded
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
             const float* d_tgt = nullptr);
+// queue the grids of the ICP targets d_tgt (nt, device) now; the next ctx_icp with them skips the build
+int ctx_icp_prepare(bshot_ctx* c, const float* d_tgt, int nt);
 }  // namespace bsh

@@ -1,6 +1,7 @@
 // ctx.hip -- bshot_ctx lifecycle and the GPU half of the C ABI (include/bshot_abi.h).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -614,18 +615,30 @@ static hipError_t icp_grids(bshot_ctx* c, const float* d_tgt, int nt, int min_ca
     return grid_build_ladder(lad, d_tgt, nt, 1000.f, c->itgt.p, c->stream, 0xFu, min_cap);
 }
 
+// the ICP targets' grids queued ahead (right after the map query, while the host runs RANSAC): the
+// next ctx_icp on the same device targets skips its own build
+int ctx_icp_prepare(bshot_ctx* c, const float* d_tgt, int nt) {
+    c->icp_prep_tgt = nullptr;
+    if (!d_tgt || nt <= 0) return BSHOT_OK;
+    HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
+    HIPCHK(icp_grids(c, d_tgt, nt, std::max(65536, 2 * nt)), "icp grids");
+    c->icp_prep_tgt = d_tgt;
+    c->icp_prep_nt = nt;
+    return BSHOT_OK;
+}
+
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
             const float* d_tgt) {
+    const bool prepared = d_tgt && c->icp_prep_tgt == d_tgt && c->icp_prep_nt == nt;
+    c->icp_prep_tgt = nullptr;
     bg::Mat4f fin = bg::Mat4f::identity();
     int it = 0;
     if (ns >= 3 && nt > 0) {
-        // the source (host, already moved by T_est) through pinned staging; the targets are in HBM
-        // already (gmap) or go the same way
-        HIPCHK(c->isrc.ensure(9 * (size_t)ns), "alloc icp src");
+        // the source (host, already moved by T_est) in pinned memory, read there by the kernels; the
+        // targets are in HBM already (gmap) or go through pinned staging
         HIPCHK(c->p_src.ensure(3 * (size_t)ns), "alloc pinned src");
         HIPCHK(c->itgt.ensure(nt), "alloc icp tgt");
         std::memcpy(c->p_src.p, src, sizeof(float) * 3 * ns);
-        HIPCHK(kcopy(c->isrc.p, c->p_src.p, sizeof(float) * 3 * ns, c->stream), "H2D icp source");
         if (!d_tgt) {
             HIPCHK(c->itgt3.ensure(3 * (size_t)nt), "alloc icp staging");
             HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
@@ -633,46 +646,34 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             HIPCHK(kcopy(c->itgt3.p, c->p_tgt.p, sizeof(float) * 3 * nt, c->stream), "H2D icp targets");
             d_tgt = c->itgt3.p;
         }
-        // the targets are fixed for the whole ICP call: their grids are built once
-        const int mc = std::max(65536, 2 * nt);
-        HIPCHK(icp_grids(c, d_tgt, nt, mc), "icp grids");
-        if (ns <= ICP_LOOP_MAXN) {
-            // the whole loop in one launch; the result lands in pinned memory
-            HIPCHK(c->p_icp.ensure(1), "alloc pinned icp result");
-            const DevGrid* g4[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
-            const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-            HIPCHK(launch_icp_loop(c->isrc.p, ns, g4, c->itgt.p, nt, max_iter, c->p_icp.p, c->stream), "icp loop");
-            c->stage_end(sg14);
-            HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
-            std::memcpy(T, c->p_icp.p->fin, sizeof(float) * 16);
-            *iters = c->p_icp.p->iters;
-            return BSHOT_OK;
-        }
-        // more sources than the loop kernel's LDS holds: one NN launch per iteration, the Umeyama
-        // step on the host (the same arithmetic). The NN keys land in pinned host memory (no
-        // copy), double-buffered by iteration parity so the next iteration's kernel can be in
-        // flight while the host finishes this one.
+        // the targets are fixed for the whole ICP call: their grids are built once (or were queued
+        // ahead by ctx_icp_prepare)
+        if (!prepared) HIPCHK(icp_grids(c, d_tgt, nt, std::max(65536, 2 * nt)), "icp grids");
+        HIPCHK(c->ilst.ensure((size_t)ICP_LIST_CAP * ns), "alloc icp lists");
+        HIPCHK(c->ilsd.ensure((size_t)ICP_LIST_CAP * ns), "alloc icp list distances");
+        HIPCHK(c->ilcnt.ensure(ns), "alloc icp list counts");
+        HIPCHK(c->ilrad.ensure(ns), "alloc icp list radii");
+        const DevGrid* g4[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
+        // PCL's loop on the host (float Umeyama, convergence), the exact 1-NN of every iteration on
+        // the device (csrc/icp.hip): one launch for iteration 0 (keys + every source's candidate
+        // list) and one persistent launch for the rest, handed over through coherent pinned memory:
+        // the host releases iteration j with its step transform, the kernel stores the keys
+        // (double-buffered by iteration parity) and flags them done. One stream sync per ICP call.
         std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
-        HIPCHK(c->p_best.ensure(2 * (size_t)ns), "alloc pinned best");
-        const float* d_src0 = c->isrc.p;
-        // iteration j moves the source by the previous step's transform (j > 0) and writes its NN
-        // keys to p_best[j & 1]
-        auto launch_it = [&](int j, const bg::Mat4f& Tj) -> int {
-            const int b = j & 1;
-            const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-            const float* s_in = j == 0 ? d_src0 : c->isrc.p + 3 * (size_t)ns * (1 + (b ^ 1));
-            unsigned long long* bo = c->p_best.p + (size_t)ns * b;
-            HIPCHK(launch_icp_grid(s_in, c->isrc.p + 3 * (size_t)ns * (1 + b), Tj.m, j > 0, ns, c->icp_lad[0],
-                                   c->icp_lad[2], c->itgt.p, nt, bo, c->stream),
-                   "icp iteration");
-            c->stage_end(sg14);
-            return BSHOT_OK;
-        };
-        double prev_mse = 1.7976931348623157e308;
-        bg::Mat4f Ts = bg::Mat4f::identity();
-        if (int e = launch_it(0, Ts)) return e;
-        std::vector<float> h_tgt;
+        if (max_iter > ICP_MAX_ITER) return c->fail("icp: max_iter > 64", BSHOT_EINVAL);
+        c->p_isync.coherent = true;
+        c->p_ibest.coherent = true;
+        HIPCHK(c->p_isync.ensure(1), "alloc icp sync");
+        HIPCHK(c->p_ibest.ensure(2 * (size_t)ns), "alloc icp keys");
+        const int nb0 = icp_lists_blocks(ns), nb1 = icp_iter_blocks(ns);
+        c->p_idone.coherent = true;
+        HIPCHK(c->p_idone.ensure((size_t)nb0 + nb1), "alloc icp flags");
+        int* done0 = c->p_idone.p;
+        int* done1 = c->p_idone.p + nb0;
+        std::memset(c->p_idone.p, 0, sizeof(int) * ((size_t)nb0 + nb1));
+        // host copy of the targets (the Umeyama step's pairs), before the persistent kernel is queued
         const float* tg = tgt;
+        std::vector<float> h_tgt;
         if (!tg) {
             h_tgt.resize(3 * (size_t)nt);
             HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
@@ -681,19 +682,65 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             std::memcpy(h_tgt.data(), c->p_tgt.p, sizeof(float) * 3 * nt);
             tg = h_tgt.data();
         }
+        IcpSync* sy = c->p_isync.p;
+        std::memset(sy, 0, sizeof(IcpSync));
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        const float* d_src0 = c->p_src.p;
+        const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
+        HIPCHK(launch_icp_lists(d_src0, ns, g4, c->itgt.p, nt, ICP_LIST_CAP, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p,
+                                c->p_ibest.p, done0, c->stream),
+               "icp lists");
+        HIPCHK(launch_icp_iterations(d_src0, ns, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p, ICP_LIST_CAP, g4, c->itgt.p, nt,
+                                     max_iter, sy, done1, c->p_ibest.p, c->stream),
+               "icp iterations");
+        c->stage_end(sg14);
+        auto release = [&](int go) { __atomic_store_n(&sy->go, go, __ATOMIC_RELEASE); };
+        // iteration j's keys are complete when every workgroup's flag says so
+        auto wait_keys = [&](int j) -> bool {
+            const int nb = j == 0 ? nb0 : nb1;
+            int* flags = j == 0 ? done0 : done1;
+            const int want = j == 0 ? 1 : j;
+            const auto t0 = std::chrono::steady_clock::now();
+            unsigned spins = 0;
+            for (int w = 0; w < nb; ++w) {
+                while (__atomic_load_n(&flags[w], __ATOMIC_ACQUIRE) < want) {
+                    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+                        return false;
+                    __builtin_ia32_pause();
+                }
+            }
+            return true;
+        };
+        double prev_mse = 1.7976931348623157e308;
+        bg::Mat4f Ts = bg::Mat4f::identity();
+        bool timed_out = false;
+        auto ns_now = []() {
+            return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+                .count();
+        };
+        long long tw = ns_now();
         while (true) {
-            const unsigned long long* best = c->p_best.p + (size_t)ns * (it & 1);
-            HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
+            const long long t_a = ns_now();
+            if (!wait_keys(it)) {
+                timed_out = true;
+                break;
+            }
+            const long long t_b = ns_now();
+            c->work[it == 0 ? 2 : 3] += t_b - t_a;  // host wait for the keys: iteration 0 / later
+            if (it > 0) c->work[4] += t_a - tw;     // host step between two waits
+            const unsigned long long* best = c->p_ibest.p + (size_t)ns * (it & 1);
             for (int i = 0; i < ns; ++i) {
                 const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);
                 tb[3 * i] = tg[3 * j]; tb[3 * i + 1] = tg[3 * j + 1]; tb[3 * i + 2] = tg[3 * j + 2];
             }
             Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
             ++it;
-            // the next iteration goes out before this one's bookkeeping and convergence test (PCL
-            // decides after the step); if the test stops the loop, that launch is never read
-            if (it < max_iter)
-                if (int e = launch_it(it, Ts)) return e;
+            // the next iteration is released before this one's bookkeeping and convergence test (PCL
+            // decides after the step); if the test stops the loop, its keys are never read
+            if (it < max_iter) {
+                std::memcpy(sy->T, Ts.m, sizeof(Ts.m));
+                release(it);
+            }
             for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);  // the device applies Ts too
             fin = bg::mul(Ts, fin);
             if (it >= max_iter) break;
@@ -705,8 +752,13 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             mse /= (double)ns;
             if (__builtin_fabs(mse - prev_mse) < 1e-12) break;
             prev_mse = mse;
+            tw = t_b;
         }
+        c->work[5] += it;
+        release(-1);
+  // the persistent kernel's waves exit
         HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
+        if (timed_out) return c->fail("icp: the device did not deliver the nearest neighbours within 2 s", BSHOT_EHIP);
     }
     std::memcpy(T, fin.m, sizeof(float) * 16);
     *iters = it;
@@ -794,7 +846,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->prep = nullptr;
     bsh::velo_free(c->velo);
     c->velo = nullptr;
-    c->gidx.release(); c->gout.release(); c->p_icp.release(); c->isrc.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gidx.release(); c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->ilrad.release(); c->p_isync.release(); c->p_ibest.release(); c->p_idone.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");

@@ -40,21 +40,35 @@ hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, in
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
-// exact 1-NN on two hashed grids of the targets (cells r1 < r2; k_icp_grid), brute force past them:
-// one NN pass of the host-driven ICP loop (source sets larger than ICP_LOOP_MAXN)
-hipError_t launch_icp_grid(const float* src_in, float* src_out, const float* T16, int apply, int ns, const DevGrid& g1,
-                           const DevGrid& g2, const float4* tgt4, int nt, unsigned long long* best_out, hipStream_t s);
-// the whole ICP loop in one launch (k_icp_loop): g4 = the targets' nested grids, cells 1000, 2000,
-// 4000, 8000 mm (all four hashed); tgt4 = the targets in index order; out (pinned host memory) =
-// the final transform and the iteration count. 3 <= ns <= ICP_LOOP_MAXN (32 B of LDS per source).
-#define ICP_LOOP_MAXN 5000
-struct IcpResult {
-    float fin[16];  // row-major 4x4
-    int iters;
-    int pad[3];
+// A11 ICP nearest neighbours on the targets' nested grids g4 (cells 1000, 2000, 4000, 8000 mm, all
+// hashed) and float4 targets tgt4 (index order). Iteration 0: the exact 1-NN keys of src0 into
+// best_out, and per source a candidate list (cap float4 entries: target xyz + index bits, and their
+// distances from the list's centre, in ascending order; entry e of source i at [e * ns + i]), its
+// count (-1: none) and radius. Iteration >= 1: the sources moved by T16 (src_in -> src_out) and
+// their exact 1-NN keys; keys (d2 bits << 32 | index) land in best_out (pinned host memory).
+#define ICP_LIST_CAP 128
+#define ICP_MAX_ITER 64
+// host <-> device hand-over of one ICP call (coherent pinned host memory, csrc/icp.hip): the host
+// releases iteration j (step transform T, then go = j; go = -1 stops the kernel). Every workgroup
+// writes its own completion flag once its keys are stored (no atomics, no cache write-back).
+struct IcpSync {
+    int go;
+    int pad0[31];
+    float T[16];
 };
-hipError_t launch_icp_loop(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int max_iter,
-                           IcpResult* out, hipStream_t s);
+// iteration 0 (one launch, a wave per source): keys of src0 into best_out (pinned), the candidate
+// lists; workgroup w sets done[w] = 1. Returns its workgroup count.
+int icp_lists_blocks(int ns);
+hipError_t launch_icp_lists(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
+                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, int* done,
+                            hipStream_t s);
+// iterations 1 .. max_iter - 1 (one persistent launch, a lane per source): each waits for the host's
+// release of the iteration (or go = -1), moves its source by T, stores the exact 1-NN key in
+// best[(j & 1) * ns + i] (pinned) and sets done[w] = j.
+int icp_iter_blocks(int ns);
+hipError_t launch_icp_iterations(const float* src0, int ns, const float4* lst, const float* lsd, const int* lcnt,
+                                 const float* lrad, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
+                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s);
 // load-balanced SHOT (describe2.hip): in-bucket rank, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;

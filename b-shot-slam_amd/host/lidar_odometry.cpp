@@ -504,6 +504,9 @@ void LidarOdometry::featureMatching() {
         stats_.n_target = nb;
         stats_.n_mutual = nc;
         stats_.host_ms[3] = (float)t_m.toc();
+        // the ICP targets are these: their grids go on the main stream now, ahead of RANSAC's launch,
+        // and build while the host draws RANSAC's hypotheses
+        if (nb > 0) check(bsh::ctx_icp_prepare(ctx_, ctx_->gtgt.p, nb), "icp prepare");
         ransacStep(na, nb, cq, cm, nc);
         return;
     }

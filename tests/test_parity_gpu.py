@@ -146,7 +146,8 @@ def test_match_exact_random_and_ties(ctx):
 
 
 def test_icp_exact(ctx, cloud, sr_ref):
-    """A11: the whole ICP loop in one launch (k_icp_loop) vs the oracle, bit for bit."""
+    """A11: ICP (iteration 0 builds candidate lists, later iterations search them) vs the oracle,
+    bit for bit."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 600)
     tgt = cloud[kidx]
@@ -163,9 +164,9 @@ def test_icp_exact(ctx, cloud, sr_ref):
 def test_icp_grid_edge_cases(big):
     """A11 1-NN on the target grids vs the oracle's brute force: sources far beyond every ball
     (the brute-force scan), exact-duplicate targets (index tie), targets exactly on a ball radius
-    (d2 == rs^2 is outside the ball), a non-finite source, sparse and dense targets. big: more
-    sources than the one-launch loop holds in LDS (ICP_LOOP_MAXN), i.e. the host-driven loop of
-    k_icp_grid launches."""
+    (d2 == rs^2 is outside the ball), a non-finite source, sparse and dense targets; sources that
+    move beyond their iteration-0 candidate lists fall back to the grid search. big: > 5000 sources
+    in dense clusters (candidate lists over capacity)."""
     rng = np.random.default_rng(11)
     tgt = (rng.random((5000, 3)) * [80000, 80000, 4000] - [40000, 40000, 2000]).astype(np.float32)
     tgt[100:110] = tgt[90]  # duplicates
