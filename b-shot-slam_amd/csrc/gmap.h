@@ -51,6 +51,10 @@ struct GMap {
     size_t blk_cap = 0;
     DBuf<int> ctr;
     PinBuf<int> p_ctr;
+    // an insert without a sync (the exchange) leaves the counters' copy in flight: ev_ctr marks it,
+    // and gmap_settle waits for it and checks the error word before the counters are read again
+    hipEvent_t ev_ctr = nullptr;
+    bool ctr_pending = false;
     DBuf<int> ipool;
     size_t ipool_cap = 0;
     DBuf<unsigned long long> cpool;
@@ -66,6 +70,7 @@ struct GMap {
         kpos.release(); kdesc.release(); tkey.release(); tval.release(); blk.release(); ctr.release(); p_ctr.release();
         ipool.release(); cpool.release(); kin.release(); refin.release(); p_kin.release(); p_refin.release(); p_tgt.release(); hrec.release(); p_hrec.release();
         keys.release(); vals.release(); seg.release(); qcnt.release(); tmp.release();
+        if (ev_ctr) (void)hipEventDestroy(ev_ctr);
     }
 };
 
@@ -92,6 +97,8 @@ int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax,
 // host records (bshot_odom_map_delta's 15-float layout) -> replica map (synchronous)
 int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n);
 int gmap_replica_size(bshot_ctx* c, int replica);
+// every replica's last unsynchronised insert has landed without error (else BSHOT_ECAP)
+int gmap_settle_replicas(bshot_ctx* c);
 // replica's entries around pos (block loop order; libstdc++ or canonical order) -> host; count or -needed
 int gmap_replica_query(bshot_ctx* c, int replica, const float pos[3], float range, int canonical, float* xyz,
                        unsigned int* bits, int cap);

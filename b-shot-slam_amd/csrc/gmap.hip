@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "ctx.h"
@@ -537,10 +538,21 @@ static GMap& replica_map(bshot_ctx* c, int r) {
     return *c->gmap_replicas[r];
 }
 
-// room for one more batch of k keypoints (counters as of the map's last D2H, which a later sync on
-// the stream has completed): slots, blocks, table load <= 1/2, pools at most half full (a batch
-// can at most double what its blocks hold)
+// the counters' copy of an unsynchronised insert has landed, and that insert reported no error
+// (a replica's capacity failure must not pass silently)
+static int gmap_settle(bshot_ctx* c, GMap& g) {
+    if (!g.ctr_pending) return BSHOT_OK;
+    HIPCHK(hipEventSynchronize(g.ev_ctr), "sync map counters");
+    g.ctr_pending = false;
+    if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > 4096 members, or pool)", BSHOT_ECAP);
+    return BSHOT_OK;
+}
+
+// room for one more batch of k keypoints (counters as of the map's last D2H, which gmap_settle or a
+// later sync on the stream has completed): slots, blocks, table load <= 1/2, pools at most half full
+// (a batch can at most double what its blocks hold)
 static int gmap_reserve(bshot_ctx* c, GMap& g, int k) {
+    if (int rc = gmap_settle(c, g)) return rc;
     const int* h = g.p_ctr.p;
     HIPCHK(grow_keep(g.kpos, (size_t)g.slots, (size_t)g.slots + k + 1, c->stream), "gmap slots");
     HIPCHK(grow_keep(g.kdesc, 11 * (size_t)g.slots, 11 * ((size_t)g.slots + k + 1), c->stream), "gmap slots");
@@ -598,7 +610,12 @@ static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync) {
     HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, c->stream), "D2H map counters");
     if (sync) {
         HIPCHK(hipStreamSynchronize(c->stream), "sync map");
-        if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > LDS image or pool)", BSHOT_ECAP);
+        g.ctr_pending = false;
+        if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > 4096 members, or pool)", BSHOT_ECAP);
+    } else {
+        if (!g.ev_ctr) HIPCHK(hipEventCreateWithFlags(&g.ev_ctr, hipEventDisableTiming), "map event");
+        HIPCHK(hipEventRecord(g.ev_ctr, c->stream), "record map counters");
+        g.ctr_pending = true;
     }
     return BSHOT_OK;
 }
@@ -638,7 +655,10 @@ int gmap_pack_delta(bshot_ctx* c, int kmax, float* d_rec) {
     GMap& g = own_map(c);
     int rc = gmap_init(c, g);
     if (rc) return rc;
-    const int k = std::min(g.last_k, kmax);
+    if (g.last_k > kmax)
+        return c->fail("map exchange: the sweep offered " + std::to_string(g.last_k) + " keypoints, more than the "
+                       "exchange's kmax " + std::to_string(kmax), BSHOT_EINVAL);
+    const int k = g.last_k;
     bsk::k_gmap_pack<<<(std::max(k, 1) + 255) / 256, 256, 0, c->stream>>>(dev_view(g), g.slots - g.last_k, k, kmax, d_rec);
     HIPCHK(hipGetLastError(), "gmap pack launch");
     return BSHOT_OK;
@@ -669,10 +689,18 @@ int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n)
     return gmap_insert_records(c, replica, g.hrec.p, n, true);
 }
 
+int gmap_settle_replicas(bshot_ctx* c) {
+    for (GMap* g : c->gmap_replicas)
+        if (g)
+            if (int rc = gmap_settle(c, *g)) return rc;
+    return BSHOT_OK;
+}
+
 int gmap_replica_size(bshot_ctx* c, int replica) {
     if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
     GMap& g = *c->gmap_replicas[replica];
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    g.ctr_pending = false;
     if (g.p_ctr.p[GM_ERR]) return -2;
     return g.p_ctr.p[GM_MEMBERS];
 }
@@ -725,9 +753,11 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
     // the maps whose entries become targets: this sequence's, then (option xseq_targets, an
     // extension for cross-sequence matching; off reproduces the reference) the replicas in rank order
     std::vector<GMap*> maps{&g};
-    if (c->opt_xseq_targets)
+    if (c->opt_xseq_targets) {
+        if ((rc = gmap_settle_replicas(c))) return rc;  // a replica that failed an insert is not matched against
         for (GMap* r : c->gmap_replicas)
             if (r && r->ready) maps.push_back(r);
+    }
     bool any = false;
     for (GMap* m : maps) {
         if ((rc = query_count(c, *m, q))) return rc;

@@ -118,7 +118,10 @@ int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self) {
     if (!c || !x) return BSHOT_EINVAL;
     if (!c->gmap) return BSHOT_ESTATE;
     const size_t per = bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * x->kmax;
-    int rc = bsh::gmap_pack_delta(c, x->kmax, x->send);
+    // the previous exchange's inserts (queued without a sync) must have succeeded
+    int rc = bsh::gmap_settle_replicas(c);
+    if (rc) return rc;
+    rc = bsh::gmap_pack_delta(c, x->kmax, x->send);
     if (rc) return rc;
     const int e = rccl().all_gather(x->send, x->recv, per, kNcclFloat32, x->comm, c->stream);
     if (e != 0) return c->fail(std::string("ncclAllGather: ") + (rccl().err ? rccl().err(e) : "error"), BSHOT_EHIP);

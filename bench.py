@@ -7,10 +7,12 @@ match (map query + Hamming) + RANSAC + gate + ICP + map update, i.e. bshot_odom_
 Workload = BASELINE config 2 sizes (130k-pt HDL-64 sweep, 2048 keypoints) run as a sequence so
 every step also matches against the map (configs[2] semantics).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each running its own sequence (scene seed 42 + rank): frames shard with no data-path
-collective ("scaling": "weak"). --map-bcast additionally all-gathers every frame's map delta
-(K x 60 B) over RCCL and inserts it into per-rank replica maps (BASELINE config 4).
+Multi-GPU: `bench.py --gpus N` starts N ranks itself (a torch.distributed.run child, launched before
+anything touches the GPU; the driver's own `torch.distributed.run ... bench.py --gpus N` works the
+same). One process per GPU, each running its own sequence (scene seed 42 + rank): frames shard with
+no data-path collective ("scaling": "weak"); with N > 1 every sweep's map offer (K x 60 B) is also
+all-gathered over RCCL and inserted into per-rank GPU replica maps (BASELINE config 4, the map
+B-SHOT set broadcast; --no-map-bcast turns it off).
 
 Prints ONE JSON line (rank 0). Roofline / cpu_baseline fields: DESIGN.md "Measurement".
 """
@@ -59,7 +61,8 @@ def parse():
     ap.add_argument("--sensor", type=int, default=0, help="0 HDL-64 (130k), 1 VLP-128 style (256k), 2 HDL-32E (--from-lasers only)")
     ap.add_argument("--shot-radius", type=float, default=3000.0)
     ap.add_argument("--map-bcast", action="store_true",
-                    help="per-sweep map exchange between ranks (C++ over RCCL, into GPU replicas)")
+                    help="per-sweep map exchange between ranks (C++ over RCCL, into GPU replicas); on by default for N > 1")
+    ap.add_argument("--no-map-bcast", action="store_true", help="N > 1 without the map exchange")
     ap.add_argument("--map-bcast-py", action="store_true",
                     help="with --map-bcast: the Python all_gather of host records into host replicas instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -77,9 +80,29 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(a):
+    """--gpus N > 1 outside a torch.distributed launcher: run N ranks as a child launcher process and
+    return its exit code (this process never touches the GPU)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and a.gpus != world:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; the launcher's world size is used", file=sys.stderr)
+    a.map_bcast = (a.map_bcast or world > 1) and not a.no_map_bcast
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

@@ -63,3 +63,70 @@ def test_gpu_map_lookahead_full_size():
             assert np.array_equal(_u(st.pose), _u(so.pose)), f
     finally:
         od.close()
+
+
+def _rec(xyz, ratio, rng):
+    """map-delta records (x, y, z on the 10 mm grid, ratio, 11 descriptor words) as float32 rows"""
+    n = len(xyz)
+    rec = np.zeros((n, 15), np.float32)
+    rec[:, :3] = xyz
+    rec[:, 3] = ratio
+    rec[:, 4:] = rng.integers(0, 2 ** 32, (n, 11), dtype=np.uint64).astype(np.uint32).view(np.float32)
+    return rec
+
+
+def _host_add(hm, rec):
+    for r in rec:
+        hm.add(r[:3].copy(), float(r[3]), r[4:].view(np.uint32).copy())
+
+
+def test_gmap_crafted_inserts_vs_host_map():
+    """k_gmap_insert's subtle paths against the host Map (myslam::Map restated, itself checked against
+    libstdc++'s unordered_map in test_host.py), through GPU replica inserts of crafted batches:
+    exact-position repeats with rising ratios (operator[] replacement), several candidates of one
+    batch in one 800 mm neighbourhood (suppression in sweep order), and a block growing past 2400
+    members in one batch (rehashes up to 5087 buckets inside the workgroup's LDS image)."""
+    rng = np.random.default_rng(3)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=64))
+    hm = bshot_py.KeypointMap()
+    try:
+        batches = []
+        # exact repeats and rising ratios, plus near neighbours in the same batch
+        base = np.array([[120.0, 340.0, -50.0], [900.0, 340.0, -50.0], [120.0, 1500.0, 10.0]], np.float32)
+        pts = np.concatenate([base, base, base + [10.0, 0.0, 0.0], base]).astype(np.float32)
+        batches.append(_rec(pts, np.linspace(0.1, 0.9, len(pts)).astype(np.float32), rng))
+        batches.append(_rec(base, np.array([0.95, 0.05, 0.5], np.float32), rng))
+        # one block (ids round(p / 1e4)) past 2400 members: rising ratios admit every candidate
+        g = np.stack(np.meshgrid(np.arange(-4800, 4800, 360), np.arange(-4800, 4800, 360), np.arange(-1000, 1000, 500)),
+                     -1).reshape(-1, 3).astype(np.float32) + [20000.0, 0.0, 0.0]
+        g = g[rng.permutation(len(g))][:2600]
+        batches.append(_rec(g, np.linspace(0.01, 0.99, len(g)).astype(np.float32), rng))
+        # a later batch into the same dense block: exact repeats of members and new points
+        again = np.concatenate([g[:50], g[100:150] + [10.0, 10.0, 0.0]]).astype(np.float32)
+        batches.append(_rec(again, rng.uniform(0, 1, len(again)).astype(np.float32), rng))
+        for rec in batches:
+            od.gpu_replica_insert(0, rec)
+            _host_add(hm, rec)
+            assert od.gpu_replica_size(0) == hm.size()
+            for pos in ([0.0, 0.0, 0.0], [20000.0, 0.0, 0.0]):
+                gx, gb = od.gpu_replica_query(0, np.array(pos, np.float32))
+                hx, hb = hm.query(np.array(pos, np.float32))
+                assert np.array_equal(_u(gx), _u(hx)) and np.array_equal(gb, hb)
+        assert hm.size() > 2400
+    finally:
+        od.close()
+
+
+def test_gmap_block_capacity_error_surfaces():
+    """A 10 m block holds at most 4096 members in the GPU map (the insert workgroup's LDS image;
+    DESIGN.md §3). Going past it is reported (BSHOT_ECAP), never silently dropped."""
+    rng = np.random.default_rng(4)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=64))
+    try:
+        g = np.stack(np.meshgrid(np.arange(-4900, 4900, 240), np.arange(-4900, 4900, 240), np.arange(-1000, 1000, 500)),
+                     -1).reshape(-1, 3).astype(np.float32)
+        assert len(g) > 4096
+        with pytest.raises(bshot_py.BshotError):
+            od.gpu_replica_insert(0, _rec(g, np.linspace(0.01, 0.99, len(g)).astype(np.float32), rng))
+    finally:
+        od.close()

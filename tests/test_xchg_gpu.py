@@ -128,3 +128,69 @@ def test_two_ranks_identical_replicas_and_solo_poses():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}, res
+
+
+def _rccl_rank(rank, world, port, q):
+    """One rank on its own GPU: the sequence's map offers go over RCCL (host/xchg.cpp) into every
+    rank's GPU replicas, including its own (include_self)."""
+    import torch.distributed as dist
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        uid = [bshot_py.Exchange.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)  # the RCCL id travels once over the process group
+        frames = _frames(seed=42 + rank, n=5)
+        solo = bshot_py.Odometry(rank, bshot_py.default_params(num_keypoints=K))
+        solo_poses = [_u(solo.process(x).pose).copy() for x in frames]
+        solo.close()
+        x = bshot_py.Exchange(uid[0], world, rank, rank, K)
+        od = bshot_py.Odometry(rank, bshot_py.default_params(num_keypoints=K))
+        ok = True
+        for f, xyz in enumerate(frames):
+            st = od.process(xyz)
+            ok &= np.array_equal(_u(st.pose), solo_poses[f])
+            od.exchange(x, include_self=True)
+            sizes = [None] * world
+            dist.all_gather_object(sizes, st.map_size)
+            ok &= all(od.gpu_replica_size(r) == sizes[r] for r in range(world))
+            digest = []
+            for r in range(world):
+                xyz_r, bits_r = od.gpu_replica_query(r, np.array([0.0, 800.0 * f, 0.0], np.float32))
+                digest.append(hashlib.sha1(_u(xyz_r).tobytes() + bits_r.tobytes()).hexdigest())
+            digests = [None] * world
+            dist.all_gather_object(digests, digest)
+            ok &= all(d == digests[0] for d in digests)
+        od.close()
+        x.close()
+        dist.destroy_process_group()
+        q.put((rank, bool(ok)))
+    except Exception as e:  # reported to the parent
+        q.put((rank, repr(e)))
+
+
+def _gpu_count():
+    import torch
+
+    return torch.cuda.device_count()  # counting does not initialise the GPU
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs 2 GPUs: a rank per GPU with an RCCL communicator between them "
+                                           "(the 1-GPU box runs the 1-rank RCCL test and the 2-rank gloo test)")
+def test_two_ranks_rccl_two_gpus():
+    """BASELINE config 4 on 2 GPUs over RCCL: every rank's poses equal its solo run's, and both ranks
+    hold identical replicas of both sequences' maps (entries, order, sizes)."""
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rccl_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}, res
