@@ -63,7 +63,7 @@ ABI_SYMBOLS = [
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
     "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
-    "bshot_odom_set_option", "bshot_odom_drain", "bshot_xchg_unique_id", "bshot_xchg_create",
+    "bshot_odom_set_option", "bshot_odom_set_metrics_file", "bshot_odom_upload", "bshot_odom_drain", "bshot_xchg_unique_id", "bshot_xchg_create",
     "bshot_xchg_destroy", "bshot_odom_exchange", "bshot_odom_gpu_replica_size", "bshot_odom_gpu_replica_query",
     "bshot_odom_gpu_replica_insert", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
     "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
@@ -524,6 +524,14 @@ class Odometry:
     def set_option(self, name, value):
         if self.L.bshot_odom_set_option(self.h, name.encode(), int(value)) < 0:
             raise BshotError(f"set_option {name}")
+
+    def upload(self, d_dst, h_src, n):
+        """sweep upload (pinned host -> device) queued ahead of its lookahead work (bshot_odom_upload)"""
+        self._chk(self.L.bshot_odom_upload(self.h, P(d_dst), P(h_src), int(n)), "upload")
+
+    def set_metrics_file(self, path):
+        """per-sweep JSON lines (counts, gate and its reasons, pose, host ms per phase); None stops"""
+        self._chk(self.L.bshot_odom_set_metrics_file(self.h, (path or "").encode()), "set_metrics_file")
 
     def set_timing(self, on):
         self.L.bshot_set_timing(P(self.context()), 1 if on else 0)

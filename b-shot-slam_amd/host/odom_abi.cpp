@@ -1,6 +1,10 @@
 // odom_abi.cpp -- C ABI over myslam::LidarOdometry: the headless odometry_test frame loop
 // (test/odometry_test.cpp:159-194, test/kp_test.cpp:159-181) plus the map-delta records used by
 // the multi-GPU throughput mode (BASELINE config 4). No exception crosses the ABI.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <functional>
@@ -29,6 +33,11 @@ struct bshot_odom {
     int next_n = 0;
     const float* next2_d = nullptr;  // the one after (bshot_odom_set_next2_device)
     int next2_n = 0;
+    std::FILE* metrics = nullptr;  // per-sweep JSON lines (bshot_odom_set_metrics_file / BSHOT_METRICS)
+    long long sweep = 0;
+    ~bshot_odom() {
+        if (metrics) std::fclose(metrics);
+    }
 };
 
 static int guard(bshot_odom* o, const std::function<void()>& f);
@@ -37,7 +46,34 @@ namespace {
 
 constexpr int kRec = 15;  // x, y, z, ratio, 11 descriptor words (bit patterns)
 
+// one JSON line per sweep: the counts of every stage, the gate's decision and why
+// (src/lidar_odometry.cpp:283-290: heading > 10 deg, |t| > 1200 mm, < 15 inliers), the pose and the
+// main thread's wall ms per phase. The reference only prints these (cout, :128,167,244,274-279).
+void write_metrics(bshot_odom* o, const bshot_frame_stats& s, double wall_ms) {
+    if (!o->metrics) return;
+    const double h_deg = (double)s.h_diff * 180.0 / M_PI;
+    std::string why;
+    if (h_deg > 10) why += "\"heading\",";
+    if (s.t_diff > 1200) why += "\"translation\",";
+    if (s.n_inliers < 15) why += "\"inliers\",";
+    if (!why.empty()) why.pop_back();
+    std::fprintf(o->metrics,
+                 "{\"sweep\": %lld, \"n_points\": %d, \"n_valid_ratios\": %d, \"n_keypoints\": %d, \"n_iss\": %d, "
+                 "\"n_target\": %d, \"n_mutual\": %d, \"n_inliers\": %d, \"icp_iters\": %d, \"gated\": %d, "
+                 "\"gate_reasons\": [%s], \"h_diff_deg\": %.6g, \"t_diff_mm\": %.6g, \"map_size\": %d, "
+                 "\"wall_ms\": %.4f, \"host_ms\": {\"extract\": %.4f, \"iss\": %.4f, \"describe\": %.4f, "
+                 "\"match\": %.4f, \"ransac\": %.4f, \"icp\": %.4f, \"map\": %.4f, \"kp_eval\": %.4f}, \"pose\": [",
+                 o->sweep, s.n_points, s.n_valid_ratios, s.n_keypoints, s.n_iss, s.n_target, s.n_mutual, s.n_inliers,
+                 s.icp_iters, s.gated, why.c_str(), std::isfinite(h_deg) ? h_deg : -1.0,
+                 std::isfinite(s.t_diff) ? (double)s.t_diff : -1.0, s.map_size, wall_ms, s.host_ms[0], s.host_ms[1],
+                 s.host_ms[2], s.host_ms[3], s.host_ms[4], s.host_ms[5], s.host_ms[6], s.host_ms[7]);
+    for (int i = 0; i < 12; ++i) std::fprintf(o->metrics, i ? ", %.9g" : "%.9g", (double)s.pose[i]);
+    std::fprintf(o->metrics, "]}\n");
+    std::fflush(o->metrics);
+}
+
 int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_frame_stats* st) {
+    const auto t0 = std::chrono::steady_clock::now();
     myslam::LidarOdometry& lo = *o->lo;
     myslam::Frame::Ptr f = myslam::Frame::createFrame();
     if (xyz) {
@@ -65,6 +101,10 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     lo.updateMap();
     lo.updateCorrespondence();
     if (st) *st = lo.lastStats();
+    if (o->metrics)
+        write_metrics(o, lo.lastStats(),
+                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    ++o->sweep;
     // map delta inputs (the records are built only when bshot_odom_map_delta asks for them)
     o->d_pose = f->getPose();
     o->d_kps = f->getKeypoints();
@@ -126,7 +166,32 @@ int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p) {
         delete o;
         return BSHOT_EHIP;
     }
+    if (const char* path = std::getenv("BSHOT_METRICS")) o->metrics = std::fopen(path, "a");
     *out = o;
+    return BSHOT_OK;
+}
+
+int bshot_odom_upload(bshot_odom* o, float* d_dst, const float* h_src, int n) {
+    if (!o || n < 0 || (n > 0 && (!d_dst || !h_src))) return BSHOT_EINVAL;
+    bshot_ctx* c = o->lo->context();
+    (void)hipSetDevice(c->device);
+    if (bsh::kcopy(d_dst, h_src, sizeof(float) * 3 * (size_t)n, c->pre) != hipSuccess) {
+        o->err = "upload: kernel copy launch";
+        return BSHOT_EHIP;
+    }
+    return BSHOT_OK;
+}
+
+int bshot_odom_set_metrics_file(bshot_odom* o, const char* path) {
+    if (!o) return BSHOT_EINVAL;
+    if (o->metrics) std::fclose(o->metrics);
+    o->metrics = nullptr;
+    if (!path || !*path) return BSHOT_OK;
+    o->metrics = std::fopen(path, "w");
+    if (!o->metrics) {
+        o->err = std::string("cannot open ") + path;
+        return BSHOT_EINVAL;
+    }
     return BSHOT_OK;
 }
 

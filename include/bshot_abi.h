@@ -204,8 +204,17 @@ int bshot_odom_set_next_device(bshot_odom* o, const float* d_next, int n_next);
 /* the cloud after that (two calls ahead): its grids, SR and ISS are queued as well, so they run
  * beside the next sweep's describe. Optional; same validity rule. */
 int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2);
+/* a sweep's upload (n points, pinned host memory -> device), queued by a kernel on the stream the
+ * sweep's grids/SR/ISS run on when it is set as next2: ordered before them without a host wait.
+ * Call it before bshot_odom_set_next2_device with the same d_dst. */
+int bshot_odom_upload(bshot_odom* o, float* d_dst, const float* h_src, int n);
 /* odometry knobs: forwarded to bshot_set_option on the odometry's context */
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value);
+/* per-sweep metrics as JSON lines (the reference only prints them): every stage's
+ * counts, gated + gate_reasons (heading / translation / inliers, src/lidar_odometry.cpp:283-290),
+ * h/t diff, map size, the main thread's wall ms per phase and the 3x4 pose. path NULL or "" stops.
+ * The environment variable BSHOT_METRICS=<path> turns it on (append) for every odometry created. */
+int bshot_odom_set_metrics_file(bshot_odom* o, const char* path);
 /* Multi-GPU map exchange (BASELINE config 4; extension, no reference counterpart):
  * one process per GPU; rank 0 makes the 128-byte RCCL id (bshot_xchg_unique_id), every rank receives
  * it (any side channel, e.g. torch.distributed) and calls bshot_xchg_create. bshot_odom_exchange,

@@ -124,3 +124,26 @@ def test_kp_test_config1_kp_evaluation(sensor, frames, lo, hi):
             assert np.array_equal(_u(np.array(st.pose)), _u(np.array(so.pose))), f
     finally:
         od.close()
+
+
+def test_metrics_jsonl(tmp_path):
+    """Per-sweep JSON lines (bshot_odom_set_metrics_file): one line per sweep with the stats the
+    process call returned, the gate's reasons and the pose."""
+    import json
+
+    path = tmp_path / "m.jsonl"
+    frames = [bshot_py.synth_sweep(f)[0][::2].copy() for f in range(3)]
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=400))
+    od.set_metrics_file(str(path))
+    stats = [od.process(x) for x in frames]
+    od.set_metrics_file(None)
+    od.close()
+    lines = [json.loads(s) for s in path.read_text().splitlines()]
+    assert len(lines) == 3
+    for i, (ln, st) in enumerate(zip(lines, stats)):
+        assert ln["sweep"] == i
+        for k in ("n_points", "n_keypoints", "n_target", "n_mutual", "n_inliers", "icp_iters", "gated", "map_size"):
+            assert ln[k] == getattr(st, k), k
+        assert np.allclose(ln["pose"], np.array(st.pose, np.float64)[:12], rtol=0, atol=1e-3)
+        assert bool(ln["gated"]) == bool(ln["gate_reasons"])
+        assert set(ln["host_ms"]) == set(bshot_py.FrameStats.HOST_PHASES)
