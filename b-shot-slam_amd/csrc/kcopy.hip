@@ -56,12 +56,13 @@ __global__ void __launch_bounds__(KC_THREADS) k_fill1(unsigned char* __restrict_
 
 namespace bsh {
 
-static inline int kc_blocks(size_t units) {
+static inline int kc_blocks(size_t units, int cap = KC_MAX_BLOCKS) {
     const size_t b = (units + KC_THREADS - 1) / KC_THREADS;
-    return (int)(b < 1 ? 1 : (b > KC_MAX_BLOCKS ? KC_MAX_BLOCKS : b));
+    return (int)(b < 1 ? 1 : (b > (size_t)cap ? (size_t)cap : b));
 }
 
-hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s, int max_blocks) {
+    if (max_blocks < 1) max_blocks = KC_MAX_BLOCKS;
     if (bytes == 0 || dst == src) return hipSuccess;
     if (!dst || !src) return hipErrorInvalidValue;
     const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
@@ -70,16 +71,16 @@ hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s) {
     if ((a & 15) == 0) {
         const size_t n16 = bytes / 16;
         const int tail = (int)(bytes % 16);
-        bsk::k_copy16<<<kc_blocks(n16), KC_THREADS, 0, s>>>(reinterpret_cast<uint4*>(d), reinterpret_cast<const uint4*>(p),
+        bsk::k_copy16<<<kc_blocks(n16, max_blocks), KC_THREADS, 0, s>>>(reinterpret_cast<uint4*>(d), reinterpret_cast<const uint4*>(p),
                                                             n16, d + 16 * n16, p + 16 * n16, tail);
     } else if ((a & 3) == 0) {
         const size_t n4 = bytes / 4;
         const int tail = (int)(bytes % 4);
-        bsk::k_copy4<<<kc_blocks(n4), KC_THREADS, 0, s>>>(reinterpret_cast<unsigned int*>(d),
+        bsk::k_copy4<<<kc_blocks(n4, max_blocks), KC_THREADS, 0, s>>>(reinterpret_cast<unsigned int*>(d),
                                                           reinterpret_cast<const unsigned int*>(p), n4, d + 4 * n4,
                                                           p + 4 * n4, tail);
     } else {
-        bsk::k_copy1<<<kc_blocks(bytes), KC_THREADS, 0, s>>>(d, p, bytes);
+        bsk::k_copy1<<<kc_blocks(bytes, max_blocks), KC_THREADS, 0, s>>>(d, p, bytes);
     }
     return hipGetLastError();
 }

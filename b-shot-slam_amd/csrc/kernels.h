@@ -8,7 +8,9 @@ namespace bsh {
 
 // copies / fills as kernels on stream s (csrc/kcopy.hip): device memory and the pinned staging
 // buffers only (never pageable host memory). The sweep loop issues no copy-engine transfer.
-hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s);
+// max_blocks: grid cap (a bulk copy that reads host memory holds its CUs for the transfer's
+// duration; a small grid leaves the rest to the concurrent kernels)
+hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s, int max_blocks = 0);
 hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s);
 
 // g4: the radius-ladder grids (cells r/16, r/8, r/4, r/2 for ladder modes 1, 2; r/8, r/8, r/2, r/2

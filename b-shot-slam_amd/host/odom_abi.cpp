@@ -175,7 +175,9 @@ int bshot_odom_upload(bshot_odom* o, float* d_dst, const float* h_src, int n) {
     if (!o || n < 0 || (n > 0 && (!d_dst || !h_src))) return BSHOT_EINVAL;
     bshot_ctx* c = o->lo->context();
     (void)hipSetDevice(c->device);
-    if (bsh::kcopy(d_dst, h_src, sizeof(float) * 3 * (size_t)n, c->pre) != hipSuccess) {
+    // 32 workgroups: a full-chip grid would hold every CU while it waits on PCIe reads (8, 32, 1024
+    // workgroups and an SDMA copy measured alike, 369-375 sweeps/s, experiments/README.md)
+    if (bsh::kcopy(d_dst, h_src, sizeof(float) * 3 * (size_t)n, c->pre, 32) != hipSuccess) {
         o->err = "upload: kernel copy launch";
         return BSHOT_EHIP;
     }

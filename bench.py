@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--no-upload-leg", action="store_true",
                     help="skip the second timed leg whose sweeps start in pinned host memory (upload inside the region)")
     ap.add_argument("--metrics", default=None, help="per-sweep JSON lines of rank 0 (bshot_odom_set_metrics_file)")
-    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=5)
     ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage HIP events in the timed region")
     ap.add_argument("--depth", type=int, default=2, help="lookahead depth (1: next sweep only, 2: two sweeps)")
@@ -203,7 +203,50 @@ def main():
             mk_.append(time.perf_counter())
         return t_0, st_, mk_
 
-    # ---- second leg (same sequence, fresh odometry): the sweeps start in pinned host memory and each
+    for i in range(a.warmup):
+        step(i)
+    # HIP events cost host time on every launch they bracket: in the default run only the stage of
+    # the roofline kernel (SR) is timed; --profile-stages times them all
+    odo.set_option("timing_mask", -1 if a.profile_stages else 1 << 1)
+    odo.set_timing(not a.no_stage_timing)
+    odo.stage_reset()
+    if pre_ctx is not None:
+        pre_ctx.set_timing(True)
+        pre_ctx.stage_reset()
+    t0, stats, marks = timed(step)
+    tot_pts = int(sum(npts[a.warmup:nwork]))
+    odo.drain()  # the lookahead started by the last timed sweep finishes inside the region
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    stages = odo.stage_times()
+    odo.set_timing(False)
+    if pre_ctx is not None:
+        stages["preprocess"] = pre_ctx.stage_times()["preprocess"]
+        pre_ctx.set_timing(False)
+    el_max = el
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+    sweeps = a.steps * world
+    value = sweeps / el_max
+
+    wc_main = None
+    if os.environ.get("BENCH_INTERVALS"):
+        import ctypes
+        wc = (ctypes.c_int64 * 8)()
+        bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 8)
+        wc_main = list(wc)
+    if xchg is not None:
+        xchg.close()
+        xchg = None
+    # one odometry per device at a time: a second context's four streams share the process's four
+    # hardware queues with the first one's (GPU_MAX_HW_QUEUES), which measured 15-20 % slower
+    odo.close()
+
+    # ---- second leg (same sequence, fresh odometry, after the first one is closed): the sweeps start in pinned host memory and each
     # one's upload (a kernel copy on the queue stream, bshot_odom_upload) is issued two sweeps ahead,
     # inside the timed region -- SURVEY.md §8(d)'s "from cloud upload" (the reference's setSrcFrame
     # copy). Reported beside `value` (which keeps the sweeps HBM-resident), never as it.
@@ -257,36 +300,6 @@ def main():
                       "path": "pinned host memory -> HBM by a kernel copy on the queue stream, issued two sweeps "
                               "ahead (bshot_odom_upload), inside the timed region"}
         del host, dbuf
-
-    for i in range(a.warmup):
-        step(i)
-    # HIP events cost host time on every launch they bracket: in the default run only the stage of
-    # the roofline kernel (SR) is timed; --profile-stages times them all
-    odo.set_option("timing_mask", -1 if a.profile_stages else 1 << 1)
-    odo.set_timing(not a.no_stage_timing)
-    odo.stage_reset()
-    if pre_ctx is not None:
-        pre_ctx.set_timing(True)
-        pre_ctx.stage_reset()
-    t0, stats, marks = timed(step)
-    tot_pts = int(sum(npts[a.warmup:nwork]))
-    odo.drain()  # the lookahead started by the last timed sweep finishes inside the region
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    stages = odo.stage_times()
-    odo.set_timing(False)
-    if pre_ctx is not None:
-        stages["preprocess"] = pre_ctx.stage_times()["preprocess"]
-        pre_ctx.set_timing(False)
-    el_max = el
-    if dist is not None:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_max = float(t.item())
-    sweeps = a.steps * world
-    value = sweeps / el_max
 
     # ---- roofline of the dominant kernel: SURVEY.md §8(d) algorithmic bytes / event-timed launches
     ctx = bshot_py.Context(local, params)
@@ -396,10 +409,7 @@ def main():
     if rank == 0:
         if os.environ.get("BENCH_INTERVALS"):
             iv = np.diff([t0] + marks) * 1e3
-            import ctypes
-            wc = (ctypes.c_int64 * 8)()
-            bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 8)
-            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": list(wc),
+            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": wc_main,
                               # CLOCK_MONOTONIC ms, the clock of BSHOT_GROW_TRACE's lines
                               "t0_ms": round(t0 * 1e3, 3), "marks_ms": np.round(np.array(marks) * 1e3, 3).tolist()}),
                   file=sys.stderr)
