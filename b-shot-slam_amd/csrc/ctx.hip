@@ -821,7 +821,8 @@ void bshot_destroy(bshot_ctx* c) {
     for (auto e : c->evpool) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->side);
     if (trace) std::fprintf(stderr, "destroy step 3\n");
-    if (c->htrace_on) {
+    // a context without marks (a second one in the same process) leaves the file alone
+    if (c->htrace_on && !c->htrace.empty()) {
         if (FILE* f = std::fopen(std::getenv("BSHOT_HOST_TRACE"), "w")) {
             for (auto& e : c->htrace) std::fprintf(f, "%s,%lld\n", e.first, e.second);
             std::fclose(f);

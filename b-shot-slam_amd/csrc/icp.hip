@@ -7,14 +7,15 @@
 // reduction order.
 //
 // Iteration 0 (k_icp_lists, a wave per source): the exact 1-NN at the source's starting position
-// q0, and a candidate list: every target within R of q0, R = d0 + {2000, 1000, 500, 250} mm (the
-// largest whose count fits the list capacity; d0 = the NN distance). Iterations >= 1
-// (k_icp_list_nn, a lane per source): the source moves rigidly by the step transform; its NN among
-// the list is the global NN whenever dm + |q - q0| < R (with float slack): a target outside the
-// list lies at least R from q0, so at least R - |q - q0| from q, farther than the list's best.
-// Sources failing the test (moved too far, no list, non-finite) take the exact grid search of
-// iteration 0 (a wave each). The targets' nested grids (cells 1000, 2000, 4000, 8000 mm) are built
-// once per ICP call.
+// q0, and a candidate list: every target within R of q0, R = d0 + {3000, 1500, 750, 350} mm (the
+// largest whose count fits the list capacity; d0 = the NN distance), sorted by distance from q0.
+// Iterations >= 1 (k_icp_iterations, one persistent launch, a lane per source): the source moves
+// rigidly by the step transform; its NN among the list is the global NN whenever
+// dm + |q - q0| < R (with float slack): a target outside the list lies at least R from q0, so at
+// least R - |q - q0| from q, farther than the list's best. Sources failing the test (moved too far,
+// no list, non-finite) take the exact grid search of iteration 0 (a wave each) and get a new list.
+// The targets' nested grids (cells 1000, 2000, 4000, 8000 mm) are built once per ICP call, queued
+// ahead of RANSAC (ctx_icp_prepare).
 #include <hip/hip_runtime.h>
 
 #include "bshot_math.h"

@@ -1,6 +1,8 @@
 """Condense one gpu_round.sh profile set into tracked files under profiles/.
 
-    python scripts/prof_summary.py r01   # reads gpurun_out/{prof,pmc_fetch,pmc_write}_r01
+    python scripts/prof_summary.py r01 [dst]   # reads gpurun_out/{prof,pmc_fetch,pmc_write}_r01
+(dst: output directory, default profiles/; gpu_round.sh writes gpurun_out/summary_<tag> on the box so
+that the raw traces can be dropped before gpurun copies gpurun_out/ back)
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary, verbatim) and
 profiles/<tag>_pmc.json: per kernel, mean FETCH_SIZE / WRITE_SIZE per dispatch in bytes.
@@ -75,9 +77,9 @@ def derive(e, c, dur, pmc_dur=None):
         e["limiter"] = "valu" if v >= l else "lds"
 
 
-def main(tag):
+def main(tag, dst=None):
     src = os.path.join(ROOT, "gpurun_out")
-    dst = os.path.join(ROOT, "profiles")
+    dst = dst or os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, f"prof_{tag}", "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 5 ({tag})",
@@ -142,4 +144,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else None)
