@@ -155,7 +155,8 @@ struct bshot_ctx {
     DBuf<float> kps;
     DBuf<int> counts;
     DBuf<long long> offs;
-    DBuf<unsigned long long> seg, segtmp;
+    DBuf<unsigned long long> seg;  // neighbour keys (d2 bits << 32 | idx), bucket-grouped (gather)
+    DBuf<unsigned int> segtmp;     // neighbour indices in (d2, idx) order (rank)
     DBuf<float> rf, shot;
     DBuf<int> ok;
     DBuf<unsigned int> bits;

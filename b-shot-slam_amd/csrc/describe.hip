@@ -2,10 +2,10 @@
 // SHOTLocalReferenceFrameEstimation radius search, include/bshot_bits.h:113-135): the sorted
 // (d2, idx) neighbour list of every keypoint that csrc/describe2.hip's LRF / histogram kernels read.
 //
-//   k_shot_count    wave/keypoint: |B(kp, R)| over the hashed grid + a 1024-bucket d2 histogram
+//   k_shot_count    workgroup/keypoint: |B(kp, R)| over the hashed grid + a 1024-bucket d2 histogram
 //   k_desc_plan     one workgroup: segment offsets, 64-rank chunk bases, LPT order, on the device
 //   k_excl_scan     one workgroup: segment offsets (host-planned describe after a plan overflow)
-//   k_shot_gather_b wave/keypoint: keys (d2 bits << 32 | idx) scattered bucket-grouped
+//   k_shot_gather_b workgroup/keypoint: keys (d2 bits << 32 | idx) scattered bucket-grouped
 //   k_shot_rank     wave per 64-rank chunk: exact rank inside each bucket -> FLANN's sorted order
 #include <hip/hip_runtime.h>
 
@@ -24,33 +24,38 @@ __device__ __forceinline__ int sg_bucket(float d2, float sc) {
     return b < 0 ? 0 : (b > SG_BUCKETS - 1 ? SG_BUCKETS - 1 : b);
 }
 
-// bh (nullable): per-keypoint histogram of the in-radius d2 over SG_BUCKETS buckets, [k][SG_BUCKETS]
-__global__ void __launch_bounds__(256) k_shot_count(GridView g, const float* __restrict__ kps, int k, float R,
-                                                    int* __restrict__ counts, unsigned int* __restrict__ bh) {
-    __shared__ CandLds lds[4];
-    __shared__ unsigned int hist[4][SG_BUCKETS];
+// bh (nullable): per-keypoint histogram of the in-radius d2 over SG_BUCKETS buckets, [k][SG_BUCKETS].
+// A workgroup per keypoint: its 4 waves stream every 4th candidate group of the keypoint's cube
+// (for_candidates' part / nparts), so a large neighbourhood takes a quarter of the dependent
+// round trips (the wave-per-keypoint kernel's tail was its largest keypoint: 0.33 ms under load).
+#define SG_WAVES 4
+__global__ void __launch_bounds__(64 * SG_WAVES) k_shot_count(GridView g, const float* __restrict__ kps, int k, float R,
+                                                             int* __restrict__ counts, unsigned int* __restrict__ bh) {
+    __shared__ CandLds lds[SG_WAVES];
+    __shared__ unsigned int hist[SG_BUCKETS];
+    __shared__ int tot;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
     const float sc = (float)SG_BUCKETS / R2;
-    unsigned int* h = hist[wave];
-    for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
+    for (int q = blockIdx.x; q < k; q += gridDim.x) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-        if (bh) {
-            for (int j = lane; j < SG_BUCKETS; j += 64) h[j] = 0u;
-            __builtin_amdgcn_wave_barrier();
-        }
+        if (bh)
+            for (int j = threadIdx.x; j < SG_BUCKETS; j += 64 * SG_WAVES) hist[j] = 0u;
+        if (threadIdx.x == 0) tot = 0;
+        __syncthreads();
         int c = 0;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))
             for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int) {
                 c += __popcll(__ballot(v));
-                if (bh && v) atomicAdd(&h[sg_bucket(d2, sc)], 1u);
-            });
-        if (bh) {
-            __builtin_amdgcn_wave_barrier();
-            for (int j = lane; j < SG_BUCKETS; j += 64) bh[(size_t)q * SG_BUCKETS + j] = h[j];
-        }
-        if (lane == 0) counts[q] = c;
+                if (bh && v) atomicAdd(&hist[sg_bucket(d2, sc)], 1u);
+            }, 0, wave, SG_WAVES);
+        if (lane == 0) atomicAdd(&tot, c);
+        __syncthreads();
+        if (bh)
+            for (int j = threadIdx.x; j < SG_BUCKETS; j += 64 * SG_WAVES) bh[(size_t)q * SG_BUCKETS + j] = hist[j];
+        if (threadIdx.x == 0) counts[q] = tot;
+        __syncthreads();
     }
 }
 
@@ -144,54 +149,59 @@ __global__ void __launch_bounds__(1024) k_excl_scan(const int* __restrict__ coun
 }
 
 // Bucketed gather: the keys land grouped by d2 bucket (buckets ascending, any order inside a
-// bucket): each wave scans its keypoint's bucket histogram (bh, from k_shot_count) into LDS
-// cursors, writes the bucket starts (bstart, relative to the segment) for k_shot_rank, and
-// scatters every in-radius key to its bucket's next slot.
-__global__ void __launch_bounds__(256) k_shot_gather_b(GridView g, const float* __restrict__ kps, int k, float R,
-                                                       const long long* __restrict__ offs,
-                                                       const unsigned int* __restrict__ bh,
-                                                       unsigned int* __restrict__ bstart,
-                                                       unsigned long long* __restrict__ seg,
-                                                       const int* __restrict__ err) {
-    __shared__ CandLds lds[4];
-    __shared__ unsigned int cur[4][SG_BUCKETS];
+// bucket): the workgroup scans its keypoint's bucket histogram (bh, from k_shot_count) into LDS
+// cursors, writes the bucket starts (bstart, relative to the segment) for k_shot_rank, and its 4
+// waves scatter every in-radius key of their share of the candidate groups to its bucket's next
+// slot (a workgroup per keypoint, as k_shot_count).
+__global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, const float* __restrict__ kps, int k, float R,
+                                                                const long long* __restrict__ offs,
+                                                                const unsigned int* __restrict__ bh,
+                                                                unsigned int* __restrict__ bstart,
+                                                                unsigned long long* __restrict__ seg,
+                                                                const int* __restrict__ err) {
+    __shared__ CandLds lds[SG_WAVES];
+    __shared__ unsigned int cu[SG_BUCKETS];
+    __shared__ int wsum[SG_WAVES];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
     const float sc = (float)SG_BUCKETS / R2;
-    unsigned int* cu = cur[wave];
-    constexpr int PER = SG_BUCKETS / 64;
+    constexpr int PER = SG_BUCKETS / (64 * SG_WAVES);  // buckets per thread
     if (err && (*err & 16)) return;  // device plan overflowed its capacity: the host re-plans
-    for (int q = blockIdx.x * 4 + wave; q < k; q += gridDim.x * 4) {
+    for (int q = blockIdx.x; q < k; q += gridDim.x) {
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         if (!(__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz))) continue;
-        // exclusive scan of the histogram: lane owns buckets [PER lane, PER lane + PER)
+        // exclusive scan of the histogram: thread t owns buckets [PER t, PER t + PER)
         unsigned int hv[PER];
         int s = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            hv[j] = bh[(size_t)q * SG_BUCKETS + PER * lane + j];
+            hv[j] = bh[(size_t)q * SG_BUCKETS + PER * threadIdx.x + j];
             s += (int)hv[j];
         }
-        int tot;
-        unsigned int run = (unsigned int)wave_excl_scan(s, tot);
+        int wt;
+        int run = wave_excl_scan(s, wt);
+        if (lane == 0) wsum[wave] = wt;
+        __syncthreads();
+        for (int w = 0; w < wave; ++w) run += wsum[w];
+        unsigned int ur = (unsigned int)run;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            cu[PER * lane + j] = run;
-            bstart[(size_t)q * SG_BUCKETS + PER * lane + j] = run;
-            run += hv[j];
+            cu[PER * threadIdx.x + j] = ur;
+            bstart[(size_t)q * SG_BUCKETS + PER * threadIdx.x + j] = ur;
+            ur += hv[j];
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
         unsigned long long* out = seg + offs[q];
         for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
             if (v) out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
-        });
-        __builtin_amdgcn_wave_barrier();
+        }, 0, wave, SG_WAVES);
+        __syncthreads();  // cu and wsum are rewritten for the next keypoint
     }
 }
 
 // wave per 64-rank chunk of a bucket-grouped segment: every key's exact (d2, idx) rank inside its
-// bucket -> the sorted segment (keys are unique, buckets hold a few keys each). The buckets the
+// bucket -> the sorted segment, stored as the neighbour indices alone (keys are unique, buckets hold a few keys each). The buckets the
 // chunk's keys belong to span [lo, hi) of the segment (the chunk plus the parts of its two end
 // buckets outside it); when that fits SR_STAGE keys it is staged in LDS and ranked from there.
 #define SR_STAGE 256
@@ -199,7 +209,7 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
                                                    const int* __restrict__ cb, const int* __restrict__ owner,
                                                    const unsigned int* __restrict__ bstart,
                                                    const unsigned long long* __restrict__ seg,
-                                                   unsigned long long* __restrict__ out) {
+                                                   unsigned int* __restrict__ out) {
     __shared__ unsigned long long stage[4][SR_STAGE];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
@@ -233,7 +243,7 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
         } else if (i < n) {
             for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
         }
-        if (i < n) out[o + s0 + rank] = key;
+        if (i < n) out[o + s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
         __builtin_amdgcn_wave_barrier();  // the next chunk restages
     }();
 }
@@ -245,7 +255,7 @@ namespace bsh {
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s, unsigned int* bh) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_count<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, counts, bh);
+    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
     bsk::k_excl_scan<<<1, 1024, 0, s>>>(counts, k, offs);
     return hipGetLastError();
 }
@@ -255,7 +265,7 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
                                   hipStream_t s) {
     if (k <= 0) return hipSuccess;
     if (k > DP_MAXK) return hipErrorInvalidValue;
-    bsk::k_shot_count<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, counts, bh);
+    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
     bsk::k_desc_plan<<<1, 1024, 0, s>>>(counts, k, seg_cap, chunk_cap, offs, cb, perm, err);
     return hipGetLastError();
 }
@@ -264,12 +274,12 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
                                 const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s,
                                 const int* err) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_gather_b<<<(k + 3) / 4, 256, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg, err);
+    bsk::k_shot_gather_b<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg, err);
     return hipGetLastError();
 }
 
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
-                            const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
+                            const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
                             hipStream_t s, int max_blocks) {
     if (k <= 0 || n_chunks <= 0) return hipSuccess;
     int blocks = (n_chunks + 3) / 4;

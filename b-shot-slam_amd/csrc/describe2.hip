@@ -32,18 +32,18 @@ __global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restric
 // csum[8 c + 0..5]: weighted covariance terms, [6]: weight sum, [7]: valid count of chunk c =
 // ranks [64 t, 64 t + 64) of keypoint q (wave; lanes 0..7 store)
 __device__ __forceinline__ void lrf_chunk_terms(const float4* __restrict__ pts4, float kx, float ky, float kz, float R,
-                                                const unsigned long long* __restrict__ sg, int n, int t,
+                                                const unsigned int* __restrict__ sg, int n, int t,
                                                 double* __restrict__ out8) {
     const int lane = lane_id();
     const int i = t * 64 + lane;
     double v[7] = {0, 0, 0, 0, 0, 0, 0};
     int isv = 0;
     if (i < n) {
-        const unsigned long long key = sg[i];
-        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+        const float4 p = pts4[sg[i]];
         if (!(p.x == kx && p.y == ky && p.z == kz)) {
             const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-            const double w = (double)R - sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+            // the gather's d2 (same expression and operands: the same bits as the ranked key's)
+            const double w = (double)R - sqrt((double)d2_flann(kx, ky, kz, p.x, p.y, p.z));
             v[0] = w * (vx * vx); v[1] = w * (vx * vy); v[2] = w * (vx * vz);
             v[3] = w * (vy * vy); v[4] = w * (vy * vz); v[5] = w * (vz * vz);
             v[6] = w;
@@ -65,7 +65,7 @@ __device__ __forceinline__ void lrf_chunk_terms(const float4* __restrict__ pts4,
 __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ pts4, const float* __restrict__ kps,
                                                     int k, float R, const long long* __restrict__ offs,
                                                     const int* __restrict__ cb, const int* __restrict__ owner,
-                                                    const unsigned long long* __restrict__ seg,
+                                                    const unsigned int* __restrict__ seg,
                                                     double* __restrict__ csum) {
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
     for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
@@ -134,13 +134,12 @@ __global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ c
 
 // #(v . x >= 0), #(v . z >= 0) over the valid neighbours of chunk t of a keypoint (wave-uniform result)
 __device__ __forceinline__ int2 lrf_sign_counts(const float4* __restrict__ pts4, float kx, float ky, float kz,
-                                                const unsigned long long* __restrict__ sg, int n, int t, const double* e) {
+                                                const unsigned int* __restrict__ sg, int n, int t, const double* e) {
     const int lane = lane_id();
     const int i = t * 64 + lane;
     int pt = 0, pn = 0;
     if (i < n) {
-        const unsigned long long key = sg[i];
-        const float4 p = pts4[(unsigned)(key & 0xFFFFFFFFu)];
+        const float4 p = pts4[sg[i]];
         if (!(p.x == kx && p.y == ky && p.z == kz)) {
             const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
             if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
@@ -154,7 +153,7 @@ __device__ __forceinline__ int2 lrf_sign_counts(const float4* __restrict__ pts4,
 __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
                                                   const int* __restrict__ owner,
-                                                  const unsigned long long* __restrict__ seg,
+                                                  const unsigned int* __restrict__ seg,
                                                   const double* __restrict__ eig, const int* __restrict__ okf,
                                                   int* __restrict__ csign) {
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
@@ -171,7 +170,7 @@ __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts
 // PCL's sign disambiguation of keypoint q's eigenvectors e (count rule from the summed sign
 // counts st / sn, median-5 rule over valid neighbours by rank) -> float LRF rows r9
 __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, float kx, float ky, float kz,
-                                            const unsigned long long* __restrict__ sg, int n, const double* e, int st,
+                                            const unsigned int* __restrict__ sg, int n, const double* e, int st,
                                             int sn, float* r9) {
     const int valid_total = (int)e[6];
     double x[3] = {e[0], e[1], e[2]}, z[3] = {e[3], e[4], e[5]};
@@ -184,8 +183,9 @@ __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, flo
         const int med = valid_total / 2;
         int addT = 0, addN = 0;
         int z0n = 0, excl = 0;
-        while (z0n < n && (unsigned)(sg[z0n] >> 32) == 0u) {
-            const float4 p = pts4[(unsigned)(sg[z0n] & 0xFFFFFFFFu)];
+        while (z0n < n) {
+            const float4 p = pts4[sg[z0n]];
+            if (__float_as_uint(d2_flann(kx, ky, kz, p.x, p.y, p.z)) != 0u) break;  // d2 > 0 (never -0)
             if (p.x == kx && p.y == ky && p.z == kz) ++excl;
             ++z0n;
         }
@@ -197,7 +197,7 @@ __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, flo
                 int rr = 0;
                 i = -1;
                 for (int u = 0; u < z0n; ++u) {
-                    const float4 p = pts4[(unsigned)(sg[u] & 0xFFFFFFFFu)];
+                    const float4 p = pts4[sg[u]];
                     if (p.x == kx && p.y == ky && p.z == kz) continue;
                     if (rr == r) { i = u; break; }
                     ++rr;
@@ -206,7 +206,7 @@ __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, flo
                 i = r + excl;
             }
             if (i < 0 || i >= n) continue;
-            const float4 p = pts4[(unsigned)(sg[i] & 0xFFFFFFFFu)];
+            const float4 p = pts4[sg[i]];
             const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
             if (((vx * x[0] + vy * x[1]) + vz * x[2]) > 0) addT++;
             if (((vx * z[0] + vy * z[1]) + vz * z[2]) > 0) addN++;
@@ -225,7 +225,7 @@ __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, flo
 
 __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
                                                 const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                const unsigned long long* __restrict__ seg,
+                                                const unsigned int* __restrict__ seg,
                                                 const double* __restrict__ eig, const int* __restrict__ okf,
                                                 const int* __restrict__ csign, float* __restrict__ rf_out,
                                                 int* __restrict__ ok_out) {
@@ -268,17 +268,16 @@ __device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0,
 #define PST2_RAD_135 2.3561944901923449288469825374596
 #define PST2_RAD_PI_7_8 2.7488935718910690836548129603691
 
-// the <= 5 (bin, value) interpolation records of one neighbour (key = its (d2 bits << 32 | idx)),
-// in PCL's add order (cos neighbour, radius, inclination, azimuth, main bin); unused slots: bin -1
+// the <= 5 (bin, value) interpolation records of neighbour idx, in PCL's add order (cos
+// neighbour, radius, inclination, azimuth, main bin); unused slots: bin -1
 __device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, const float4* __restrict__ normals,
                                              float kx, float ky, float kz, float R, const float* rf,
-                                             unsigned long long key, int* bins, float* vals) {
+                                             unsigned int idx, int* bins, float* vals) {
         const double Rd = (double)R;
         const double r12 = Rd / 2, r34 = (Rd * 3) / 4, r14 = Rd / 4;
         const int nr_bins = 10;
     #pragma unroll
         for (int j = 0; j < 5; ++j) { bins[j] = -1; vals[j] = 0.f; }
-        const unsigned int idx = (unsigned int)(key & 0xFFFFFFFFu);
         const float4 nv = normals[idx];
         if (__builtin_isfinite(nv.x) && __builtin_isfinite(nv.y) && __builtin_isfinite(nv.z)) {
             double cosd = (double)dot4f_2(nv.x, nv.y, nv.z, rf[6], rf[7], rf[8]);
@@ -287,7 +286,8 @@ __device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, co
             double bd = ((1.0 + cosd) * nr_bins) / 2;
             const float4 p = pts4[idx];
             const float dx = p.x - kx, dy = p.y - ky, dz = p.z - kz;
-            const double distance = sqrt((double)__uint_as_float((unsigned)(key >> 32)));
+            // the gather's d2 (same expression and operands as the ranked key's)
+            const double distance = sqrt((double)d2_flann(kx, ky, kz, p.x, p.y, p.z));
             if (!(fabs(distance - 0.0) < 1e-15)) {
                 double xr = (double)dot4f_2(dx, dy, dz, rf[0], rf[1], rf[2]);
                 double yr = (double)dot4f_2(dx, dy, dz, rf[3], rf[4], rf[5]);
@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
                                                               const int* __restrict__ perm,
                                                               const long long* __restrict__ offs,
                                                               const int* __restrict__ cb,
-                                                              const unsigned long long* __restrict__ seg,
+                                                              const unsigned int* __restrict__ seg,
                                                               const float* __restrict__ rf_in,
                                                               const int* __restrict__ ok_in, float* __restrict__ shot_out,
                                                               unsigned int* __restrict__ bits_out) {

@@ -36,16 +36,23 @@ __device__ __forceinline__ void cand_init(CandLds* cs) {
 }
 
 // streams the candidates of one 64-cell round (lane = cell: spts run [st, st + cnt), off = its
-// exclusive prefix among the round's runs, total = their sum)
+// exclusive prefix among the round's runs, total = their sum). nparts > 1: only the groups
+// g = part, part + nparts, ... (the waves of a workgroup share one query's candidates); each
+// group's first owner then comes from the runs directly instead of the previous group.
 template <int GROUP, class F>
 __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs, int& epoch, float qx, float qy,
                                                   float qz, float rs2, unsigned int st, unsigned int cnt, int off,
-                                                  int total, F& f) {
+                                                  int total, F& f, int part = 0, int nparts = 1) {
     const int lane = lane_id();
     const int cbase = (int)st - off;  // spts index of flattened candidate t is cbase(cell) + t
     const unsigned long long nonempty = __ballot(cnt > 0);
     int carry = (int)__ffsll((long long)nonempty) - 1;
-    for (int t0 = 0; t0 < total; t0 += 64 * GROUP) {
+    for (int t0 = part * 64 * GROUP; t0 < total; t0 += 64 * GROUP * nparts) {
+        if (nparts > 1) {
+            // the non-empty run holding position t0: the last one starting at or before it
+            const unsigned long long started = __ballot(cnt > 0 && off <= t0);
+            carry = 63 - __clzll((long long)started);
+        }
         ++epoch;
         const int tag = epoch << 6;
         if (cnt > 0 && off >= t0 && off < t0 + 64 * GROUP) cs->mark[off - t0] = tag | lane;
@@ -104,9 +111,11 @@ __device__ __forceinline__ void cand_lookup(const GridView& g, double c, int x0,
 
 // Returns false (and streams nothing) when the cube holds fewer than min_total candidates -- the
 // ball then holds fewer too. Cubes of <= 128 cells do all their lookups before streaming.
+// part / nparts: this wave streams only its share of the candidate groups (see cand_stream_round);
+// every wave of the share does the cell lookups itself.
 template <int GROUP = CAND_GROUP, class F>
 __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, float qx, float qy, float qz, float rs,
-                                               float rs2, F&& f, int min_total = 0) {
+                                               float rs2, F&& f, int min_total = 0, int part = 0, int nparts = 1) {
     const int lane = lane_id();
     const double c = (double)g.cell;
     const int x0 = (int)floor(((double)qx - rs) / c), x1 = (int)floor(((double)qx + rs) / c);
@@ -132,7 +141,7 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
                 const int tot = r ? tot1 : tot0;
                 if (tot > 0)
                     cand_stream_round<GROUP>(g, cs, epoch, qx, qy, qz, rs2, r ? st1 : st0, r ? cnt1 : cnt0,
-                                             r ? off1 : off0, tot, f);
+                                             r ? off1 : off0, tot, f, part, nparts);
             }
         }
     } else {
@@ -142,7 +151,7 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
             int total;
             const int off = wave_excl_scan((int)cnt, total);
             if (total == 0) continue;
-            cand_stream_round<GROUP>(g, cs, epoch, qx, qy, qz, rs2, st, cnt, off, total, f);
+            cand_stream_round<GROUP>(g, cs, epoch, qx, qy, qz, rs2, st, cnt, off, total, f, part, nparts);
         }
     }
     if (lane == 0) cs->epoch = epoch;

@@ -35,8 +35,10 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
 hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, float R, int* counts, unsigned int* bh,
                                   long long seg_cap, int chunk_cap, long long* offs, int* cb, int* perm, int* err,
                                   hipStream_t s);
+// out: the neighbour indices of every segment in (d2, idx) order (4 B each; the consumers recompute
+// d2 from the points with the gather's expression, bit-identical)
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
-                            const unsigned int* bstart, const unsigned long long* seg, unsigned long long* out,
+                            const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
                             hipStream_t s, int max_blocks = 0);
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s);
@@ -83,7 +85,7 @@ struct Describe2Args {
     const float4* normals = nullptr;
     const float* kps = nullptr;
     const unsigned long long* seg = nullptr;  // unsorted keys (gather)
-    unsigned long long* sorted = nullptr;     // sorted keys (output of k_shot_rank)
+    unsigned int* sorted = nullptr;           // neighbour indices in (d2, idx) order (output of k_shot_rank)
     double* csum = nullptr;                   // 8 per chunk
     double* eig = nullptr;                    // 8 per keypoint
     int* okf = nullptr;                       // eigen ok per keypoint

@@ -36,12 +36,12 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 L2_PEAK_GBPS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md "L2 (per XCD)")
 
 
-def pmc_kernel(stage):
+def pmc_kernel(stage, path=None):
     """Counters of the stage's kernel from the newest committed PMC summary (profiles/rNN_pmc.json,
     scripts/pmc_summary.py): HBM bytes per launch (rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE,
     separate passes) and, where collected, the SQ / TCC / TCP derived metrics."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    files = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
     if not files:
         return None, None
     try:
@@ -70,6 +70,8 @@ def parse():
                     help="skip the second timed leg whose sweeps start in pinned host memory (upload inside the region)")
     ap.add_argument("--metrics", default=None, help="per-sweep JSON lines of rank 0 (bshot_odom_set_metrics_file)")
     ap.add_argument("--cpu-frames", type=int, default=5)
+    ap.add_argument("--pmc-file", default=None,
+                    help="PMC summary (scripts/prof_summary.py) of this configuration; default: the newest profiles/r*_pmc.json")
     ap.add_argument("--profile-stages", action="store_true", help="print per-stage ms to stderr")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage HIP events in the timed region")
     ap.add_argument("--depth", type=int, default=2, help="lookahead depth (1: next sweep only, 2: two sweeps)")
@@ -327,7 +329,7 @@ def main():
     roof = None
     if dname in alg and per_launch_ms[dname] > 0:
         t_launch = per_launch_ms[dname] * 1e-3
-        pmc, psrc = pmc_kernel(dname)
+        pmc, psrc = pmc_kernel(dname, a.pmc_file)
         traffic = round(pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]) if pmc and "hbm_read_bytes" in pmc else None
         roof = {"kernel": dname, "ms_per_launch": round(per_launch_ms[dname], 4), "traffic": traffic,
                 "traffic_unit": "HBM bytes/launch (PMC)", "pmc_source": psrc}
