@@ -6,7 +6,11 @@ mkdir -p gpurun_out
 for i in $(seq 1 $N); do
   for v in base new; do
     if [ $v = base ]; then L=experiments/ab/libbshot_base.so; else L=b-shot-slam_amd/lib/libbshot_amd.so; fi
-    BSHOT_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --no-upload-leg "$@" > gpurun_out/ab_$v$i.json 2> gpurun_out/ab_$v$i.err || { tail -5 gpurun_out/ab_$v$i.err; exit 1; }
-    python3 -c "import json; d=json.load(open('gpurun_out/ab_$v$i.json')); print('$v', $i, d['value'], d['ms_per_step_median'], d['host_ms_per_sweep'])"
+    BENCH_INTERVALS=1 BSHOT_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --no-upload-leg "$@" > gpurun_out/ab_$v$i.json 2> gpurun_out/ab_$v$i.err || { tail -5 gpurun_out/ab_$v$i.err; exit 1; }
+    python3 -c "
+import json
+d = json.load(open('gpurun_out/ab_$v$i.json'))
+w = [json.loads(l) for l in open('gpurun_out/ab_$v$i.err') if l.startswith('{\"sweep_intervals_ms')][0]['work']
+print('$v', $i, d['value'], d['ms_per_step_median'], d['host_ms_per_sweep'], 'work', w)"
   done
 done
