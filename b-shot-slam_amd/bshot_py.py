@@ -64,7 +64,7 @@ ABI_SYMBOLS = [
     "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
     "bshot_odom_set_option", "bshot_odom_set_metrics_file", "bshot_odom_upload", "bshot_odom_drain", "bshot_xchg_unique_id", "bshot_xchg_create",
-    "bshot_xchg_destroy", "bshot_odom_exchange", "bshot_odom_gpu_replica_size", "bshot_odom_gpu_replica_query",
+    "bshot_xchg_destroy", "bshot_odom_exchange", "bshot_odom_exchange_sim", "bshot_odom_gpu_replica_size", "bshot_odom_gpu_replica_query",
     "bshot_odom_gpu_replica_insert", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
     "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
     "bshot_pcap_load", "bshot_velodyne_decode", "bshot_velodyne_decode_device",
@@ -486,6 +486,10 @@ class Odometry:
     def exchange(self, xchg, include_self=False):
         """Map offer of the last sweep -> every rank's GPU replicas over RCCL (bshot_odom_exchange)."""
         self._chk(self.L.bshot_odom_exchange(self.h, xchg.h, 1 if include_self else 0), "odom_exchange")
+
+    def exchange_sim(self, xchg, peers):
+        """bshot_odom_exchange_sim: the exchange plus `peers` simulated ranks' inserts (measurement)."""
+        self._chk(self.L.bshot_odom_exchange_sim(self.h, xchg.h, int(peers)), "odom_exchange_sim")
 
     def gpu_replica_insert(self, replica, rec):
         rec = np.ascontiguousarray(rec, np.float32).reshape(-1, 15)

@@ -183,6 +183,15 @@ struct bshot_ctx {
     int opt_gpu_map = 1;
     bsh::GMap* gmap = nullptr;
     std::vector<bsh::GMap*> gmap_replicas;  // other sequences' maps (multi-GPU exchange, bshot_odom_exchange)
+    // the exchange queues its replica inserts from a thread of its own (host/xchg.cpp): every host
+    // access to the replicas (and the context's teardown) first waits until that thread is idle
+    // (detach = 1 at the context's teardown: the exchange forgets it)
+    void (*replica_quiesce)(void* arg, int detach) = nullptr;
+    void* replica_quiesce_arg = nullptr;
+    void quiesce_replicas(int detach = 0) {
+        if (replica_quiesce) replica_quiesce(replica_quiesce_arg, detach);
+        if (detach) replica_quiesce = nullptr;
+    }
     int opt_xseq_targets = 0;  // 1: the replicas' entries join the matching targets (extension; 0 = reference)
     DBuf<float> gtgt;  // matching targets assembled on the device (float3)
 

@@ -809,6 +809,7 @@ void bshot_destroy(bshot_ctx* c) {
     if (!c) return;
     const bool trace = std::getenv("BSHOT_TRACE") != nullptr;
     if (trace) std::fprintf(stderr, "destroy enter\n");
+    c->quiesce_replicas(1);  // an exchange's insert thread is done with this context and forgets it
     (void)hipSetDevice(c->device);
     if (trace) std::fprintf(stderr, "destroy step 0\n");
     (void)hipStreamSynchronize(c->stream);

@@ -92,13 +92,16 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
 // this sweep's map offer (the last gmap_insert's slots) as an exchange record batch at d_rec
 // (GM_REC_HDR + GM_REC_W * kmax floats), on c->stream
 int gmap_pack_delta(bshot_ctx* c, int kmax, float* d_rec);
-// a record batch (device, count in the header) inserted into replica map `replica` on c->stream
-int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync);
+// a record batch (device, count in the header) inserted into replica map `replica` on stream st
+// (nullptr: the context's main stream)
+int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync, hipStream_t st = nullptr);
 // host records (bshot_odom_map_delta's 15-float layout) -> replica map (synchronous)
 int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n);
 int gmap_replica_size(bshot_ctx* c, int replica);
-// every replica's last unsynchronised insert has landed without error (else BSHOT_ECAP)
+// every replica's last unsynchronised insert has landed without error (else BSHOT_ECAP); the
+// _noquiesce form is the exchange's insert thread's own (it does not wait for itself)
 int gmap_settle_replicas(bshot_ctx* c);
+int gmap_settle_replicas_noquiesce(bshot_ctx* c);
 // replica's entries around pos (block loop order; libstdc++ or canonical order) -> host; count or -needed
 int gmap_replica_query(bshot_ctx* c, int replica, const float pos[3], float range, int canonical, float* xyz,
                        unsigned int* bits, int cap);

@@ -504,12 +504,13 @@ static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s)
     return hipSuccess;
 }
 
-static int gmap_init(bshot_ctx* c, GMap& g) {
+static int gmap_init(bshot_ctx* c, GMap& g, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     if (g.ready) return BSHOT_OK;
     g.tsize = 1u << 16;
     HIPCHK(g.tkey.ensure(g.tsize), "gmap table");
     HIPCHK(g.tval.ensure(g.tsize), "gmap table");
-    HIPCHK(kfill(g.tkey.p, 0xFF, sizeof(unsigned long long) * g.tsize, c->stream), "gmap table clear");
+    HIPCHK(kfill(g.tkey.p, 0xFF, sizeof(unsigned long long) * g.tsize, st), "gmap table clear");
     g.blk_cap = 1 << 14;
     HIPCHK(g.blk.ensure(g.blk_cap), "gmap blocks");
     g.ipool_cap = (size_t)1 << 24;
@@ -519,7 +520,7 @@ static int gmap_init(bshot_ctx* c, GMap& g) {
     g.ipool_cap = g.ipool.cap;
     g.cpool_cap = g.cpool.cap;
     HIPCHK(g.ctr.ensure(GM_NCTR), "gmap counters");
-    HIPCHK(kfill(g.ctr.p, 0, sizeof(int) * GM_NCTR, c->stream), "gmap counters");
+    HIPCHK(kfill(g.ctr.p, 0, sizeof(int) * GM_NCTR, st), "gmap counters");
     HIPCHK(g.p_ctr.ensure(GM_NCTR), "gmap pinned counters");
     std::memset(g.p_ctr.p, 0, sizeof(int) * GM_NCTR);
     g.slots = 0;
@@ -551,17 +552,18 @@ static int gmap_settle(bshot_ctx* c, GMap& g) {
 // room for one more batch of k keypoints (counters as of the map's last D2H, which gmap_settle or a
 // later sync on the stream has completed): slots, blocks, table load <= 1/2, pools at most half full
 // (a batch can at most double what its blocks hold)
-static int gmap_reserve(bshot_ctx* c, GMap& g, int k) {
+static int gmap_reserve(bshot_ctx* c, GMap& g, int k, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     if (int rc = gmap_settle(c, g)) return rc;
     const int* h = g.p_ctr.p;
-    HIPCHK(grow_keep(g.kpos, (size_t)g.slots, (size_t)g.slots + k + 1, c->stream), "gmap slots");
-    HIPCHK(grow_keep(g.kdesc, 11 * (size_t)g.slots, 11 * ((size_t)g.slots + k + 1), c->stream), "gmap slots");
+    HIPCHK(grow_keep(g.kpos, (size_t)g.slots, (size_t)g.slots + k + 1, st), "gmap slots");
+    HIPCHK(grow_keep(g.kdesc, 11 * (size_t)g.slots, 11 * ((size_t)g.slots + k + 1), st), "gmap slots");
     const size_t nb = (size_t)h[GM_NBLOCKS];
-    HIPCHK(grow_keep(g.blk, nb, nb + k + 1, c->stream), "gmap blocks");
+    HIPCHK(grow_keep(g.blk, nb, nb + k + 1, st), "gmap blocks");
     g.blk_cap = g.blk.cap;
     if (2 * (nb + k) > g.tsize) {
         // rehash the block table on the host side of a sync: rebuilt from the headers
-        HIPCHK(hipStreamSynchronize(c->stream), "sync map table");
+        HIPCHK(hipStreamSynchronize(st), "sync map table");
         unsigned int ts = g.tsize;
         while (2 * (nb + k) > ts) ts <<= 1;
         std::vector<GBlock> hb(nb);
@@ -585,8 +587,8 @@ static int gmap_reserve(bshot_ctx* c, GMap& g, int k) {
         g.tsize = ts;
     }
     const size_t itop = (size_t)(unsigned)h[GM_ITOP], ctop = (size_t)(unsigned)h[GM_CTOP];
-    HIPCHK(grow_keep(g.ipool, itop, 2 * itop + 64 * (size_t)k + 4096, c->stream), "gmap pool");
-    HIPCHK(grow_keep(g.cpool, ctop, 2 * ctop + 16 * (size_t)k + 1024, c->stream), "gmap pool");
+    HIPCHK(grow_keep(g.ipool, itop, 2 * itop + 64 * (size_t)k + 4096, st), "gmap pool");
+    HIPCHK(grow_keep(g.cpool, ctop, 2 * ctop + 16 * (size_t)k + 1024, st), "gmap pool");
     g.ipool_cap = g.ipool.cap;
     g.cpool_cap = g.cpool.cap;
     return BSHOT_OK;
@@ -594,27 +596,32 @@ static int gmap_reserve(bshot_ctx* c, GMap& g, int k) {
 
 // sort the batch's block ids (stable: sweep order inside a block), runs -> segments, insert waves;
 // the counters go to the pinned copy (synchronously when sync)
-static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync) {
+static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     const int B = 256;
     size_t tb = 0;
     HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
-                                     c->stream), "gmap sort size");
+                                     st), "gmap sort size");
     HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
     HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
-                                     c->stream), "gmap sort");
-    HIPCHK(kfill(g.ctr.p + GM_NSEG, 0, sizeof(int), c->stream), "gmap seg count");
-    bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, c->stream>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
-    bsk::k_gmap_insert<<<std::min(k, 1024), GM_INS_T, 0, c->stream>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
+                                     st), "gmap sort");
+    HIPCHK(kfill(g.ctr.p + GM_NSEG, 0, sizeof(int), st), "gmap seg count");
+    bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, st>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
+    // a workgroup holds a whole CU's LDS (the block image), and a batch touches a few hundred blocks
+    // at most: more workgroups than that only occupy CUs to exit. Replica inserts (another stream,
+    // off the critical chain) take fewer, leaving the CUs to the lookahead.
+    const int wgs = std::min(k, st == c->stream ? 256 : 64);
+    bsk::k_gmap_insert<<<wgs, GM_INS_T, 0, st>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
     HIPCHK(hipGetLastError(), "gmap insert launch");
     g.slots += k;
-    HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, c->stream), "D2H map counters");
+    HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, st), "D2H map counters");
     if (sync) {
-        HIPCHK(hipStreamSynchronize(c->stream), "sync map");
+        HIPCHK(hipStreamSynchronize(st), "sync map");
         g.ctr_pending = false;
         if (g.p_ctr.p[GM_ERR]) return c->fail("gpu map: capacity exceeded (block > 4096 members, or pool)", BSHOT_ECAP);
     } else {
         if (!g.ev_ctr) HIPCHK(hipEventCreateWithFlags(&g.ev_ctr, hipEventDisableTiming), "map event");
-        HIPCHK(hipEventRecord(g.ev_ctr, c->stream), "record map counters");
+        HIPCHK(hipEventRecord(g.ev_ctr, st), "record map counters");
         g.ctr_pending = true;
     }
     return BSHOT_OK;
@@ -664,17 +671,19 @@ int gmap_pack_delta(bshot_ctx* c, int kmax, float* d_rec) {
     return BSHOT_OK;
 }
 
-int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync) {
+int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync, hipStream_t st) {
+    if (!st) st = c->stream;
     GMap& g = replica_map(c, replica);
-    int rc = gmap_init(c, g);
+    int rc = gmap_init(c, g, st);
     if (rc) return rc;
     if (kmax <= 0) return BSHOT_OK;
-    if ((rc = gmap_reserve(c, g, kmax)) || (rc = gmap_scratch(c, g, kmax))) return rc;
-    bsk::k_gmap_prep_rec<<<(kmax + 255) / 256, 256, 0, c->stream>>>(d_rec, kmax, g.slots, dev_view(g), g.keys.p, g.vals.p);
-    return gmap_run_insert(c, g, kmax, sync);
+    if ((rc = gmap_reserve(c, g, kmax, st)) || (rc = gmap_scratch(c, g, kmax))) return rc;
+    bsk::k_gmap_prep_rec<<<(kmax + 255) / 256, 256, 0, st>>>(d_rec, kmax, g.slots, dev_view(g), g.keys.p, g.vals.p);
+    return gmap_run_insert(c, g, kmax, sync, st);
 }
 
 int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n) {
+    c->quiesce_replicas();
     // host records (bshot_odom_map_delta layout: x, y, z, ratio, 11 words) -> a device batch
     GMap& g = replica_map(c, replica);
     int rc = gmap_init(c, g);
@@ -689,17 +698,25 @@ int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n)
     return gmap_insert_records(c, replica, g.hrec.p, n, true);
 }
 
-int gmap_settle_replicas(bshot_ctx* c) {
+int gmap_settle_replicas_noquiesce(bshot_ctx* c) {
     for (GMap* g : c->gmap_replicas)
         if (g)
             if (int rc = gmap_settle(c, *g)) return rc;
     return BSHOT_OK;
 }
 
+int gmap_settle_replicas(bshot_ctx* c) {
+    c->quiesce_replicas();
+    return gmap_settle_replicas_noquiesce(c);
+}
+
 int gmap_replica_size(bshot_ctx* c, int replica) {
+    c->quiesce_replicas();
     if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
     GMap& g = *c->gmap_replicas[replica];
+    // its inserts may run on another stream (the exchange's): wait for the counters' copy itself
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    if (g.ctr_pending && hipEventSynchronize(g.ev_ctr) != hipSuccess) return -1;
     g.ctr_pending = false;
     if (g.p_ctr.p[GM_ERR]) return -2;
     return g.p_ctr.p[GM_MEMBERS];
@@ -804,10 +821,12 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
 
 int gmap_replica_query(bshot_ctx* c, int replica, const float pos[3], float range, int canonical, float* xyz,
                        unsigned int* bits, int cap) {
+    c->quiesce_replicas();
     if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
     GMap& g = *c->gmap_replicas[replica];
     const QueryBox q = query_box(pos, range);
     HIPCHK(hipStreamSynchronize(c->stream), "sync replica");
+    if (int rc = gmap_settle(c, g)) return rc;  // inserts on the exchange's stream have landed
     int rc = query_count(c, g, q);
     if (rc) return rc;
     if (!g.q_active) return 0;

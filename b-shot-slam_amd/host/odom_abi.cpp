@@ -17,7 +17,7 @@
 #include "../csrc/ctx.h"
 #include "../csrc/gmap.h"
 
-int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self);  // host/xchg.cpp
+int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self, int sim_peers);  // host/xchg.cpp
 
 struct bshot_odom {
     std::unique_ptr<myslam::LidarOdometry> lo;
@@ -222,7 +222,14 @@ int bshot_odom_set_next2_device(bshot_odom* o, const float* d_next2, int n_next2
 
 int bshot_odom_exchange(bshot_odom* o, bshot_xchg* x, int include_self) {
     if (!o || !x) return BSHOT_EINVAL;
-    const int rc = bshot_odom_exchange_ctx(o->lo->context(), x, include_self);
+    const int rc = bshot_odom_exchange_ctx(o->lo->context(), x, include_self, 0);
+    if (rc < 0) o->err = bshot_last_error(o->lo->context());
+    return rc;
+}
+
+int bshot_odom_exchange_sim(bshot_odom* o, bshot_xchg* x, int peers) {
+    if (!o || !x || peers < 0) return BSHOT_EINVAL;
+    const int rc = bshot_odom_exchange_ctx(o->lo->context(), x, 0, peers);
     if (rc < 0) o->err = bshot_last_error(o->lo->context());
     return rc;
 }

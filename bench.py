@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--map-bcast", action="store_true",
                     help="per-sweep map exchange between ranks (C++ over RCCL, into GPU replicas); on by default for N > 1")
     ap.add_argument("--no-map-bcast", action="store_true", help="N > 1 without the map exchange")
+    ap.add_argument("--sim-peers", type=int, default=0,
+                    help="N = 1: run the RCCL map exchange on a 1-rank communicator and insert this rank's batch "
+                         "into P more replicas per sweep (bshot_odom_exchange_sim): the insert work of a job of 1 + P ranks")
     ap.add_argument("--map-bcast-py", action="store_true",
                     help="with --map-bcast: the Python all_gather of host records into host replicas instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,6 +107,11 @@ def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a))
+    # the JSON line is the only output on stdout: whatever the libraries print there (RCCL's
+    # version banner at communicator init when NCCL_DEBUG is set, ...) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and a.gpus != world:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; the launcher's world size is used", file=sys.stderr)
@@ -173,6 +181,8 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(bshot_py.Exchange.unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         xchg = bshot_py.Exchange(bytes(uid.cpu().numpy().tobytes()), world, rank, local, a.keypoints)
+    elif a.sim_peers > 0 and world == 1:
+        xchg = bshot_py.Exchange(bshot_py.Exchange.unique_id(), 1, 0, local, a.keypoints)
 
     def step(i):
         # sweeps are preprocessed when first needed (this one or a lookahead)
@@ -186,7 +196,10 @@ def main():
         st = odo.process_device(frames[i].data_ptr(), npts[i])
         if xchg is not None:
             # C++ / RCCL: the sweep's map offer all-gathered from HBM into the GPU replicas, no host sync
-            odo.exchange(xchg)
+            if a.sim_peers > 0:
+                odo.exchange_sim(xchg, a.sim_peers)
+            else:
+                odo.exchange(xchg)
         elif a.map_bcast and world > 1:
             for r, rec in exchange_map_delta(odo.map_delta(), dist, dev):
                 odo.replica_insert(r, rec)
@@ -442,7 +455,9 @@ def main():
                                    f"full extract+describe+match+RANSAC+ICP+map per sweep",
                        "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
                        "icp_iters": icp_it, "mutual_corr": round(corr, 1), "parallelism": f"frame-shard x{world}" +
-                       (" + RCCL map exchange" if a.map_bcast else "")},
+                       (" + RCCL map exchange" if a.map_bcast else "") +
+                       (f" + RCCL map exchange (1 rank) with {a.sim_peers} simulated peers' replica inserts"
+                        if a.sim_peers > 0 else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "upload_inclusive": upload_leg,
@@ -452,7 +467,7 @@ def main():
             "host_ms_per_sweep": dict(zip(bshot_py.FrameStats.HOST_PHASES,
                                           np.round(np.mean([list(s.host_ms) for s in stats], axis=0), 3).tolist())),
         }
-        print(json.dumps(line))
+        print(json.dumps(line), file=json_out, flush=True)
     if xchg is not None:
         xchg.close()
     if dist is not None:

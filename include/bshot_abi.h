@@ -228,6 +228,10 @@ int bshot_xchg_unique_id(void* id128);
 int bshot_xchg_create(bshot_xchg** out, const void* id128, int nranks, int rank, int device, int kmax);
 void bshot_xchg_destroy(bshot_xchg* x);
 int bshot_odom_exchange(bshot_odom* o, bshot_xchg* x, int include_self);
+/* measurement of the exchange's insert cost on fewer GPUs than ranks: bshot_odom_exchange, then
+ * this rank's gathered batch is also inserted into `peers` further replicas (ids nranks ..
+ * nranks + peers - 1), the per-sweep insert work of a job with nranks + peers ranks */
+int bshot_odom_exchange_sim(bshot_odom* o, bshot_xchg* x, int peers);
 /* GPU replica of rank r's map: entry count (syncs), and its entries around pos within range (the
  * reference's block loop; libstdc++ order) -> xyz (n x 3), bits (n x 11); count or -needed */
 int bshot_odom_gpu_replica_size(bshot_odom* o, int replica);

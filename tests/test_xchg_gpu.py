@@ -55,6 +55,28 @@ def test_rccl_exchange_self_replica():
         x.close()
 
 
+def test_exchange_sim_peers_replicas():
+    # bshot_odom_exchange_sim (bench.py --sim-peers): every simulated peer's replica receives this
+    # rank's batch, so each must equal the own map (entries, block order, size) sweep after sweep
+    uid = bshot_py.Exchange.unique_id()
+    x = bshot_py.Exchange(uid, 1, 0, 0, K)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+    try:
+        for f, xyz in enumerate(_frames(n=4)):
+            st = od.process(xyz)
+            od.exchange_sim(x, 3)
+            pos = np.array(st.pose, np.float32).reshape(4, 4)[:3, 3]
+            ref = od.gpu_replica_query(1, pos)
+            for r in (1, 2, 3):
+                assert od.gpu_replica_size(r) == st.map_size, (f, r)
+                got = od.gpu_replica_query(r, pos)
+                assert np.array_equal(_u(got[0]), _u(ref[0])) and np.array_equal(got[1], ref[1]), (f, r)
+            assert od.gpu_replica_size(0) == 0  # this rank's own replica is not fed (include_self off)
+    finally:
+        od.close()
+        x.close()
+
+
 def test_xseq_targets_append_replicas():
     uid = bshot_py.Exchange.unique_id()
     x = bshot_py.Exchange(uid, 1, 0, 0, K)
@@ -87,27 +109,31 @@ def _rank(rank, world, port, q):
         solo_poses = [_u(solo.process(x).pose).copy() for x in frames]
         solo.close()
         od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
-        ok = True
+        bad = []
         for f, xyz in enumerate(frames):
             st = od.process(xyz)
-            ok &= np.array_equal(_u(st.pose), solo_poses[f])
+            if not np.array_equal(_u(st.pose), solo_poses[f]):
+                bad.append(f"pose {f}")
             deltas = [None] * world
             dist.all_gather_object(deltas, od.map_delta())
             for r in range(world):
                 od.gpu_replica_insert(r, deltas[r])
             sizes = [None] * world
             dist.all_gather_object(sizes, st.map_size)
-            ok &= all(od.gpu_replica_size(r) == sizes[r] for r in range(world))
+            got = [od.gpu_replica_size(r) for r in range(world)]
+            if got != sizes:
+                bad.append(f"sizes {f}: {got} vs {sizes}")
             digest = []
             for r in range(world):
                 xyz_r, bits_r = od.gpu_replica_query(r, np.array([0.0, 800.0 * f, 0.0], np.float32))
                 digest.append(hashlib.sha1(_u(xyz_r).tobytes() + bits_r.tobytes()).hexdigest())
             digests = [None] * world
             dist.all_gather_object(digests, digest)
-            ok &= all(d == digests[0] for d in digests)
+            if not all(d == digests[0] for d in digests):
+                bad.append(f"digests {f}")
         od.close()
         dist.destroy_process_group()
-        q.put((rank, bool(ok)))
+        q.put((rank, True if not bad else "; ".join(bad)))
     except Exception as e:  # reported to the parent
         q.put((rank, repr(e)))
 
