@@ -137,6 +137,8 @@ struct bshot_ctx {
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
     int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
     int opt_side_prio = 0;      // describe (side) stream priority: 0 low (as SR/ISS ahead), 1 middle, 2 the main stream's
+    int opt_host_map_log = 1;   // LidarOdometry keeps the GPU map's insert log for the host Map view (bshot_odom: 0)
+    int opt_normals_seg = 1;    // normals from the SHOT neighbour lists when normal_radius == shot_radius
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
 

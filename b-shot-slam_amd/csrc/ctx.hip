@@ -412,11 +412,23 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(c->ok.ensure(k), "alloc ok");
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
-    const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
-    HIPCHK(launch_normals(S.ladder, c->ladder_mode(S), S.pts4.p, c->kps.p, k, c->prm.normal_radius, c->prm.normal_max_nn,
-                          c->normals.p, c->errw.p, st),
-           "normals launch");
-    c->stage_end(sg4, st);
+    // A4: with normal_radius == shot_radius the normals' neighbours are the head of each keypoint's
+    // sorted SHOT segment (k_normals_seg after the rank below); otherwise a search of their own
+    const bool nseg = c->opt_normals_seg && c->prm.normal_radius == c->prm.shot_radius;
+    auto normals_from_segments = [&](const long long* offs, const unsigned int* sorted) -> int {
+        const int sgn = c->stage_begin(BSHOT_STAGE_NORMALS, st);
+        HIPCHK(launch_normals_seg(S.pts4.p, c->kps.p, k, offs, sorted, c->prm.normal_max_nn, c->normals.p, st),
+               "normals (segments) launch");
+        c->stage_end(sgn, st);
+        return BSHOT_OK;
+    };
+    if (!nseg) {
+        const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
+        HIPCHK(launch_normals(S.ladder, c->ladder_mode(S), S.pts4.p, c->kps.p, k, c->prm.normal_radius,
+                              c->prm.normal_max_nn, c->normals.p, c->errw.p, st),
+               "normals launch");
+        c->stage_end(sg4, st);
+    }
     const float R = c->prm.shot_radius;
     const int sg5 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
     HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
@@ -460,6 +472,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
+        if (nseg) {
+            const int rc = normals_from_segments(c->offs.p, c->segtmp.p);
+            if (rc) return rc;
+        }
         const int sg11 = c->stage_begin(BSHOT_STAGE_LRF, st);
         HIPCHK(launch_describe2(A, 1, st), "describe2 lrf");
         c->stage_end(sg11, st);
@@ -526,6 +542,10 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
+    if (nseg) {
+        const int rc = normals_from_segments(c->offs.p, c->segtmp.p);
+        if (rc) return rc;
+    }
     const int sg11 = c->stage_begin(BSHOT_STAGE_LRF, st);
     HIPCHK(launch_describe2(A, 1, st), "describe2 lrf");
     c->stage_end(sg11, st);
@@ -1100,6 +1120,8 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
+    else if (k == "normals_seg") c->opt_normals_seg = value ? 1 : 0;
+    else if (k == "host_map_log") c->opt_host_map_log = value ? 1 : 0;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);

@@ -259,6 +259,83 @@ __global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4,
     ok_out[q] = 1;
 }
 
+// A4 from the SHOT neighbour lists (include/bshot_bits.h:63-80): with normal_radius == shot_radius
+// the normals' FLANN radius search (the normal_max_nn smallest (d2, idx) with d2 < r^2, in that
+// order) is the first min(n, normal_max_nn) entries of the keypoint's sorted SHOT segment, so no
+// search of its own is needed. A wave per keypoint: the neighbours' coordinates in LDS, the 9
+// accumulators of pcl::computeMeanAndCovarianceMatrix as sequential float sums in rank order
+// (lanes 0..5: xx xy xz yy yz zz products, lanes 6..8: x y z -- k_normals' order), then eigen33 and
+// the flip towards the origin.
+#define NS_WAVES 4
+__global__ void __launch_bounds__(64 * NS_WAVES) k_normals_seg(const float4* __restrict__ pts4,
+                                                               const float* __restrict__ kps, int k,
+                                                               const long long* __restrict__ offs,
+                                                               const unsigned int* __restrict__ seg, int max_nn,
+                                                               float4* __restrict__ normals) {
+    __shared__ float fl[NS_WAVES][3 * 512];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    const int q = blockIdx.x * NS_WAVES + wave;
+    if (q >= k) return;  // no workgroup barrier below
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const float qn = __builtin_nanf("");
+    float nx = qn, ny = qn, nz = qn, curv = qn;
+    if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
+        const long long o = offs[q];
+        const long long cnt = offs[q + 1] - o;
+        const int need = (int)(cnt < max_nn ? cnt : max_nn);
+        if (need > 0) {
+            float* f = fl[wave];
+            float acc = 0.f;
+            if (need >= 3) {
+                for (int r = lane; r < need; r += 64) {
+                    const float4 p = pts4[seg[o + r]];
+                    f[r] = p.x; f[512 + r] = p.y; f[1024 + r] = p.z;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 9) {
+                    const bool prod = lane < 6;
+                    const int a = prod ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
+                    const int b = lane < 3 ? lane : (lane < 5 ? lane - 2 : 2);
+                    const float* pa = f + 512 * a;
+                    const float* pb = f + 512 * (prod ? b : a);
+                    int r = 0;
+                    for (; r + 4 <= need; r += 4) {
+                        float v[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) v[u] = prod ? pa[r + u] * pb[r + u] : pa[r + u];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) acc = acc + v[u];
+                    }
+                    for (; r < need; ++r) acc = acc + (prod ? pa[r] * pb[r] : pa[r]);
+                }
+            }
+            if (need >= 3) {
+                float ac[9];
+                const float fn = (float)need;
+#pragma unroll
+                for (int a = 0; a < 9; ++a) ac[a] = __shfl(acc, a, 64) / fn;
+                float cov[9];
+                cov[0] = ac[0] - ac[6] * ac[6];
+                cov[1] = ac[1] - ac[6] * ac[7];
+                cov[2] = ac[2] - ac[6] * ac[8];
+                cov[4] = ac[3] - ac[7] * ac[7];
+                cov[5] = ac[4] - ac[7] * ac[8];
+                cov[8] = ac[5] - ac[8] * ac[8];
+                cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+                float ev, vec[3];
+                bm::eigen33_min(cov, &ev, vec);
+                nx = vec[0]; ny = vec[1]; nz = vec[2];
+                const float eig_sum = (cov[0] + cov[4]) + cov[8];
+                curv = (eig_sum != 0.f) ? fabsf(ev / eig_sum) : 0.f;
+            }
+            const float vx = 0.f - kx, vy = 0.f - ky, vz = 0.f - kz;
+            const float cth = (vx * nx + vy * ny) + vz * nz;
+            if (cth < 0.f) { nx *= -1.f; ny *= -1.f; nz *= -1.f; }
+        }
+    }
+    if (lane == 0) normals[q] = make_float4(nx, ny, nz, curv);
+}
+
 __device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0, float b1, float b2) {
     return (a0 * b0 + a2 * b2) + (a1 * b1 + 0.0f);
 }
@@ -525,6 +602,14 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
 }  // namespace bsk
 
 namespace bsh {
+
+hipError_t launch_normals_seg(const float4* pts4, const float* kps, int k, const long long* offs, const unsigned int* seg,
+                              int max_nn, float4* normals, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    if (max_nn < 1 || max_nn > 512) return hipErrorInvalidValue;
+    bsk::k_normals_seg<<<(k + NS_WAVES - 1) / NS_WAVES, 64 * NS_WAVES, 0, s>>>(pts4, kps, k, offs, seg, max_nn, normals);
+    return hipGetLastError();
+}
 
 // part 0: in-bucket rank (sorted segments); 1: LRF; 2: histogram records + ordered apply
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {

@@ -40,6 +40,10 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
                             hipStream_t s, int max_blocks = 0);
+// A4 from the sorted SHOT segments (normal_radius == shot_radius): the first min(n, max_nn) neighbour
+// indices of each keypoint's segment (seg: launch_shot_rank's output, offs its segment offsets)
+hipError_t launch_normals_seg(const float4* pts4, const float* kps, int k, const long long* offs, const unsigned int* seg,
+                              int max_nn, float4* normals, hipStream_t s);
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);

@@ -442,6 +442,9 @@ void LidarOdometry::computeDescriptors() {
 bool LidarOdometry::gpuMap() const { return ctx_->opt_gpu_map != 0; }
 
 void LidarOdometry::syncHostMap() {
+    if (map_log_skipped_)
+        throw std::runtime_error("host Map view unavailable: sweeps were inserted with context option host_map_log=0 "
+                                 "(set it to 1 before the first sweep)");
     // replay updateMap's offers into the host Map (same keypoints, ratios, descriptors, poses, order)
     for (; map_log_done_ < map_log_.size(); ++map_log_done_) {
         MapLogEntry& e = map_log_[map_log_done_];
@@ -625,9 +628,13 @@ void LidarOdometry::updateMap() {
     if (gpuMap()) {
         // csrc/gmap.hip: the same inserts in HBM; the descriptors are the rows featureMatching staged
         const int k = (int)cloud1_bshot_.size();
-        map_log_.push_back(MapLogEntry{kps, src_->getDescriptors(), std::vector<float>(seg_ratios_.begin(),
-                                                                                       seg_ratios_.begin() + k),
-                                       T_best_});
+        // the host view's replay log grows by ~60 B per keypoint per sweep; a caller that never
+        // reads the host Map (bshot_odom) turns it off
+        if (ctx_->opt_host_map_log)
+            map_log_.push_back(MapLogEntry{kps, src_->getDescriptors(),
+                                           std::vector<float>(seg_ratios_.begin(), seg_ratios_.begin() + k), T_best_});
+        else
+            ++map_log_skipped_;
         int msz = 0;
         check(bsh::gmap_insert(ctx_, k ? &(*kps)[0][0] : nullptr, seg_ratios_.data(), ctx_->ma.p, k, T_best_.m, &msz),
               "map update");

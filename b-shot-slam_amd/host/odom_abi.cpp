@@ -166,6 +166,9 @@ int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p) {
         delete o;
         return BSHOT_EHIP;
     }
+    // the headless loop never reads the host Map: no replay log (host memory stays flat over a run;
+    // bshot_odom_set_option(o, "host_map_log", 1) before the first sweep restores it)
+    o->lo->context()->opt_host_map_log = 0;
     if (const char* path = std::getenv("BSHOT_METRICS")) o->metrics = std::fopen(path, "a");
     *out = o;
     return BSHOT_OK;

@@ -13,6 +13,9 @@ __device__ __forceinline__ unsigned long long stamp() {
 // mode 0: ds_add_f32 (atomicAdd, no return) by lanes 0..4, bins from a table
 // mode 1: plain ds_read + add + ds_write by lanes 0..4 (dependent RMW chain)
 // mode 2: ds_add_f32 by all 64 lanes to distinct bins
+// mode 3: ds_add_f32 by lanes 0..2 only
+// mode 4: lanes 0..4, each add exec-masked off when its bin is = 0 mod 8 or odd (about 56% kept)
+// mode 5: as 4, the exec mask set around each ds_add_f32 in inline asm (no branch)
 template <int MODE>
 __global__ void k(const int* __restrict__ bins, int nops, unsigned long long* out, float* sink) {
     __shared__ float hist[384];
@@ -22,7 +25,7 @@ __global__ void k(const int* __restrict__ bins, int nops, unsigned long long* ou
     for (int i = threadIdx.x; i < 1024 * 5; i += blockDim.x) bt[i] = bins[i];
     __syncthreads();
     const unsigned long long t0 = stamp();
-    if (MODE == 2 || lane < 5) {
+    if (MODE == 2 || lane < (MODE == 3 ? 3 : 5)) {
         for (int r0 = 0; r0 < nops; r0 += 16) {
             int bb[16];
 #pragma unroll
@@ -30,6 +33,25 @@ __global__ void k(const int* __restrict__ bins, int nops, unsigned long long* ou
             if (MODE == 1) {
 #pragma unroll
                 for (int u = 0; u < 16; ++u) hist[bb[u]] = hist[bb[u]] + 0.5f;
+            } else if (MODE == 5) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const unsigned int keep = ((bb[u] & 1) == 0 && (bb[u] & 7) != 0) ? 1u : 0u;
+                    const unsigned int addr = (unsigned int)(size_t)&hist[bb[u]];
+                    asm volatile(
+                        "s_mov_b64 s[40:41], exec\n\t"
+                        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+                        "s_and_b64 exec, exec, vcc\n\t"
+                        "ds_add_f32 %1, %2\n\t"
+                        "s_mov_b64 exec, s[40:41]"
+                        :
+                        : "v"(keep), "v"(addr), "v"(0.5f)
+                        : "s40", "s41", "vcc", "memory");
+                }
+            } else if (MODE == 4) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if ((bb[u] & 1) == 0 && (bb[u] & 7) != 0) atomicAdd(&hist[bb[u]], 0.5f);
             } else {
 #pragma unroll
                 for (int u = 0; u < 16; ++u) atomicAdd(&hist[bb[u]], 0.5f);
@@ -67,6 +89,13 @@ int main() {
     run(k<0>, "ds_add lanes0-4, 1 wave/block", 1, 64);
     run(k<1>, "rmw lanes0-4, 1 wave/block", 1, 64);
     run(k<2>, "ds_add 64 lanes, 1 wave/block", 1, 64);
+    run(k<3>, "ds_add lanes0-2, 1 wave/block", 1, 64);
+    run(k<4>, "ds_add lanes0-4 masked ~40%, 1 wave", 1, 64);
+    run(k<5>, "ds_add lanes0-4 asm-masked, 1 wave", 1, 64);
+    run(k<0>, "ds_add lanes0-4, 8 waves, 256 blk", 256, 512);
+    run(k<5>, "ds_add lanes0-4 asm-masked, 8 waves, 256 blk", 256, 512);
+    run(k<3>, "ds_add lanes0-2, 8 waves, 256 blk", 256, 512);
+    run(k<4>, "ds_add lanes0-4 masked, 8 waves, 256 blk", 256, 512);
     run(k<0>, "ds_add lanes0-4, 1 wave, 2048 blk", 2048, 64);
     run(k<0>, "ds_add lanes0-4, 8 waves, 2048 blk", 2048, 512);
     run(k<0>, "ds_add lanes0-4, 1 wave, 16384 blk", 16384, 64);

@@ -128,8 +128,9 @@ class LidarOdometry {
         std::vector<float> ratios;
         Matrix4f T;
     };
-    std::vector<MapLogEntry> map_log_;
+    std::vector<MapLogEntry> map_log_;  // kept only with context option host_map_log (default 1)
     size_t map_log_done_ = 0;
+    size_t map_log_skipped_ = 0;  // sweeps inserted while host_map_log was 0: the host view is incomplete
     bool targets_on_device_ = false;  // cloud2_bshot_ not filled: the rows are in the context
     int last_na_ = 0;
     void syncHostMap();

@@ -272,11 +272,20 @@ uint64_t bshot_map_block_id(const float* pos);
  * reference's 21^3 block lookups, 1 always runs the reference's lookup loop */
 int bshot_map_set_query_mode(bshot_map* m, int mode);
 
-/* ---- tuning knobs (results never depend on them): "ladder_grids" 4 (default) or 2 grids for the
- *      exact-kNN radius ladder (4: seven radii r 2^(-k/2)); "describe2" 1 (default) load-balanced
- *      SHOT / 0 one workgroup per keypoint; "side_cu_reserve" N (default 0): CUs the side stream
- *      (ISS, lookahead) leaves to the main one (0: plain low-priority stream);
- *      "iss_cell" 2 (default) / 1: ISS grid cell in salient radii. Grid options take effect at the next set_cloud. */
+/* ---- options. Tuning knobs (results never depend on them): "ladder_grids" 4 (default) / 2 grids for
+ *      the exact-kNN radius ladder; "ladder_front" 1 (default): two more small radii in front;
+ *      "sr_start" percent scale of the ladder-start prediction (0: step 0); "sr_blocks" SR grid cap;
+ *      "iss_cell" 2 (default) / 1: ISS grid cell in salient radii (grid options take effect at the
+ *      next set_cloud); "iss_ovf_blocks", "iss_nms_blocks", "chunk_blocks" grid caps; "normals_seg"
+ *      1 (default): keypoint normals from the first normal_max_nn entries of the SHOT neighbour
+ *      lists when normal_radius == shot_radius (the same (d2, idx)-sorted radius search);
+ *      "ransac_dev" 1 (default): RANSAC hypotheses scored on the GPU; "topk_thread" 1 (default);
+ *      "pre_fast" 1 (default): the preprocessor's one-sort path when it applies; "side_prio";
+ *      "timing_mask" stage-event mask. Behaviour: "gpu_map" 1 (default, libstdc++ order) / 2
+ *      (canonical order) / 0 (host Map); "xseq_targets" 0 (default): other sequences' replicas join
+ *      the matching targets; "host_map_log" 1 (default; 0 under bshot_odom): keep the GPU map's
+ *      insert log so the host Map view (LidarOdometry::getKeypoints, getBlockKeypoints) can be
+ *      rebuilt -- without it host memory stays flat over a run and that view is unavailable. */
 int bshot_set_option(bshot_ctx* c, const char* name, int value);
 
 /* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's

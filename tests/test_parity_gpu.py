@@ -87,15 +87,21 @@ def test_iss_exact(ctx, cloud):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("k", [600, 2048])  # k ascending: the module context's persistent normals array must not hold stale slots from a larger K
-def test_describe_parity(ctx, cloud, sr_ref, k):
+@pytest.mark.parametrize("k,nseg", [(600, 1), (2048, 1), (2048, 0)])  # k ascending: the module context's persistent normals array must not hold stale slots from a larger K
+def test_describe_parity(ctx, cloud, sr_ref, k, nseg):
     """Load-balanced SHOT: bucketed gather + in-bucket rank, chunked LRF, records + ordered apply
-    (7 waves compute the records and one applies them, in one workgroup per keypoint: k_hist_fused)."""
+    (7 waves compute the records and one applies them, in one workgroup per keypoint: k_hist_fused).
+    Normals from the sorted SHOT segments (nseg 1, the default with normal_radius == shot_radius) or
+    from their own radius search (k_normals)."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, k)
     kps = cloud[kidx]
     ctx.set_cloud(cloud)
-    bits, shot, rf = ctx.describe(kps)
+    ctx.set_option("normals_seg", nseg)
+    try:
+        bits, shot, rf = ctx.describe(kps)
+    finally:
+        ctx.set_option("normals_seg", 1)
     nrm = ctx.normals(len(cloud))
     rn = orc.normals(cloud, kps)
     # normals: bit-exact by convention (contract tolerance 1e-5)
@@ -111,6 +117,30 @@ def test_describe_parity(ctx, cloud, sr_ref, k):
     np.testing.assert_array_equal(rf.view(np.uint32)[~np.isnan(rf)], rrf.view(np.uint32)[~np.isnan(rrf)])
     np.testing.assert_array_equal(shot.view(np.uint32)[~np.isnan(shot)], rs.view(np.uint32)[~np.isnan(rs)])
     np.testing.assert_array_equal(bits, rb)
+
+
+def test_normals_from_segments_edge_keypoints(ctx, cloud):
+    """k_normals_seg on keypoints that are not cloud points: off-surface, isolated (< 3 or no
+    neighbours within the radius), duplicated and non-finite. Equal to k_normals and the oracle."""
+    rng = np.random.default_rng(21)
+    kps = np.concatenate([cloud[rng.choice(len(cloud), 200, replace=False)] + rng.normal(0, 400, (200, 3)),
+                          np.array([[9.0e5, 9.0e5, 0.0], [0.0, 0.0, 0.0], [np.nan, 1.0, 2.0], [1.0, np.inf, 2.0]]),
+                          cloud[:3], cloud[:3]]).astype(np.float32)
+    ctx.set_cloud(cloud)
+    out = {}
+    for nseg in (1, 0):
+        ctx.set_option("normals_seg", nseg)
+        bits, shot, rf = ctx.describe(kps)
+        out[nseg] = (ctx.normals(len(kps)), bits, shot)
+    ctx.set_option("normals_seg", 1)
+    rn = orc.normals(cloud, kps)
+    for nseg in (1, 0):
+        nrm = out[nseg][0]
+        np.testing.assert_array_equal(np.isnan(nrm), np.isnan(rn[:len(kps)]))
+        ok = ~np.isnan(rn[:len(kps)])
+        np.testing.assert_array_equal(nrm.view(np.uint32)[ok], rn[:len(kps)].view(np.uint32)[ok])
+    np.testing.assert_array_equal(out[1][1], out[0][1])
+    np.testing.assert_array_equal(out[1][2].view(np.uint32), out[0][2].view(np.uint32))
 
 
 @pytest.mark.parametrize("hint", [1 << 26, 1])
