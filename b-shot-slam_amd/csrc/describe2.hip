@@ -534,6 +534,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     __shared__ unsigned int gcode[88];
     __shared__ __attribute__((aligned(16))) unsigned short sS[2][HF_B][320];  // [buffer][chunk][slot x 64 ranks]
     __shared__ __attribute__((aligned(16))) float sV[2][HF_B][320];
+    __shared__ int s0use[2][HF_B];  // [buffer][chunk]: the chunk has a slot-0 record of nonzero value
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     if ((int)blockIdx.x >= k) return;
     const int q = perm[blockIdx.x];
@@ -556,6 +557,10 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
             sS[buf][bi][64 * j + lane] = bins[j] < 0 ? (unsigned short)360 : (unsigned short)bins[j];
             sV[buf][bi][64 * j + lane] = bins[j] < 0 ? 0.f : vals[j];
         }
+        // slot 0 (the cosine interpolation) adds +-0 for every neighbour whose normal slot is zero,
+        // i.e. all but the few with index < K in the reference's mis-indexed normals array
+        const bool u0 = __ballot(bins[0] >= 0 && vals[0] != 0.f) != 0ull;
+        if (lane == 0) s0use[buf][bi] = u0 ? 1 : 0;
     };
     if (wave >= 1 && wave - 1 < nch) produce(wave - 1, 0, wave - 1);
     __syncthreads();
@@ -563,7 +568,12 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     for (int b = 0; b < nb; ++b) {
         const int buf = b & 1;
         if (wave == 0) {
-            if (lane < 5) {
+            // a batch whose slot-0 records all add +-0 is applied by lanes 1..4 only: adding +-0
+            // leaves a bin's bits unchanged (bins start at +0 and every record value is >= +0 or
+            // -0, so no bin is ever -0), and the LDS atomic unit's time is per active lane
+            int use0 = 0;
+            for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use0 |= s0use[buf][bi];
+            if (lane < 5 && (lane > 0 || use0)) {
                 for (int half = 0; half < 2 * HF_B && b * HF_B + (half >> 1) < nch; ++half) {
                     // 32 ranks of chunk half / 2 at a time (keeps the applying path's registers low)
                     const int bi = half >> 1, r0 = 32 * (half & 1);

@@ -116,20 +116,62 @@ __device__ __forceinline__ int wave_excl_scan(int v, int& total) {
 
 __device__ __forceinline__ int wave_sum_i(int v) { return readlane_i(wave_incl_add_i(v), 63); }
 
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(v, off, 64);
-        v = o < v ? o : v;
+// the value of lane (lane ^ OFF), without the LDS crossbar (ds_bpermute): gfx950's
+// v_permlane32/16_swap for the cross-row offsets, DPP row rotate / shifts / quad permutes inside a row
+template <int OFF>
+__device__ __forceinline__ unsigned int xor_lane_u32(unsigned int v) {
+    const int lane = lane_id();
+    if constexpr (OFF == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // {lanes 32..63 <- 0..31, 0..31 <- 32..63}
+        return (lane & 32) ? r[0] : r[1];
+    } else if constexpr (OFF == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // odd rows <- even rows and back
+        return (lane & 16) ? r[0] : r[1];
+    } else if constexpr (OFF == 8) {
+        return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (OFF == 4) {
+        const unsigned int up = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, false);  // row_shl:4
+        const unsigned int dn = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+        return (lane & 4) ? dn : up;
+    } else if constexpr (OFF == 2) {
+        return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else {
+        static_assert(OFF == 1, "xor offsets 32, 16, 8, 4, 2, 1");
+        return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     }
+}
+
+template <int OFF>
+__device__ __forceinline__ unsigned long long xor_lane_u64(unsigned long long v) {
+    const unsigned int lo = xor_lane_u32<OFF>((unsigned int)v), hi = xor_lane_u32<OFF>((unsigned int)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+template <int OFF>
+__device__ __forceinline__ double xor_lane_d(double v) {
+    return __longlong_as_double((long long)xor_lane_u64<OFF>((unsigned long long)__double_as_longlong(v)));
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+    unsigned long long o;
+    o = xor_lane_u64<32>(v); v = o < v ? o : v;
+    o = xor_lane_u64<16>(v); v = o < v ? o : v;
+    o = xor_lane_u64<8>(v); v = o < v ? o : v;
+    o = xor_lane_u64<4>(v); v = o < v ? o : v;
+    o = xor_lane_u64<2>(v); v = o < v ? o : v;
+    o = xor_lane_u64<1>(v); v = o < v ? o : v;
     return v;
 }
 
 // pairwise butterfly sum with a FIXED tree (lane 0's association: partner = lane ^ off,
 // off = 32, 16, ..., 1). Documented convention for the LRF covariance.
 __device__ __forceinline__ double wave_tree_sum_d(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    v = v + xor_lane_d<32>(v);
+    v = v + xor_lane_d<16>(v);
+    v = v + xor_lane_d<8>(v);
+    v = v + xor_lane_d<4>(v);
+    v = v + xor_lane_d<2>(v);
+    v = v + xor_lane_d<1>(v);
     return v;
 }
 
