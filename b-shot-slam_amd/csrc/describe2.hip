@@ -5,10 +5,10 @@
 //
 //   (sorting: k_shot_rank, csrc/describe.hip -- exact rank inside the count pass's d2 buckets)
 //   k_lrf_chunks  wave per 64-rank chunk: 7 weighted-covariance terms by the xor-butterfly tree
-//   k_lrf_eig     thread per keypoint: chunk sums in chunk order, Jacobi eigenvectors
+//   k_lrf_eig     wave per keypoint: chunk sums in chunk order (a lane per term), Jacobi eigenvectors
 //   k_lrf_sign    wave per chunk: sign counts for the x/z disambiguation (integer, order-free)
-//   k_lrf_fin     thread per keypoint: PCL's count + median-5 rule, float LRF rows
-//   k_hist_fused  workgroup per keypoint (default): 7 waves compute the <= 5 (bin, value)
+//   k_hist_fused  workgroup per keypoint: PCL's count + median-5 sign rule (float LRF rows) first,
+//                 then 7 waves compute the <= 5 (bin, value)
 //                 interpolation records of every neighbour into a double-buffered LDS batch while
 //                 one wave applies them in rank order to the LDS histogram (in-order ds_add_f32),
 //                 then L2 normalisation and B-SHOT bits
@@ -76,29 +76,10 @@ __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ p
     }
 }
 
-// chunk sums of keypoint q in chunk order, then the Jacobi eigenvectors: e[0..2] = x axis (largest),
-// [3..5] = z axis (smallest), [6] = valid count; returns the ok flag
-__device__ __forceinline__ int lrf_eig_one(const double* __restrict__ csum, int c0, int c1, double* e) {
-    double tot[7] = {0, 0, 0, 0, 0, 0, 0};
-    long long valid = 0;
-    for (int cc = c0; cc < c1; cc += 4) {
-        double4 blk[4][2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (cc + u < c1) {
-                const double4* s4 = reinterpret_cast<const double4*>(csum + 8 * (size_t)(cc + u));
-                blk[u][0] = s4[0];
-                blk[u][1] = s4[1];
-            }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (cc + u < c1) {
-                tot[0] = tot[0] + blk[u][0].x; tot[1] = tot[1] + blk[u][0].y; tot[2] = tot[2] + blk[u][0].z;
-                tot[3] = tot[3] + blk[u][0].w; tot[4] = tot[4] + blk[u][1].x; tot[5] = tot[5] + blk[u][1].y;
-                tot[6] = tot[6] + blk[u][1].z;
-                valid += (long long)blk[u][1].w;
-            }
-    }
+// Jacobi eigenvectors of keypoint q's weighted covariance (tot: the 7 chunk-ordered sums, valid: the
+// valid-neighbour count): e[0..2] = x axis (largest), [3..5] = z axis (smallest), [6] = valid count;
+// returns the ok flag
+__device__ __forceinline__ int lrf_eig_of_sums(const double* tot, long long valid, double* e) {
     int ok = 0;
     if (valid >= 5) {
         const double sum = tot[6];
@@ -118,18 +99,51 @@ __device__ __forceinline__ int lrf_eig_one(const double* __restrict__ csum, int 
     return ok;
 }
 
-// eig[8 q + 0..6] as lrf_eig_one; okf[q]
-__global__ void __launch_bounds__(64) k_lrf_eig(int k, const int* __restrict__ cb, const double* __restrict__ csum,
-                                                double* __restrict__ eig, int* __restrict__ okf) {
-    const int q = blockIdx.x * 64 + threadIdx.x;
-    if (q >= k) return;
-    double e[7] = {0, 0, 0, 0, 0, 0, 0};
-    const int ok = lrf_eig_one(csum, cb[q], cb[q + 1], e);
-    double* eo = eig + 8 * (size_t)q;
-    if (ok)
-        for (int j = 0; j < 6; ++j) eo[j] = e[j];
-    eo[6] = e[6];
-    okf[q] = ok;
+// eig[8 q + 0..6] (lrf_eig_of_sums), okf[q]. A wave per keypoint: lane j < 7 sums column j of the
+// keypoint's chunk partials in chunk order (sequential double adds; the 8 lanes of a chunk read its
+// 64 B together), lane 7 the valid counts (integers); lane 0 then runs the Jacobi solver.
+#define LE_WAVES 4
+__global__ void __launch_bounds__(64 * LE_WAVES) k_lrf_eig(int k, const int* __restrict__ cb,
+                                                           const double* __restrict__ csum, double* __restrict__ eig,
+                                                           int* __restrict__ okf) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    const int q = blockIdx.x * LE_WAVES + wave;
+    if (q >= k) return;  // no workgroup barrier below
+    const int c0 = cb[q], c1 = cb[q + 1];
+    double acc = 0.0;
+    long long valid = 0;
+    if (lane < 8) {
+        const double* col = csum + lane;
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = col[8 * (size_t)(c + u)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (lane < 7) acc = acc + v[u];
+                else valid += (long long)v[u];
+            }
+        }
+        for (; c < c1; ++c) {
+            const double v = col[8 * (size_t)c];
+            if (lane < 7) acc = acc + v;
+            else valid += (long long)v;
+        }
+    }
+    double tot[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) tot[j] = __shfl(acc, j, 64);
+    valid = __shfl(valid, 7, 64);
+    if (lane == 0) {
+        double e[7] = {0, 0, 0, 0, 0, 0, 0};
+        const int ok = lrf_eig_of_sums(tot, valid, e);
+        double* eo = eig + 8 * (size_t)q;
+        if (ok)
+            for (int j = 0; j < 6; ++j) eo[j] = e[j];
+        eo[6] = e[6];
+        okf[q] = ok;
+    }
 }
 
 // #(v . x >= 0), #(v . z >= 0) over the valid neighbours of chunk t of a keypoint (wave-uniform result)
@@ -149,7 +163,7 @@ __device__ __forceinline__ int2 lrf_sign_counts(const float4* __restrict__ pts4,
     return make_int2(__popcll(__ballot(pt != 0)), __popcll(__ballot(pn != 0)));
 }
 
-// csign[2 c], [2 c + 1]: chunk c's sign counts (summed by k_lrf_fin: no same-address atomics)
+// csign[2 c], [2 c + 1]: chunk c's sign counts (summed by k_hist_fused's first wave: no same-address atomics)
 __global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
                                                   const long long* __restrict__ offs, const int* __restrict__ cb,
                                                   const int* __restrict__ owner,
@@ -221,42 +235,6 @@ __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, flo
     r9[0] = x0; r9[1] = x1; r9[2] = x2;
     r9[3] = z1 * x2 - z2 * x1; r9[4] = z2 * x0 - z0 * x2; r9[5] = z0 * x1 - z1 * x0;
     r9[6] = z0; r9[7] = z1; r9[8] = z2;
-}
-
-__global__ void __launch_bounds__(64) k_lrf_fin(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
-                                                const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                const unsigned int* __restrict__ seg,
-                                                const double* __restrict__ eig, const int* __restrict__ okf,
-                                                const int* __restrict__ csign, float* __restrict__ rf_out,
-                                                int* __restrict__ ok_out) {
-    const int q = blockIdx.x * 64 + threadIdx.x;
-    if (q >= k) return;
-    float* r9 = rf_out + 9 * (size_t)q;
-    if (!okf[q]) {
-        for (int j = 0; j < 9; ++j) r9[j] = __builtin_nanf("");
-        ok_out[q] = 0;
-        return;
-    }
-    // sign counts: sum of the keypoint's per-chunk counts (integers, any order)
-    int st = 0, sn = 0;
-    {
-        const int2* cs2 = reinterpret_cast<const int2*>(csign);
-        const int c0 = cb[q], c1 = cb[q + 1];
-        int cc = c0;
-        for (; cc + 8 <= c1; cc += 8) {
-            int2 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = cs2[cc + u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) { st += v[u].x; sn += v[u].y; }
-        }
-        for (; cc < c1; ++cc) { st += cs2[cc].x; sn += cs2[cc].y; }
-    }
-    const long long o = offs[q];
-    double e[7];
-    for (int j = 0; j < 7; ++j) e[j] = eig[8 * (size_t)q + j];
-    lrf_fin_one(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o, (int)(offs[q + 1] - o), e, st, sn, r9);
-    ok_out[q] = 1;
 }
 
 // A4 from the SHOT neighbour lists (include/bshot_bits.h:63-80): with normal_radius == shot_radius
@@ -504,14 +482,6 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ bool apply_good(const float* __restrict__ kps, const long long* __restrict__ offs,
-                                           const int* __restrict__ ok_in, int q) {
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const int n = (int)(offs[q + 1] - offs[q]);
-    const bool fin = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz);
-    return fin && ok_in[q] && n >= 5;
-}
-
 // Records and ordered apply fused: a workgroup per keypoint (LPT order); waves 1..HF_B compute the
 // interpolation records of HF_B chunks into an LDS batch (shot_records) while wave 0 applies the
 // previous batch in rank order (one in-order ds_add_f32 per rank on lanes 0..4: every bin sees its
@@ -526,27 +496,65 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
                                                               const long long* __restrict__ offs,
                                                               const int* __restrict__ cb,
                                                               const unsigned int* __restrict__ seg,
-                                                              const float* __restrict__ rf_in,
-                                                              const int* __restrict__ ok_in, float* __restrict__ shot_out,
+                                                              const double* __restrict__ eig,
+                                                              const int* __restrict__ okf,
+                                                              const int* __restrict__ csign,
+                                                              float* __restrict__ rf_out, int* __restrict__ ok_out,
+                                                              float* __restrict__ shot_out,
                                                               unsigned int* __restrict__ bits_out) {
     constexpr int HF_B = HF_WAVES - 1;  // chunks per batch (one per producing wave)
     __shared__ float hist[384];
+    __shared__ float rfs[9];
+    __shared__ int okq;
     __shared__ unsigned int gcode[88];
     __shared__ __attribute__((aligned(16))) unsigned short sS[2][HF_B][320];  // [buffer][chunk][slot x 64 ranks]
     __shared__ __attribute__((aligned(16))) float sV[2][HF_B][320];
-    __shared__ int s0use[2][HF_B];  // [buffer][chunk]: the chunk has a slot-0 record of nonzero value
+    __shared__ int suse[2][HF_B];  // [buffer][chunk]: bit j = the chunk has a slot-j record of nonzero value
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     if ((int)blockIdx.x >= k) return;
     const int q = perm[blockIdx.x];
     const long long o = offs[q];
     const int n = (int)(offs[q + 1] - o);
     const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const bool good = apply_good(kps, offs, ok_in, q);
+    if (wave == 0) {
+        // the LRF's sign disambiguation first (PCL's count + median-5 rule, lrf_fin_one): the keypoint's
+        // per-chunk sign counts summed by the wave (integers, any order), the rule on lane 0
+        const int ok0 = okf[q];
+        int st = 0, sn = 0;
+        if (ok0) {
+            const int2* cs2 = reinterpret_cast<const int2*>(csign);
+            for (int c = cb[q] + lane; c < cb[q + 1]; c += 64) {
+                const int2 v = cs2[c];
+                st += v.x;
+                sn += v.y;
+            }
+            st = wave_sum_i(st);
+            sn = wave_sum_i(sn);
+        }
+        if (lane == 0) {
+            float r9[9];
+            if (ok0) {
+                double e[7];
+                for (int j = 0; j < 7; ++j) e[j] = eig[8 * (size_t)q + j];
+                lrf_fin_one(pts4, kx, ky, kz, seg + o, n, e, st, sn, r9);
+            } else {
+                for (int j = 0; j < 9; ++j) r9[j] = __builtin_nanf("");
+            }
+            for (int j = 0; j < 9; ++j) {
+                rfs[j] = r9[j];
+                rf_out[9 * (size_t)q + j] = r9[j];
+            }
+            ok_out[q] = ok0;
+            okq = ok0;
+        }
+    }
+    for (int j = threadIdx.x; j < 384; j += 64 * HF_WAVES) hist[j] = 0.0f;
+    __syncthreads();
+    const bool good = __builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz) && okq && n >= 5;
     const int nch = good ? cb[q + 1] - cb[q] : 0;
     float rf[9];
 #pragma unroll
-    for (int j = 0; j < 9; ++j) rf[j] = good ? rf_in[9 * (size_t)q + j] : 0.f;
-    for (int j = threadIdx.x; j < 384; j += 64 * HF_WAVES) hist[j] = 0.0f;
+    for (int j = 0; j < 9; ++j) rf[j] = good ? rfs[j] : 0.f;
     auto produce = [&](int t, int buf, int bi) {
         const int i = t * 64 + lane;
         int bins[5] = {-1, -1, -1, -1, -1};
@@ -557,10 +565,14 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
             sS[buf][bi][64 * j + lane] = bins[j] < 0 ? (unsigned short)360 : (unsigned short)bins[j];
             sV[buf][bi][64 * j + lane] = bins[j] < 0 ? 0.f : vals[j];
         }
-        // slot 0 (the cosine interpolation) adds +-0 for every neighbour whose normal slot is zero,
-        // i.e. all but the few with index < K in the reference's mis-indexed normals array
-        const bool u0 = __ballot(bins[0] >= 0 && vals[0] != 0.f) != 0ull;
-        if (lane == 0) s0use[buf][bi] = u0 ? 1 : 0;
+        // which slots hold a live record (nonzero value): slot 0 (the cosine interpolation) adds +-0
+        // for every neighbour whose normal slot is zero, i.e. all but the few with index < K in the
+        // reference's mis-indexed normals array; slot 1 (the radial one) is live only for distances
+        // in [R/4, 3R/4], a contiguous rank range since ranks ascend in distance
+        int use = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) use |= __ballot(bins[j] >= 0 && vals[j] != 0.f) != 0ull ? 1 << j : 0;
+        if (lane == 0) suse[buf][bi] = use;
     };
     if (wave >= 1 && wave - 1 < nch) produce(wave - 1, 0, wave - 1);
     __syncthreads();
@@ -568,12 +580,13 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     for (int b = 0; b < nb; ++b) {
         const int buf = b & 1;
         if (wave == 0) {
-            // a batch whose slot-0 records all add +-0 is applied by lanes 1..4 only: adding +-0
-            // leaves a bin's bits unchanged (bins start at +0 and every record value is >= +0 or
-            // -0, so no bin is ever -0), and the LDS atomic unit's time is per active lane
-            int use0 = 0;
-            for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use0 |= s0use[buf][bi];
-            if (lane < 5 && (lane > 0 || use0)) {
+            // a slot whose records in this batch all add +-0 sits the batch out (one wave-uniform
+            // exec mask per batch, no per-record branch): adding +-0 leaves a bin's bits unchanged
+            // (bins start at +0 and every record value is >= +0 or -0, so no bin is ever -0), and the
+            // LDS atomic unit's time is per active lane
+            int use = 0;
+            for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use |= suse[buf][bi];
+            if (lane < 5 && ((use >> lane) & 1)) {
                 for (int half = 0; half < 2 * HF_B && b * HF_B + (half >> 1) < nch; ++half) {
                     // 32 ranks of chunk half / 2 at a time (keeps the applying path's registers low)
                     const int bi = half >> 1, r0 = 32 * (half & 1);
@@ -641,17 +654,16 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
             bsk::k_lrf_chunks<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.R, A.offs, A.cb, A.owner, A.sorted,
                                                        A.csum);
         }
-        bsk::k_lrf_eig<<<(A.k + 63) / 64, 64, 0, s>>>(A.k, A.cb, A.csum, A.eig, A.okf);
+        bsk::k_lrf_eig<<<(A.k + LE_WAVES - 1) / LE_WAVES, 64 * LE_WAVES, 0, s>>>(A.k, A.cb, A.csum, A.eig, A.okf);
         if (A.n_chunks > 0)
             bsk::k_lrf_sign<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.owner, A.sorted, A.eig,
                                                      A.okf, A.signs);
-        bsk::k_lrf_fin<<<(A.k + 63) / 64, 64, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.sorted, A.eig, A.okf,
-                                                      A.signs, A.rf, A.ok);
+        // the sign rule (k_lrf_fin of round 2) runs at the start of the histogram kernel
         return hipGetLastError();
     }
     // 8 waves per workgroup: 1 applies, 7 produce records
     bsk::k_hist_fused<8><<<A.k, 64 * 8, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
-                                                 A.rf, A.ok, A.shot, A.bits);
+                                                 A.eig, A.okf, A.signs, A.rf, A.ok, A.shot, A.bits);
     return hipGetLastError();
 }
 
