@@ -137,8 +137,10 @@ struct bshot_ctx {
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
     int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
     int opt_side_prio = 0;      // describe (side) stream priority: 0 low (as SR/ISS ahead), 1 middle, 2 the main stream's
+    int opt_map_sync = 1;       // GPU map insert: wait for it and report the map size per sweep (0: stream-ordered, size -1)
     int opt_host_map_log = 1;   // LidarOdometry keeps the GPU map's insert log for the host Map view (bshot_odom: 0)
     int opt_normals_seg = 1;    // normals from the SHOT neighbour lists when normal_radius == shot_radius
+    int opt_sr_run = 1;         // SR: consecutive cell-order queries per wave (a query near its predecessor starts at its step)
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
 
@@ -164,7 +166,7 @@ struct bshot_ctx {
     DBuf<unsigned int> bits;
     // load-balanced SHOT (describe2.hip)
     DBuf<int4> plan;
-    DBuf<int> cb, owner, okf, signs, perm;
+    DBuf<int> cb, owner, okf, perm;
     DBuf<double> csum, eig;
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)

@@ -197,7 +197,7 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks),
+                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks, c->opt_sr_run),
                "seg_ratio launch");
         c->stage_end(sg2, st);
         HIPCHK(kcopy(s.h_ratio.p, s.ratio.p, sizeof(float) * n, st), "D2H ratio");
@@ -415,13 +415,6 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     // A4: with normal_radius == shot_radius the normals' neighbours are the head of each keypoint's
     // sorted SHOT segment (k_normals_seg after the rank below); otherwise a search of their own
     const bool nseg = c->opt_normals_seg && c->prm.normal_radius == c->prm.shot_radius;
-    auto normals_from_segments = [&](const long long* offs, const unsigned int* sorted) -> int {
-        const int sgn = c->stage_begin(BSHOT_STAGE_NORMALS, st);
-        HIPCHK(launch_normals_seg(S.pts4.p, c->kps.p, k, offs, sorted, c->prm.normal_max_nn, c->normals.p, st),
-               "normals (segments) launch");
-        c->stage_end(sgn, st);
-        return BSHOT_OK;
-    };
     if (!nseg) {
         const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
         HIPCHK(launch_normals(S.ladder, c->ladder_mode(S), S.pts4.p, c->kps.p, k, c->prm.normal_radius,
@@ -450,7 +443,6 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         HIPCHK(c->csum.ensure(8 * (size_t)chunk_cap), "alloc csum");
         HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
         HIPCHK(c->okf.ensure(k), "alloc okf");
-        HIPCHK(c->signs.ensure(2 * (size_t)chunk_cap), "alloc signs");
         HIPCHK(launch_shot_count_plan(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->sbh.p, seg_cap, chunk_cap,
                                       c->offs.p, c->cb.p, c->perm.p, c->errw.p, st),
                "shot count + plan");
@@ -465,17 +457,14 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p;
         A.pts4 = S.pts4.p; A.normals = c->normals.p;
         A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
-        A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p;
+        A.okf = c->okf.p; A.rf = c->rf.p; A.ok = c->ok.p;
+        A.nseg_max_nn = nseg ? c->prm.normal_max_nn : 0; A.normals_out = c->normals.p;
         A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
         A.bstart = c->sbst.p;
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
-        if (nseg) {
-            const int rc = normals_from_segments(c->offs.p, c->segtmp.p);
-            if (rc) return rc;
-        }
         const int sg11 = c->stage_begin(BSHOT_STAGE_LRF, st);
         HIPCHK(launch_describe2(A, 1, st), "describe2 lrf");
         c->stage_end(sg11, st);
@@ -527,7 +516,6 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     HIPCHK(c->csum.ensure(8 * (size_t)(cbr > 0 ? cbr : 1)), "alloc csum");
     HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
     HIPCHK(c->okf.ensure(k), "alloc okf");
-    HIPCHK(c->signs.ensure(2 * (size_t)(cbr > 0 ? cbr : 1)), "alloc signs");  // per-chunk sign counts
     HIPCHK(c->perm.ensure(k), "alloc perm");
     HIPCHK(kcopy(c->cb.p, hcb, sizeof(int) * ((size_t)k + 1), st), "H2D cb");
     HIPCHK(kcopy(c->perm.p, hperm, sizeof(int) * k, st), "H2D perm");
@@ -535,17 +523,14 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.k = k; A.n_plan = n_plan; A.n_chunks = cbr; A.R = R;
     A.cb = c->cb.p; A.owner = c->owner.p; A.perm = c->perm.p; A.offs = c->offs.p; A.pts4 = S.pts4.p; A.normals = c->normals.p;
     A.kps = c->kps.p; A.seg = c->seg.p; A.sorted = c->segtmp.p; A.csum = c->csum.p; A.eig = c->eig.p;
-    A.okf = c->okf.p; A.signs = c->signs.p; A.rf = c->rf.p; A.ok = c->ok.p;
+    A.okf = c->okf.p; A.rf = c->rf.p; A.ok = c->ok.p;
+    A.nseg_max_nn = nseg ? c->prm.normal_max_nn : 0; A.normals_out = c->normals.p;
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
     A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
-    if (nseg) {
-        const int rc = normals_from_segments(c->offs.p, c->segtmp.p);
-        if (rc) return rc;
-    }
     const int sg11 = c->stage_begin(BSHOT_STAGE_LRF, st);
     HIPCHK(launch_describe2(A, 1, st), "describe2 lrf");
     c->stage_end(sg11, st);
@@ -1103,7 +1088,7 @@ int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
     HIPCHK(c->cs.ratio.ensure(c->cs.n), "alloc ratio");
     HIPCHK(hipMemsetAsync(k.p, 0, 32 * sizeof(unsigned long long), c->stream), "memset");
     HIPCHK(launch_seg_ratio(c->cs.ladder, c->ladder_mode(c->cs), c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                            c->opt_sr_start, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p),
+                            c->opt_sr_start, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p, c->opt_sr_blocks, c->opt_sr_run),
            "seg_ratio (stats)");
     unsigned long long h[32];
     HIPCHK(hipMemcpyAsync(h, k.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
@@ -1120,8 +1105,10 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     if (k == "ladder_grids") c->opt_ladder4 = value == 4 ? 1 : 0;
     else if (k == "iss_cell") c->opt_iss_cell = value >= 2 ? 2 : 1;
     else if (k == "sr_start") c->opt_sr_start = value < 0 ? 0 : value;
+    else if (k == "sr_run") c->opt_sr_run = value < 1 ? 1 : (value > 64 ? 64 : value);
     else if (k == "normals_seg") c->opt_normals_seg = value ? 1 : 0;
     else if (k == "host_map_log") c->opt_host_map_log = value ? 1 : 0;
+    else if (k == "map_sync") c->opt_map_sync = value ? 1 : 0;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);

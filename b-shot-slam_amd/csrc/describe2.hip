@@ -5,9 +5,10 @@
 //
 //   (sorting: k_shot_rank, csrc/describe.hip -- exact rank inside the count pass's d2 buckets)
 //   k_lrf_chunks  wave per 64-rank chunk: 7 weighted-covariance terms by the xor-butterfly tree
-//   k_lrf_eig     wave per keypoint: chunk sums in chunk order (a lane per term), Jacobi eigenvectors
-//   k_lrf_sign    wave per chunk: sign counts for the x/z disambiguation (integer, order-free)
-//   k_hist_fused  workgroup per keypoint: PCL's count + median-5 sign rule (float LRF rows) first,
+//   k_lrf_eig     wave per keypoint: chunk sums in chunk order (a lane per term), Jacobi eigenvectors;
+//                 with normal_radius == shot_radius also the keypoint normal (segment_normal)
+//   k_hist_fused  workgroup per keypoint: the x/z sign counts and PCL's count + median-5 rule
+//                 (float LRF rows) first,
 //                 then 7 waves compute the <= 5 (bin, value)
 //                 interpolation records of every neighbour into a double-buffered LDS batch while
 //                 one wave applies them in rank order to the LDS histogram (in-order ds_add_f32),
@@ -76,6 +77,73 @@ __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ p
     }
 }
 
+// A4 from the SHOT neighbour lists (include/bshot_bits.h:63-80): with normal_radius == shot_radius
+// the normals' FLANN radius search (the normal_max_nn smallest (d2, idx) with d2 < r^2, in that
+// order) is the first min(n, normal_max_nn) entries of the keypoint's sorted SHOT segment, so no
+// search of its own is needed. One wave: the neighbours' coordinates in LDS (f: 3 x 512 floats), the
+// 9 accumulators of pcl::computeMeanAndCovarianceMatrix as sequential float sums in rank order
+// (lanes 0..5: xx xy xz yy yz zz products, lanes 6..8: x y z -- k_normals' order), then eigen33 and
+// the flip towards the origin. Returns (nx, ny, nz, curvature), NaN as k_normals.
+__device__ __forceinline__ float4 segment_normal(const float4* __restrict__ pts4, float kx, float ky, float kz,
+                                                 const unsigned int* __restrict__ sg, long long cnt, int max_nn,
+                                                 float* f) {
+    const int lane = lane_id();
+    const float qn = __builtin_nanf("");
+    float nx = qn, ny = qn, nz = qn, curv = qn;
+    if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
+        const int need = (int)(cnt < max_nn ? cnt : max_nn);
+        if (need > 0) {
+            float acc = 0.f;
+            if (need >= 3) {
+                for (int r = lane; r < need; r += 64) {
+                    const float4 p = pts4[sg[r]];
+                    f[r] = p.x; f[512 + r] = p.y; f[1024 + r] = p.z;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 9) {
+                    const bool prod = lane < 6;
+                    const int a = prod ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
+                    const int b = lane < 3 ? lane : (lane < 5 ? lane - 2 : 2);
+                    const float* pa = f + 512 * a;
+                    const float* pb = f + 512 * (prod ? b : a);
+                    int r = 0;
+                    for (; r + 4 <= need; r += 4) {
+                        float v[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) v[u] = prod ? pa[r + u] * pb[r + u] : pa[r + u];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) acc = acc + v[u];
+                    }
+                    for (; r < need; ++r) acc = acc + (prod ? pa[r] * pb[r] : pa[r]);
+                }
+            }
+            if (need >= 3) {
+                float ac[9];
+                const float fn = (float)need;
+#pragma unroll
+                for (int a = 0; a < 9; ++a) ac[a] = __shfl(acc, a, 64) / fn;
+                float cov[9];
+                cov[0] = ac[0] - ac[6] * ac[6];
+                cov[1] = ac[1] - ac[6] * ac[7];
+                cov[2] = ac[2] - ac[6] * ac[8];
+                cov[4] = ac[3] - ac[7] * ac[7];
+                cov[5] = ac[4] - ac[7] * ac[8];
+                cov[8] = ac[5] - ac[8] * ac[8];
+                cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+                float ev, vec[3];
+                bm::eigen33_min(cov, &ev, vec);
+                nx = vec[0]; ny = vec[1]; nz = vec[2];
+                const float eig_sum = (cov[0] + cov[4]) + cov[8];
+                curv = (eig_sum != 0.f) ? fabsf(ev / eig_sum) : 0.f;
+            }
+            const float vx = 0.f - kx, vy = 0.f - ky, vz = 0.f - kz;
+            const float cth = (vx * nx + vy * ny) + vz * nz;
+            if (cth < 0.f) { nx *= -1.f; ny *= -1.f; nz *= -1.f; }
+        }
+    }
+    return make_float4(nx, ny, nz, curv);
+}
+
 // Jacobi eigenvectors of keypoint q's weighted covariance (tot: the 7 chunk-ordered sums, valid: the
 // valid-neighbour count): e[0..2] = x axis (largest), [3..5] = z axis (smallest), [6] = valid count;
 // returns the ok flag
@@ -102,13 +170,26 @@ __device__ __forceinline__ int lrf_eig_of_sums(const double* tot, long long vali
 // eig[8 q + 0..6] (lrf_eig_of_sums), okf[q]. A wave per keypoint: lane j < 7 sums column j of the
 // keypoint's chunk partials in chunk order (sequential double adds; the 8 lanes of a chunk read its
 // 64 B together), lane 7 the valid counts (integers); lane 0 then runs the Jacobi solver.
+// nmax > 0: the same wave first writes the keypoint's normal from the head of its sorted segment
+// (segment_normal; normal_radius == shot_radius), which the histogram kernel reads.
 #define LE_WAVES 4
 __global__ void __launch_bounds__(64 * LE_WAVES) k_lrf_eig(int k, const int* __restrict__ cb,
                                                            const double* __restrict__ csum, double* __restrict__ eig,
-                                                           int* __restrict__ okf) {
+                                                           int* __restrict__ okf, const float4* __restrict__ pts4,
+                                                           const float* __restrict__ kps,
+                                                           const long long* __restrict__ offs,
+                                                           const unsigned int* __restrict__ seg, int nmax,
+                                                           float4* __restrict__ normals) {
+    __shared__ float fl[LE_WAVES][3 * 512];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int q = blockIdx.x * LE_WAVES + wave;
     if (q >= k) return;  // no workgroup barrier below
+    if (nmax > 0) {
+        const long long o = offs[q];
+        const float4 nv = segment_normal(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o, offs[q + 1] - o, nmax,
+                                         fl[wave]);
+        if (lane == 0) normals[q] = nv;
+    }
     const int c0 = cb[q], c1 = cb[q + 1];
     double acc = 0.0;
     long long valid = 0;
@@ -143,41 +224,6 @@ __global__ void __launch_bounds__(64 * LE_WAVES) k_lrf_eig(int k, const int* __r
             for (int j = 0; j < 6; ++j) eo[j] = e[j];
         eo[6] = e[6];
         okf[q] = ok;
-    }
-}
-
-// #(v . x >= 0), #(v . z >= 0) over the valid neighbours of chunk t of a keypoint (wave-uniform result)
-__device__ __forceinline__ int2 lrf_sign_counts(const float4* __restrict__ pts4, float kx, float ky, float kz,
-                                                const unsigned int* __restrict__ sg, int n, int t, const double* e) {
-    const int lane = lane_id();
-    const int i = t * 64 + lane;
-    int pt = 0, pn = 0;
-    if (i < n) {
-        const float4 p = pts4[sg[i]];
-        if (!(p.x == kx && p.y == ky && p.z == kz)) {
-            const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
-            if (((vx * e[0] + vy * e[1]) + vz * e[2]) >= 0) pt = 1;
-            if (((vx * e[3] + vy * e[4]) + vz * e[5]) >= 0) pn = 1;
-        }
-    }
-    return make_int2(__popcll(__ballot(pt != 0)), __popcll(__ballot(pn != 0)));
-}
-
-// csign[2 c], [2 c + 1]: chunk c's sign counts (summed by k_hist_fused's first wave: no same-address atomics)
-__global__ void __launch_bounds__(256) k_lrf_sign(const float4* __restrict__ pts4, const float* __restrict__ kps, int k,
-                                                  const long long* __restrict__ offs, const int* __restrict__ cb,
-                                                  const int* __restrict__ owner,
-                                                  const unsigned int* __restrict__ seg,
-                                                  const double* __restrict__ eig, const int* __restrict__ okf,
-                                                  int* __restrict__ csign) {
-    // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
-        const int q = owner[c];
-        if (!okf[q]) continue;
-        const long long o = offs[q];
-        const int2 v = lrf_sign_counts(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o,
-                                       (int)(offs[q + 1] - o), c - cb[q], eig + 8 * (size_t)q);
-        if (lane_id() == 0) reinterpret_cast<int2*>(csign)[c] = v;
     }
 }
 
@@ -235,83 +281,6 @@ __device__ __forceinline__ void lrf_fin_one(const float4* __restrict__ pts4, flo
     r9[0] = x0; r9[1] = x1; r9[2] = x2;
     r9[3] = z1 * x2 - z2 * x1; r9[4] = z2 * x0 - z0 * x2; r9[5] = z0 * x1 - z1 * x0;
     r9[6] = z0; r9[7] = z1; r9[8] = z2;
-}
-
-// A4 from the SHOT neighbour lists (include/bshot_bits.h:63-80): with normal_radius == shot_radius
-// the normals' FLANN radius search (the normal_max_nn smallest (d2, idx) with d2 < r^2, in that
-// order) is the first min(n, normal_max_nn) entries of the keypoint's sorted SHOT segment, so no
-// search of its own is needed. A wave per keypoint: the neighbours' coordinates in LDS, the 9
-// accumulators of pcl::computeMeanAndCovarianceMatrix as sequential float sums in rank order
-// (lanes 0..5: xx xy xz yy yz zz products, lanes 6..8: x y z -- k_normals' order), then eigen33 and
-// the flip towards the origin.
-#define NS_WAVES 4
-__global__ void __launch_bounds__(64 * NS_WAVES) k_normals_seg(const float4* __restrict__ pts4,
-                                                               const float* __restrict__ kps, int k,
-                                                               const long long* __restrict__ offs,
-                                                               const unsigned int* __restrict__ seg, int max_nn,
-                                                               float4* __restrict__ normals) {
-    __shared__ float fl[NS_WAVES][3 * 512];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
-    const int q = blockIdx.x * NS_WAVES + wave;
-    if (q >= k) return;  // no workgroup barrier below
-    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    const float qn = __builtin_nanf("");
-    float nx = qn, ny = qn, nz = qn, curv = qn;
-    if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
-        const long long o = offs[q];
-        const long long cnt = offs[q + 1] - o;
-        const int need = (int)(cnt < max_nn ? cnt : max_nn);
-        if (need > 0) {
-            float* f = fl[wave];
-            float acc = 0.f;
-            if (need >= 3) {
-                for (int r = lane; r < need; r += 64) {
-                    const float4 p = pts4[seg[o + r]];
-                    f[r] = p.x; f[512 + r] = p.y; f[1024 + r] = p.z;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (lane < 9) {
-                    const bool prod = lane < 6;
-                    const int a = prod ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
-                    const int b = lane < 3 ? lane : (lane < 5 ? lane - 2 : 2);
-                    const float* pa = f + 512 * a;
-                    const float* pb = f + 512 * (prod ? b : a);
-                    int r = 0;
-                    for (; r + 4 <= need; r += 4) {
-                        float v[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) v[u] = prod ? pa[r + u] * pb[r + u] : pa[r + u];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) acc = acc + v[u];
-                    }
-                    for (; r < need; ++r) acc = acc + (prod ? pa[r] * pb[r] : pa[r]);
-                }
-            }
-            if (need >= 3) {
-                float ac[9];
-                const float fn = (float)need;
-#pragma unroll
-                for (int a = 0; a < 9; ++a) ac[a] = __shfl(acc, a, 64) / fn;
-                float cov[9];
-                cov[0] = ac[0] - ac[6] * ac[6];
-                cov[1] = ac[1] - ac[6] * ac[7];
-                cov[2] = ac[2] - ac[6] * ac[8];
-                cov[4] = ac[3] - ac[7] * ac[7];
-                cov[5] = ac[4] - ac[7] * ac[8];
-                cov[8] = ac[5] - ac[8] * ac[8];
-                cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
-                float ev, vec[3];
-                bm::eigen33_min(cov, &ev, vec);
-                nx = vec[0]; ny = vec[1]; nz = vec[2];
-                const float eig_sum = (cov[0] + cov[4]) + cov[8];
-                curv = (eig_sum != 0.f) ? fabsf(ev / eig_sum) : 0.f;
-            }
-            const float vx = 0.f - kx, vy = 0.f - ky, vz = 0.f - kz;
-            const float cth = (vx * nx + vy * ny) + vz * nz;
-            if (cth < 0.f) { nx *= -1.f; ny *= -1.f; nz *= -1.f; }
-        }
-    }
-    if (lane == 0) normals[q] = make_float4(nx, ny, nz, curv);
 }
 
 __device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0, float b1, float b2) {
@@ -498,7 +467,6 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
                                                               const unsigned int* __restrict__ seg,
                                                               const double* __restrict__ eig,
                                                               const int* __restrict__ okf,
-                                                              const int* __restrict__ csign,
                                                               float* __restrict__ rf_out, int* __restrict__ ok_out,
                                                               float* __restrict__ shot_out,
                                                               unsigned int* __restrict__ bits_out) {
@@ -506,6 +474,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     __shared__ float hist[384];
     __shared__ float rfs[9];
     __shared__ int okq;
+    __shared__ int sgn[2];
     __shared__ unsigned int gcode[88];
     __shared__ __attribute__((aligned(16))) unsigned short sS[2][HF_B][320];  // [buffer][chunk][slot x 64 ranks]
     __shared__ __attribute__((aligned(16))) float sV[2][HF_B][320];
@@ -516,37 +485,53 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
     const long long o = offs[q];
     const int n = (int)(offs[q + 1] - o);
     const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
-    if (wave == 0) {
-        // the LRF's sign disambiguation first (PCL's count + median-5 rule, lrf_fin_one): the keypoint's
-        // per-chunk sign counts summed by the wave (integers, any order), the rule on lane 0
-        const int ok0 = okf[q];
-        int st = 0, sn = 0;
-        if (ok0) {
-            const int2* cs2 = reinterpret_cast<const int2*>(csign);
-            for (int c = cb[q] + lane; c < cb[q + 1]; c += 64) {
-                const int2 v = cs2[c];
-                st += v.x;
-                sn += v.y;
+    // the LRF's sign disambiguation first (SHOTLocalReferenceFrameEstimation: PCL's count rule, then
+    // the median-5 rule on ties, lrf_fin_one): #(v . x >= 0) and #(v . z >= 0) over the valid
+    // neighbours, counted by the whole workgroup (integers, any order)
+    const int ok0 = okf[q];
+    if (threadIdx.x < 2) sgn[threadIdx.x] = 0;
+    __syncthreads();
+    double ev[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) ev[j] = ok0 ? eig[8 * (size_t)q + j] : 0.0;
+    if (ok0) {
+        int pt = 0, pn = 0;
+        for (int i0 = 0; i0 < n; i0 += 64 * HF_WAVES) {
+            const int i = i0 + (int)threadIdx.x;
+            bool a = false, c = false;
+            if (i < n) {
+                const float4 p = pts4[seg[o + i]];
+                if (!(p.x == kx && p.y == ky && p.z == kz)) {
+                    const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
+                    a = ((vx * ev[0] + vy * ev[1]) + vz * ev[2]) >= 0;
+                    c = ((vx * ev[3] + vy * ev[4]) + vz * ev[5]) >= 0;
+                }
             }
-            st = wave_sum_i(st);
-            sn = wave_sum_i(sn);
+            pt += __popcll(__ballot(a));
+            pn += __popcll(__ballot(c));
         }
         if (lane == 0) {
-            float r9[9];
-            if (ok0) {
-                double e[7];
-                for (int j = 0; j < 7; ++j) e[j] = eig[8 * (size_t)q + j];
-                lrf_fin_one(pts4, kx, ky, kz, seg + o, n, e, st, sn, r9);
-            } else {
-                for (int j = 0; j < 9; ++j) r9[j] = __builtin_nanf("");
-            }
-            for (int j = 0; j < 9; ++j) {
-                rfs[j] = r9[j];
-                rf_out[9 * (size_t)q + j] = r9[j];
-            }
-            ok_out[q] = ok0;
-            okq = ok0;
+            atomicAdd(&sgn[0], pt);
+            atomicAdd(&sgn[1], pn);
         }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r9[9];
+        if (ok0) {
+            double e[7];
+            for (int j = 0; j < 6; ++j) e[j] = ev[j];
+            e[6] = eig[8 * (size_t)q + 6];
+            lrf_fin_one(pts4, kx, ky, kz, seg + o, n, e, sgn[0], sgn[1], r9);
+        } else {
+            for (int j = 0; j < 9; ++j) r9[j] = __builtin_nanf("");
+        }
+        for (int j = 0; j < 9; ++j) {
+            rfs[j] = r9[j];
+            rf_out[9 * (size_t)q + j] = r9[j];
+        }
+        ok_out[q] = ok0;
+        okq = ok0;
     }
     for (int j = threadIdx.x; j < 384; j += 64 * HF_WAVES) hist[j] = 0.0f;
     __syncthreads();
@@ -626,14 +611,6 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
 
 namespace bsh {
 
-hipError_t launch_normals_seg(const float4* pts4, const float* kps, int k, const long long* offs, const unsigned int* seg,
-                              int max_nn, float4* normals, hipStream_t s) {
-    if (k <= 0) return hipSuccess;
-    if (max_nn < 1 || max_nn > 512) return hipErrorInvalidValue;
-    bsk::k_normals_seg<<<(k + NS_WAVES - 1) / NS_WAVES, 64 * NS_WAVES, 0, s>>>(pts4, kps, k, offs, seg, max_nn, normals);
-    return hipGetLastError();
-}
-
 // part 0: in-bucket rank (sorted segments); 1: LRF; 2: histogram records + ordered apply
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.k <= 0) return hipSuccess;
@@ -654,16 +631,16 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
             bsk::k_lrf_chunks<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.R, A.offs, A.cb, A.owner, A.sorted,
                                                        A.csum);
         }
-        bsk::k_lrf_eig<<<(A.k + LE_WAVES - 1) / LE_WAVES, 64 * LE_WAVES, 0, s>>>(A.k, A.cb, A.csum, A.eig, A.okf);
-        if (A.n_chunks > 0)
-            bsk::k_lrf_sign<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.offs, A.cb, A.owner, A.sorted, A.eig,
-                                                     A.okf, A.signs);
-        // the sign rule (k_lrf_fin of round 2) runs at the start of the histogram kernel
+        // nmax > 0: the keypoint normals from the sorted segments in the same launch
+        bsk::k_lrf_eig<<<(A.k + LE_WAVES - 1) / LE_WAVES, 64 * LE_WAVES, 0, s>>>(
+            A.k, A.cb, A.csum, A.eig, A.okf, A.pts4, A.kps, A.offs, A.sorted, A.nseg_max_nn, A.normals_out);
+        // the sign counts and PCL's sign rule (k_lrf_sign / k_lrf_fin of round 2) run at the start of
+        // the histogram kernel
         return hipGetLastError();
     }
     // 8 waves per workgroup: 1 applies, 7 produce records
     bsk::k_hist_fused<8><<<A.k, 64 * 8, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
-                                                 A.eig, A.okf, A.signs, A.rf, A.ok, A.shot, A.bits);
+                                                 A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
     return hipGetLastError();
 }
 

@@ -649,12 +649,14 @@ int gmap_insert(bshot_ctx* c, const float* kps_host, const float* ratio_host, co
         HIPCHK(kcopy(g.kin.p, g.p_kin.p, sizeof(float) * 4 * k, c->stream), "H2D map in");
         bsk::k_gmap_prep<<<(k + 255) / 256, 256, 0, c->stream>>>(g.kin.p, g.kin.p + 3 * (size_t)k, d_bits, k, xf(T),
                                                                  g.slots, dev_view(g), g.keys.p, g.vals.p);
-        if ((rc = gmap_run_insert(c, g, k, true))) return rc;
-    } else {
+        // option map_sync 0: no host wait for the insert here -- the next map query is stream-ordered
+        // behind it and settles its counters (capacity errors surface there); the size is not read back
+        if ((rc = gmap_run_insert(c, g, k, c->opt_map_sync != 0))) return rc;
+    } else if (c->opt_map_sync) {
         HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, c->stream), "D2H map counters");
         HIPCHK(hipStreamSynchronize(c->stream), "sync map");
     }
-    *map_size = g.p_ctr.p[GM_MEMBERS];
+    *map_size = c->opt_map_sync ? g.p_ctr.p[GM_MEMBERS] : -1;
     return BSHOT_OK;
 }
 
@@ -724,7 +726,8 @@ int gmap_replica_size(bshot_ctx* c, int replica) {
 
 // the 21^3 block loop over one map: counts + scan (async; the total lands in the pinned GM_QTOT slot)
 static int query_count(bshot_ctx* c, GMap& g, const QueryBox& q) {
-    if (q.npos <= 0 || g.p_ctr.p[GM_NBLOCKS] <= 0) {
+    // (an insert whose counters are still in flight may have made the map non-empty: query it)
+    if (q.npos <= 0 || (!g.ctr_pending && g.p_ctr.p[GM_NBLOCKS] <= 0)) {
         g.p_ctr.p[GM_QTOT] = 0;
         g.q_active = false;
         return BSHOT_OK;
@@ -780,7 +783,12 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
         if ((rc = query_count(c, *m, q))) return rc;
         any = any || m->q_active;
     }
-    if (any) HIPCHK(hipStreamSynchronize(c->stream), "sync map query");
+    if (any) {
+        HIPCHK(hipStreamSynchronize(c->stream), "sync map query");
+        // the stream sync covers this map's last unsynchronised insert (option map_sync 0): its
+        // counters have landed; an insert that ran out of capacity fails the sweep here
+        if ((rc = gmap_settle(c, g))) return rc;
+    }
     c->hmark("M_q_synced");
     int mtot = 0;
     for (GMap* m : maps) mtot += m->q_active ? m->p_ctr.p[GM_QTOT] : 0;

@@ -17,7 +17,7 @@ hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s);
 // for mode 0), see ladder() in knn.hip
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst = nullptr, int max_blocks = 8192);
+                            unsigned long long* kst = nullptr, int max_blocks = 8192, int run = 1);
 hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float4* pts4, const float* kps, int k,
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
@@ -40,10 +40,6 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
                             hipStream_t s, int max_blocks = 0);
-// A4 from the sorted SHOT segments (normal_radius == shot_radius): the first min(n, max_nn) neighbour
-// indices of each keypoint's segment (seg: launch_shot_rank's output, offs its segment offsets)
-hipError_t launch_normals_seg(const float4* pts4, const float* kps, int k, const long long* offs, const unsigned int* seg,
-                              int max_nn, float4* normals, hipStream_t s);
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
@@ -93,7 +89,8 @@ struct Describe2Args {
     double* csum = nullptr;                   // 8 per chunk
     double* eig = nullptr;                    // 8 per keypoint
     int* okf = nullptr;                       // eigen ok per keypoint
-    int* signs = nullptr;                     // 2 per chunk: sign counts (k_lrf_sign)
+    int nseg_max_nn = 0;                      // > 0: k_lrf_eig also writes the keypoint normals from the sorted
+    float4* normals_out = nullptr;            //   segments' heads (normal_max_nn; normal_radius == shot_radius)
     float* rf = nullptr;
     int* ok = nullptr;
     float* shot = nullptr;

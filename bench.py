@@ -82,6 +82,9 @@ def parse():
                     help="process sweeps strictly one after another (no lookahead of the next sweep's SR/ISS)")
     ap.add_argument("--ladder-grids", type=int, default=None, help="tuning knob: 2 or 4 kNN ladder grids")
     ap.add_argument("--opt", action="append", default=[], help="tuning knob name=value (bshot_odom_set_option)")
+    ap.add_argument("--map-sync", action="store_true",
+                    help="wait for every GPU map insert and read the map size back per sweep (odometry_test never "
+                         "reads it; default: the insert stays stream-ordered before the next sweep's map query)")
     ap.add_argument("--from-lasers", action="store_true",
                     help="each sweep starts as HBM-resident laser returns and runs the GPU preprocessor "
                          "(SURVEY 8f row 3: range image, ground + occlusion removal) before the odometry")
@@ -165,6 +168,10 @@ def main():
         pre_done[j] = True
 
     odo = bshot_py.Odometry(device=local, params=params)
+    try:
+        odo.set_option("map_sync", 1 if a.map_sync else 0)
+    except bshot_py.BshotError:  # an older library (A/B runs against a previous build)
+        pass
     if a.ladder_grids is not None:
         odo.set_option("ladder_grids", a.ladder_grids)
     if a.metrics and rank == 0:
@@ -270,6 +277,10 @@ def main():
         host = [f_.cpu().pin_memory() for f_ in frames]
         dbuf = [torch.empty_like(f_) for f_ in frames]
         odo2 = bshot_py.Odometry(device=local, params=params)
+        try:
+            odo2.set_option("map_sync", 1 if a.map_sync else 0)
+        except bshot_py.BshotError:
+            pass
         if a.ladder_grids is not None:
             odo2.set_option("ladder_grids", a.ladder_grids)
         for kv in a.opt:
@@ -454,6 +465,7 @@ def main():
                                    f"{int(n_eff)} pts/sweep, K={a.keypoints}, SHOT r={a.shot_radius:g} mm, "
                                    f"full extract+describe+match+RANSAC+ICP+map per sweep",
                        "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
+                       "map_size_readback": bool(a.map_sync),
                        "icp_iters": icp_it, "mutual_corr": round(corr, 1), "parallelism": f"frame-shard x{world}" +
                        (" + RCCL map exchange" if a.map_bcast else "") +
                        (f" + RCCL map exchange (1 rank) with {a.sim_peers} simulated peers' replica inserts"

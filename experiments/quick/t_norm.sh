@@ -4,4 +4,4 @@ timeout -k 10 900 python -u -m pytest tests/test_golden.py tests/test_odometry_g
 tail -3 $O/t_norm.log
 [ $rc -eq 0 ] || exit $rc
 bash experiments/quick/r03_diag.sh new || exit 1
-bash experiments/quick/ab_lib.sh 3
+bash experiments/quick/ab_lib.sh 4

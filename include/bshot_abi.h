@@ -285,7 +285,10 @@ int bshot_map_set_query_mode(bshot_map* m, int mode);
  *      (canonical order) / 0 (host Map); "xseq_targets" 0 (default): other sequences' replicas join
  *      the matching targets; "host_map_log" 1 (default; 0 under bshot_odom): keep the GPU map's
  *      insert log so the host Map view (LidarOdometry::getKeypoints, getBlockKeypoints) can be
- *      rebuilt -- without it host memory stays flat over a run and that view is unavailable. */
+ *      rebuilt -- without it host memory stays flat over a run and that view is unavailable;
+ *      "map_sync" 1 (default): the GPU map insert is waited for and bshot_frame_stats.map_size
+ *      reported every sweep; 0: the insert stays stream-ordered before the next sweep's map query
+ *      (which settles its counters and reports capacity errors), map_size is -1. */
 int bshot_set_option(bshot_ctx* c, const char* name, int value);
 
 /* ---- instrumentation: per-stage device time (ms) accumulated with hipEvents on the context's

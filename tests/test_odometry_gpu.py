@@ -70,12 +70,14 @@ def test_odometry_no_icp_no_iss():
     _run_pair(range(3), run_icp=0, run_iss=0)
 
 
-@pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"topk_thread": 0}), (2, {"ransac_dev": 0})])
+@pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"topk_thread": 0}), (2, {"ransac_dev": 0}),
+                                        (2, {"map_sync": 0})])
 def test_odometry_lookahead_device_frames(depth, opts):
     """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
     stream during the current one (bshot_odom_set_next_device; depth 2 also queues the sweep after
     next, bshot_odom_set_next2_device) -- results must not change, whichever host threading
-    (top-K thread) and RANSAC scorer (GPU or host) the knobs select."""
+    (top-K thread), RANSAC scorer (GPU or host) and map-insert wait (map_sync 0: stream-ordered,
+    the size not read back) the knobs select."""
     import torch
 
     frames = [bshot_py.synth_sweep(f)[0] for f in range(20, 25)]
@@ -94,6 +96,8 @@ def test_odometry_lookahead_device_frames(depth, opts):
             st = od.process_device(d.data_ptr(), len(xyz))
             so = oo.process(xyz)
             assert st.n_keypoints == so.n_keypoints and st.n_iss == so.n_iss and st.n_inliers == so.n_inliers, f
+            assert st.n_target == so.n_target, f
+            assert st.map_size == (-1 if opts.get("map_sync", 1) == 0 else so.map_size), f
             assert np.array_equal(od.bits(), oo.bits()), f
             assert np.array_equal(od.iss(), oo.iss()), f
             assert np.array_equal(_u(np.array(st.pose, np.float32)), _u(np.array(so.pose, np.float32))), f
