@@ -16,16 +16,27 @@ __device__ __forceinline__ unsigned long long stamp() {
 // mode 3: ds_add_f32 by lanes 0..2 only
 // mode 4: lanes 0..4, each add exec-masked off when its bin is = 0 mod 8 or odd (about 56% kept)
 // mode 5: as 4, the exec mask set around each ds_add_f32 in inline asm (no branch)
+// mode 6: ds_add_u32 (integer atomic) by all 64 lanes to distinct bins
+// mode 7: ds_add_u32 by all 64 lanes to random bins of 192 (SR histogram pattern)
 template <int MODE>
 __global__ void k(const int* __restrict__ bins, int nops, unsigned long long* out, float* sink) {
     __shared__ float hist[384];
+    __shared__ unsigned int ihist[384];
     __shared__ int bt[1024 * 5];
     const int lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) hist[i] = 0.f;
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) { hist[i] = 0.f; ihist[i] = 0u; }
     for (int i = threadIdx.x; i < 1024 * 5; i += blockDim.x) bt[i] = bins[i];
     __syncthreads();
     const unsigned long long t0 = stamp();
-    if (MODE == 2 || lane < (MODE == 3 ? 3 : 5)) {
+    if (MODE == 6 || MODE == 7) {
+        for (int r0 = 0; r0 < nops; r0 += 16) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int b = MODE == 6 ? ((lane * 5 + u) % 352) : bt[((r0 + u) % 1024) * 5 + (lane % 5)] % 192 + (lane & 7) * 0;
+                atomicAdd(&ihist[MODE == 7 ? (b + lane * 7) % 192 : b], 1u);
+            }
+        }
+    } else if (MODE == 2 || lane < (MODE == 3 ? 3 : 5)) {
         for (int r0 = 0; r0 < nops; r0 += 16) {
             int bb[16];
 #pragma unroll
@@ -61,7 +72,7 @@ __global__ void k(const int* __restrict__ bins, int nops, unsigned long long* ou
     __syncthreads();
     const unsigned long long t1 = stamp();
     if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;
-    if (threadIdx.x < 352) sink[blockIdx.x * 352 + threadIdx.x] = hist[threadIdx.x];
+    if (threadIdx.x < 352) sink[blockIdx.x * 352 + threadIdx.x] = hist[threadIdx.x] + (float)ihist[threadIdx.x];
 }
 
 int main() {
@@ -70,9 +81,12 @@ int main() {
     unsigned s = 12345;
     for (auto& b : hb) { s = s * 1664525u + 1013904223u; b = (s >> 8) % 352; }
     int* db; unsigned long long* dout; float* sink;
-    hipMalloc(&db, hb.size() * 4); hipMalloc(&dout, 8 * 4096); hipMalloc(&sink, 4096 * 352 * 4);
+    // out / sink hold one slot per block of the largest launch below (16384 blocks)
+    const int max_blocks = 16384;
+    hipMalloc(&db, hb.size() * 4); hipMalloc(&dout, 8 * (size_t)max_blocks); hipMalloc(&sink, (size_t)max_blocks * 352 * 4);
     hipMemcpy(db, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
     auto run = [&](auto kern, const char* name, int blocks, int threads) {
+        if (blocks > max_blocks) { printf("%s: %d blocks > %d slots, skipped\n", name, blocks, max_blocks); return; }
         kern<<<blocks, threads>>>(db, nops, dout, sink);
         hipDeviceSynchronize();
         hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
@@ -89,6 +103,11 @@ int main() {
     run(k<0>, "ds_add lanes0-4, 1 wave/block", 1, 64);
     run(k<1>, "rmw lanes0-4, 1 wave/block", 1, 64);
     run(k<2>, "ds_add 64 lanes, 1 wave/block", 1, 64);
+    run(k<6>, "ds_add_u32 64 lanes distinct, 1 wave", 1, 64);
+    run(k<7>, "ds_add_u32 64 lanes random/192, 1 wave", 1, 64);
+    run(k<2>, "ds_add_f32 64 lanes distinct, 8 waves, 256 blk", 256, 512);
+    run(k<6>, "ds_add_u32 64 lanes distinct, 8 waves, 256 blk", 256, 512);
+    run(k<7>, "ds_add_u32 64 lanes random/192, 8 waves, 256 blk", 256, 512);
     run(k<3>, "ds_add lanes0-2, 1 wave/block", 1, 64);
     run(k<4>, "ds_add lanes0-4 masked ~40%, 1 wave", 1, 64);
     run(k<5>, "ds_add lanes0-4 asm-masked, 1 wave", 1, 64);
