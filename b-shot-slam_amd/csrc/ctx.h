@@ -140,7 +140,6 @@ struct bshot_ctx {
     int opt_map_sync = 1;       // GPU map insert: wait for it and report the map size per sweep (0: stream-ordered, size -1)
     int opt_host_map_log = 1;   // LidarOdometry keeps the GPU map's insert log for the host Map view (bshot_odom: 0)
     int opt_normals_seg = 1;    // normals from the SHOT neighbour lists when normal_radius == shot_radius
-    int opt_sr_run = 1;         // SR: consecutive cell-order queries per wave (a query near its predecessor starts at its step)
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
 

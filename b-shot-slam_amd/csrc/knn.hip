@@ -540,13 +540,14 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
 // ------------------------------------------------------------------------------------------
 // A1: segmentation ratio of every point. max_nn <= 512 (host-checked).
 // Queries go in the ladder grids' cell order (g[0].spts, a permutation of the cloud whose .w holds
-// each point's index): a wave takes `run` consecutive positions, and a query whose predecessor in
-// the run lies within one finest-cell diagonal starts its radius ladder at the step that delivered
-// the predecessor (same-cell neighbours need the same step ~93 % of the time on HDL-64 sweeps) --
-// the first query of a run, or one after a jump, starts from its own-cell density prediction
-// (hint). Speed only: any start step gives the same exact selection.
+// each point's index), dealt round-robin over the grid's waves (consecutive workgroups sit on
+// different XCDs; a contiguous stretch of cell order per XCD would hand one XCD the dense
+// near-sensor region). One query per wave pass: short waves let the other streams' kernels in
+// (runs of several cell-order queries per wave, each starting its ladder at its predecessor's
+// step, streamed 11-18 % fewer candidates but were slower in the pipeline,
+// profiles/r03_ab_sr_order_runs.txt).
 __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
-                                                              float radius, int max_nn, int sr_type, int hint, int run,
+                                                              float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
                                                               unsigned long long* __restrict__ kst) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -554,55 +555,33 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
     cand_init(&L->cand);
-    // runs dealt round-robin over every wave of the grid (consecutive workgroups sit on different
-    // XCDs): a contiguous stretch of the cell order per XCD would hand one XCD the dense near-sensor
-    // region (the cloud and grids fit every XCD's L2 either way)
-    const int nw = gridDim.x * KNN_WAVES, gw = blockIdx.x * KNN_WAVES + wave;
-    const int q_end = n;
+    const int nw = gridDim.x * KNN_WAVES;
     const float4* __restrict__ order = lg.g[0].spts;
-    const float c0 = lg.g[0].cell;
-    const float near2 = 3.f * c0 * c0;
     float* fl = reinterpret_cast<float*>(L->list);
-    for (int j0 = gw * run; j0 < q_end; j0 += nw * run) {
-        int prev_used = -1;
-        float px = 0.f, py = 0.f, pz = 0.f;
-        const int j1 = min(q_end, j0 + run);
-        for (int j = j0; j < j1; ++j) {
-            // wave-uniform: held in SGPRs (the kernel sits at its 96-VGPR budget)
-            const float4 spv = order[j];
-            const float4 sp = make_float4(
-                __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spv.x))),
-                __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spv.y))),
-                __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spv.z))),
-                __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spv.w))));
-            const int q = (int)__float_as_uint(sp.w);
-            float out = __builtin_nanf("");
-            const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
-            const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
-            if (!origin && fin) {
-                int need = 0, used = 0, tot = 0;
-                const unsigned long long* sorted = nullptr;
-                const float dx = sp.x - px, dy = sp.y - py, dz = sp.z - pz;
-                int start;
-                if (prev_used >= 0 && dx * dx + dy * dy + dz * dz <= near2) start = prev_used;
-                else start = hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
-                const bool ok = knn_select(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
-                const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
-                if (!ok) {
-                    if (lane == 0) atomicOr(err, 1);
-                } else if (need > 0) {
-                    out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
-                }
-                prev_used = __builtin_amdgcn_readfirstlane(ok ? used : -1);
-                px = sp.x; py = sp.y; pz = sp.z;
-                if (kst) {
-                    const unsigned long long tm1 = cycle_stamp();
-                    if (lane == 0) atomicAdd(&kst[15], tm1 - tm0);
-                }
+    for (int j = blockIdx.x * KNN_WAVES + wave; j < n; j += nw) {
+        const float4 sp = order[j];
+        const int q = (int)__float_as_uint(sp.w);
+        float out = __builtin_nanf("");
+        const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
+        const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
+        if (!origin && fin) {
+            int need = 0, used = 0, tot = 0;
+            const unsigned long long* sorted = nullptr;
+            const int start = hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
+            const bool ok = knn_select(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
+            const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
+            if (!ok) {
+                if (lane == 0) atomicOr(err, 1);
+            } else if (need > 0) {
+                out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
             }
-            if (lane == 0) ratio[q] = out;
-            __builtin_amdgcn_wave_barrier();
+            if (kst) {
+                const unsigned long long tm1 = cycle_stamp();
+                if (lane == 0) atomicAdd(&kst[15], tm1 - tm0);
+            }
         }
+        if (lane == 0) ratio[q] = out;
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -699,16 +678,14 @@ static LadderGrids ladder(const DevGrid* const* g4, int mode) {
 
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst, int max_blocks, int run) {
+                            unsigned long long* kst, int max_blocks) {
     const size_t lds = bsk::knn_lds_bytes();
-    if (run < 1) run = 1;
-    int blocks = ((n + run - 1) / run + KNN_WAVES - 1) / KNN_WAVES;
+    int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     // fewer, longer-lived waves cost less dispatch; more, short-lived ones let high-priority
     // kernels of other streams in sooner
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    blocks = (blocks + 7) & ~7;
     bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type, hint,
-                                                         run, ratio, err, kst);
+                                                         ratio, err, kst);
     return hipGetLastError();
 }
 
