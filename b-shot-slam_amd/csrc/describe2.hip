@@ -30,6 +30,31 @@ __global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restric
     for (int c = cb[q] + threadIdx.x; c < cb[q + 1]; c += 256) owner[c] = q;
 }
 
+// The 7 butterfly sums of wave_tree_sum_d (partners lane ^ 32, ^ 16, ..., ^ 1 in that order), all at
+// once with 10 cross-lane exchanges instead of 42: at the xor-32 level the lanes with bit 5 clear
+// keep terms 0..3 and receive their partners' 0..3 while the others keep 4..6 (+ a zero pad), at xor
+// 16 each keeps two, at xor 8 one, then a plain butterfly over xor 4, 2, 1. Every term still adds
+// the same pairs at every level (x + y == y + x), so each sum has wave_tree_sum_d's bits. Returns
+// term (lane >> 3): lanes 8 j .. 8 j + 7 hold term j's sum.
+__device__ __forceinline__ double wave_tree_sum7(const double* v) {
+    const int lane = lane_id();
+    const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
+    double a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const double lo = v[j], hi = j + 4 < 7 ? v[j + 4] : 0.0;
+        a[j] = (b5 ? hi : lo) + xor_lane_d<32>(b5 ? lo : hi);
+    }
+    double b[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = (b4 ? a[j + 2] : a[j]) + xor_lane_d<16>(b4 ? a[j] : a[j + 2]);
+    double c = (b3 ? b[1] : b[0]) + xor_lane_d<8>(b3 ? b[0] : b[1]);
+    c = c + xor_lane_d<4>(c);
+    c = c + xor_lane_d<2>(c);
+    c = c + xor_lane_d<1>(c);
+    return c;
+}
+
 // csum[8 c + 0..5]: weighted covariance terms, [6]: weight sum, [7]: valid count of chunk c =
 // ranks [64 t, 64 t + 64) of keypoint q (wave; lanes 0..7 store)
 __device__ __forceinline__ void lrf_chunk_terms(const float4* __restrict__ pts4, float kx, float ky, float kz, float R,
@@ -51,16 +76,9 @@ __device__ __forceinline__ void lrf_chunk_terms(const float4* __restrict__ pts4,
             isv = 1;
         }
     }
-#pragma unroll
-    for (int j = 0; j < 7; ++j) v[j] = wave_tree_sum_d(v[j]);
+    const double sum = wave_tree_sum7(v);  // term (lane >> 3)
     const int nv = __popcll(__ballot(isv != 0));
-    if (lane < 8) {
-        double x = (double)nv;
-#pragma unroll
-        for (int j = 0; j < 7; ++j)
-            if (lane == j) x = v[j];
-        out8[lane] = x;
-    }
+    if ((lane & 7) == 0) out8[lane >> 3] = (lane >> 3) < 7 ? sum : (double)nv;
 }
 
 __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ pts4, const float* __restrict__ kps,
