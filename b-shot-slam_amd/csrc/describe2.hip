@@ -5,8 +5,9 @@
 //
 //   (sorting: k_shot_rank, csrc/describe.hip -- exact rank inside the count pass's d2 buckets)
 //   k_lrf_chunks  wave per 64-rank chunk: 7 weighted-covariance terms by the xor-butterfly tree
-//   k_lrf_eig     wave per keypoint: chunk sums in chunk order (a lane per term), Jacobi eigenvectors;
-//                 with normal_radius == shot_radius also the keypoint normal (segment_normal)
+//   k_lrf_eig     two waves per keypoint: chunk sums in chunk order (a lane per term) + Jacobi
+//                 eigenvectors; with normal_radius == shot_radius the other wave writes the keypoint
+//                 normal (segment_normal)
 //   k_hist_fused  workgroup per keypoint: the x/z sign counts and PCL's count + median-5 rule
 //                 (float LRF rows) first,
 //                 then 7 waves compute the <= 5 (bin, value)
@@ -198,15 +199,20 @@ __global__ void __launch_bounds__(64 * LE_WAVES) k_lrf_eig(int k, const int* __r
                                                            const long long* __restrict__ offs,
                                                            const unsigned int* __restrict__ seg, int nmax,
                                                            float4* __restrict__ normals) {
-    __shared__ float fl[LE_WAVES][3 * 512];
+    __shared__ float fl[LE_WAVES / 2][3 * 512];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
-    const int q = blockIdx.x * LE_WAVES + wave;
+    // two waves per keypoint: the odd one computes the normal (nmax > 0), the even one the LRF eigen
+    // system -- two independent sequential chains side by side instead of one after the other
+    const int q = blockIdx.x * (LE_WAVES / 2) + (wave >> 1);
     if (q >= k) return;  // no workgroup barrier below
-    if (nmax > 0) {
-        const long long o = offs[q];
-        const float4 nv = segment_normal(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o, offs[q + 1] - o, nmax,
-                                         fl[wave]);
-        if (lane == 0) normals[q] = nv;
+    if (wave & 1) {
+        if (nmax > 0) {
+            const long long o = offs[q];
+            const float4 nv = segment_normal(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], seg + o, offs[q + 1] - o,
+                                             nmax, fl[wave >> 1]);
+            if (lane == 0) normals[q] = nv;
+        }
+        return;
     }
     const int c0 = cb[q], c1 = cb[q + 1];
     double acc = 0.0;
@@ -650,7 +656,7 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
                                                        A.csum);
         }
         // nmax > 0: the keypoint normals from the sorted segments in the same launch
-        bsk::k_lrf_eig<<<(A.k + LE_WAVES - 1) / LE_WAVES, 64 * LE_WAVES, 0, s>>>(
+        bsk::k_lrf_eig<<<(A.k + LE_WAVES / 2 - 1) / (LE_WAVES / 2), 64 * LE_WAVES, 0, s>>>(
             A.k, A.cb, A.csum, A.eig, A.okf, A.pts4, A.kps, A.offs, A.sorted, A.nseg_max_nn, A.normals_out);
         // the sign counts and PCL's sign rule (k_lrf_sign / k_lrf_fin of round 2) run at the start of
         // the histogram kernel
