@@ -189,11 +189,13 @@ struct bshot_ctx {
     // the exchange queues its replica inserts from a thread of its own (host/xchg.cpp): every host
     // access to the replicas (and the context's teardown) first waits until that thread is idle
     // (detach = 1 at the context's teardown: the exchange forgets it)
-    void (*replica_quiesce)(void* arg, int detach) = nullptr;
+    int (*replica_quiesce)(void* arg, int detach) = nullptr;
     void* replica_quiesce_arg = nullptr;
-    void quiesce_replicas(int detach = 0) {
-        if (replica_quiesce) replica_quiesce(replica_quiesce_arg, detach);
+    // before any access to the replicas: the exchange indexes the offers it has logged (its error code)
+    int quiesce_replicas(int detach = 0) {
+        const int rc = replica_quiesce ? replica_quiesce(replica_quiesce_arg, detach) : 0;
         if (detach) replica_quiesce = nullptr;
+        return rc;
     }
     int opt_xseq_targets = 0;  // 1: the replicas' entries join the matching targets (extension; 0 = reference)
     DBuf<float> gtgt;  // matching targets assembled on the device (float3)
@@ -211,9 +213,11 @@ struct bshot_ctx {
     void hmark(const char* name);
 
     // icp
-    PinBuf<bsh::IcpSync> p_isync;  // ICP host <-> kernel hand-over (coherent)
-    PinBuf<unsigned long long> p_ibest;  // ICP NN keys, two iterations' worth (coherent)
-    PinBuf<int> p_idone;  // ICP per-workgroup completion flags (coherent)
+    PinBuf<bsh::IcpOut> p_iout;  // ICP result: composed transform, iteration count, seq (coherent)
+    int icp_seq = 0;             // seq of the last ICP call
+    DBuf<float4> ipos, ilcen;    // ICP loop: current source positions, list centres (xyz) + radii (w)
+    DBuf<int> iqueue;            // ICP loop: sources queued for the grid search
+    DBuf<float> irec;            // ICP loop: Umeyama terms in HBM when the sources exceed the LDS staging
     DBuf<float4> ilst;  // ICP candidate lists (ICP_LIST_CAP per source)
     DBuf<float> ilsd;   // their entries' distances from the list centre (ascending)
     DBuf<int> ilcnt;    // their counts (-1: none)
@@ -228,7 +232,7 @@ struct bshot_ctx {
     const float* icp_prep_tgt = nullptr;  // device targets whose ICP grids ctx_icp_prepare has queued
     int icp_prep_nt = 0;
     DBuf<float4> itgt;
-    DBuf<unsigned long long> ibest;
+    DBuf<unsigned long long> ibest;  // ICP iteration 0's NN keys
 
     // RANSAC scoring (bshot_ransac_dev): correspondence points, hypotheses, scores
     DBuf<float> rpts;

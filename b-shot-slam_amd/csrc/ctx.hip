@@ -632,6 +632,10 @@ int ctx_icp_prepare(bshot_ctx* c, const float* d_tgt, int nt) {
     return BSHOT_OK;
 }
 
+static long long ns_now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T, int* iters,
             const float* d_tgt) {
     const bool prepared = d_tgt && c->icp_prep_tgt == d_tgt && c->icp_prep_nt == nt;
@@ -659,111 +663,48 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         HIPCHK(c->ilcnt.ensure(ns), "alloc icp list counts");
         HIPCHK(c->ilrad.ensure(ns), "alloc icp list radii");
         const DevGrid* g4[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
-        // PCL's loop on the host (float Umeyama, convergence), the exact 1-NN of every iteration on
-        // the device (csrc/icp.hip): one launch for iteration 0 (keys + every source's candidate
-        // list) and one persistent launch for the rest, handed over through coherent pinned memory:
-        // the host releases iteration j with its step transform, the kernel stores the keys
-        // (double-buffered by iteration parity) and flags them done. One stream sync per ICP call.
-        std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
-        if (max_iter > ICP_MAX_ITER) return c->fail("icp: max_iter > 64", BSHOT_EINVAL);
-        c->p_isync.coherent = true;
-        c->p_ibest.coherent = true;
-        HIPCHK(c->p_isync.ensure(1), "alloc icp sync");
-        HIPCHK(c->p_ibest.ensure(2 * (size_t)ns), "alloc icp keys");
-        const int nb0 = icp_lists_blocks(ns), nb1 = icp_iter_blocks(ns);
-        c->p_idone.coherent = true;
-        HIPCHK(c->p_idone.ensure((size_t)nb0 + nb1), "alloc icp flags");
-        int* done0 = c->p_idone.p;
-        int* done1 = c->p_idone.p + nb0;
-        std::memset(c->p_idone.p, 0, sizeof(int) * ((size_t)nb0 + nb1));
-        // host copy of the targets (the Umeyama step's pairs), before the persistent kernel is queued
-        const float* tg = tgt;
-        std::vector<float> h_tgt;
-        if (!tg) {
-            h_tgt.resize(3 * (size_t)nt);
-            HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
-            HIPCHK(kcopy(c->p_tgt.p, d_tgt, sizeof(float) * 3 * nt, c->stream), "D2H icp targets");
-            HIPCHK(hipStreamSynchronize(c->stream), "sync icp targets");
-            std::memcpy(h_tgt.data(), c->p_tgt.p, sizeof(float) * 3 * nt);
-            tg = h_tgt.data();
-        }
-        IcpSync* sy = c->p_isync.p;
-        std::memset(sy, 0, sizeof(IcpSync));
-        std::atomic_thread_fence(std::memory_order_seq_cst);
+        // PCL's loop on the device (csrc/icp.hip): k_icp_lists finds iteration 0's exact 1-NN and every
+        // source's candidate list, k_icp_loop runs the rest in one workgroup (float Umeyama, the
+        // convergence test, the step, the next keys) and writes the composed transform and the
+        // iteration count to coherent pinned memory, seq last. The host waits once.
+        HIPCHK(c->ibest.ensure(ns), "alloc icp keys");
+        HIPCHK(c->ipos.ensure(ns), "alloc icp positions");
+        HIPCHK(c->ilcen.ensure(ns), "alloc icp list centres");
+        HIPCHK(c->iqueue.ensure(ns), "alloc icp queue");
+        const size_t nrec = icp_loop_rec_floats(ns);
+        if (nrec) HIPCHK(c->irec.ensure(nrec), "alloc icp terms");
+        c->p_iout.coherent = true;
+        HIPCHK(c->p_iout.ensure(1), "alloc icp result");
+        IcpOut* out = c->p_iout.p;
+        const int seq = ++c->icp_seq;
         const float* d_src0 = c->p_src.p;
         const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
         HIPCHK(launch_icp_lists(d_src0, ns, g4, c->itgt.p, nt, ICP_LIST_CAP, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p,
-                                c->p_ibest.p, done0, c->stream),
+                                c->ibest.p, c->stream),
                "icp lists");
-        HIPCHK(launch_icp_iterations(d_src0, ns, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p, ICP_LIST_CAP, g4, c->itgt.p, nt,
-                                     max_iter, sy, done1, c->p_ibest.p, c->stream),
-               "icp iterations");
+        HIPCHK(launch_icp_loop(d_src0, ns, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p, ICP_LIST_CAP, g4, c->itgt.p, nt,
+                               max_iter, c->ibest.p, c->ipos.p, c->ilcen.p, c->iqueue.p, nrec ? c->irec.p : nullptr, out,
+                               seq, c->stream),
+               "icp loop");
         c->stage_end(sg14);
-        auto release = [&](int go) { __atomic_store_n(&sy->go, go, __ATOMIC_RELEASE); };
-        // iteration j's keys are complete when every workgroup's flag says so
-        auto wait_keys = [&](int j) -> bool {
-            const int nb = j == 0 ? nb0 : nb1;
-            int* flags = j == 0 ? done0 : done1;
-            const int want = j == 0 ? 1 : j;
-            const auto t0 = std::chrono::steady_clock::now();
-            unsigned spins = 0;
-            for (int w = 0; w < nb; ++w) {
-                while (__atomic_load_n(&flags[w], __ATOMIC_ACQUIRE) < want) {
-                    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
-                        return false;
-                    __builtin_ia32_pause();
-                }
-            }
-            return true;
-        };
-        double prev_mse = 1.7976931348623157e308;
-        bg::Mat4f Ts = bg::Mat4f::identity();
-        bool timed_out = false;
-        auto ns_now = []() {
-            return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
-                .count();
-        };
-        long long tw = ns_now();
-        while (true) {
-            const long long t_a = ns_now();
-            if (!wait_keys(it)) {
-                timed_out = true;
-                break;
-            }
-            const long long t_b = ns_now();
-            c->work[it == 0 ? 2 : 3] += t_b - t_a;  // host wait for the keys: iteration 0 / later
-            if (it > 0) c->work[4] += t_a - tw;     // host step between two waits
-            const unsigned long long* best = c->p_ibest.p + (size_t)ns * (it & 1);
-            for (int i = 0; i < ns; ++i) {
-                const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);
-                tb[3 * i] = tg[3 * j]; tb[3 * i + 1] = tg[3 * j + 1]; tb[3 * i + 2] = tg[3 * j + 2];
-            }
-            Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
-            ++it;
-            // the next iteration is released before this one's bookkeeping and convergence test (PCL
-            // decides after the step); if the test stops the loop, its keys are never read
-            if (it < max_iter) {
-                std::memcpy(sy->T, Ts.m, sizeof(Ts.m));
-                release(it);
-            }
-            for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);  // the device applies Ts too
-            fin = bg::mul(Ts, fin);
-            if (it >= max_iter) break;
-            const double cos_angle = 0.5 * (double)(((Ts.m[0] + Ts.m[5]) + Ts.m[10]) - 1.0f);
-            const double tsq = (double)((Ts.m[3] * Ts.m[3] + Ts.m[7] * Ts.m[7]) + Ts.m[11] * Ts.m[11]);
-            if (cos_angle >= 1.0 && tsq <= 0.0) break;
-            double mse = 0;
-            for (int i = 0; i < ns; ++i) mse += (double)__builtin_bit_cast(float, (unsigned)(best[i] >> 32));
-            mse /= (double)ns;
-            if (__builtin_fabs(mse - prev_mse) < 1e-12) break;
-            prev_mse = mse;
-            tw = t_b;
+        // spin briefly on seq (the loop takes ~0.1-0.3 ms), then block on the stream: a slow GPU
+        // (contention, a profiler) only makes the call wait longer, it never fails it
+        const long long t_a = ns_now();
+        bool seen = false;
+        for (unsigned spins = 0;; ++spins) {
+            if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) == seq) { seen = true; break; }
+            if ((spins & 255) == 0 && ns_now() - t_a > 5000000ll) break;
+            __builtin_ia32_pause();
         }
+        if (!seen) {
+            HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
+            if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) != seq)
+                return c->fail("icp: the loop kernel finished without its result", BSHOT_EHIP);
+        }
+        c->work[2] += ns_now() - t_a;  // host wait for the device loop
+        std::memcpy(fin.m, out->T, sizeof(fin.m));
+        it = out->iters;
         c->work[5] += it;
-        release(-1);
-  // the persistent kernel's waves exit
-        HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
-        if (timed_out) return c->fail("icp: the device did not deliver the nearest neighbours within 2 s", BSHOT_EHIP);
     }
     std::memcpy(T, fin.m, sizeof(float) * 16);
     *iters = it;
@@ -814,7 +755,7 @@ void bshot_destroy(bshot_ctx* c) {
     if (!c) return;
     const bool trace = std::getenv("BSHOT_TRACE") != nullptr;
     if (trace) std::fprintf(stderr, "destroy enter\n");
-    c->quiesce_replicas(1);  // an exchange's insert thread is done with this context and forgets it
+    c->quiesce_replicas(1);  // the exchange forgets this context (its unindexed offers are dropped)
     (void)hipSetDevice(c->device);
     if (trace) std::fprintf(stderr, "destroy step 0\n");
     (void)hipStreamSynchronize(c->stream);
@@ -853,7 +794,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->prep = nullptr;
     bsh::velo_free(c->velo);
     c->velo = nullptr;
-    c->gidx.release(); c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->ilrad.release(); c->p_isync.release(); c->p_ibest.release(); c->p_idone.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gidx.release(); c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->ilrad.release(); c->p_iout.release(); c->ipos.release(); c->ilcen.release(); c->iqueue.release(); c->irec.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");

@@ -685,7 +685,7 @@ int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax,
 }
 
 int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n) {
-    c->quiesce_replicas();
+    if (int rc = c->quiesce_replicas()) return rc;
     // host records (bshot_odom_map_delta layout: x, y, z, ratio, 11 words) -> a device batch
     GMap& g = replica_map(c, replica);
     int rc = gmap_init(c, g);
@@ -708,12 +708,12 @@ int gmap_settle_replicas_noquiesce(bshot_ctx* c) {
 }
 
 int gmap_settle_replicas(bshot_ctx* c) {
-    c->quiesce_replicas();
+    if (int rc = c->quiesce_replicas()) return rc;
     return gmap_settle_replicas_noquiesce(c);
 }
 
 int gmap_replica_size(bshot_ctx* c, int replica) {
-    c->quiesce_replicas();
+    if (c->quiesce_replicas()) return -1;
     if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
     GMap& g = *c->gmap_replicas[replica];
     // its inserts may run on another stream (the exchange's): wait for the counters' copy itself
@@ -829,7 +829,7 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
 
 int gmap_replica_query(bshot_ctx* c, int replica, const float pos[3], float range, int canonical, float* xyz,
                        unsigned int* bits, int cap) {
-    c->quiesce_replicas();
+    if (int rc = c->quiesce_replicas()) return rc;
     if (replica < 0 || replica >= (int)c->gmap_replicas.size() || !c->gmap_replicas[replica]) return 0;
     GMap& g = *c->gmap_replicas[replica];
     const QueryBox q = query_box(pos, range);

@@ -1,16 +1,16 @@
 // icp.hip -- A11 point-to-point ICP on gfx950 (PCL IterativeClosestPoint defaults,
 // src/lidar_odometry.cpp:291-297: CorrespondenceEstimation::determineCorrespondences, 1-NN, no
-// distance cap; TransformationEstimationSVD; DefaultConvergenceCriteria). The host runs PCL's loop
-// (float Umeyama, convergence test); the GPU finds every iteration's exact 1-NN. Exact: the packed
-// key (float bits of d2 << 32 | target index) min picks the smallest squared distance, smallest
-// index on ties (DESIGN.md convention for FLANN's traversal-dependent tie), independent of the
-// reduction order.
+// distance cap; TransformationEstimationSVD; DefaultConvergenceCriteria). The whole loop runs on the
+// device: the exact 1-NN of every iteration, the float Umeyama step in Eigen's operation order and
+// PCL's convergence test; the host launches two kernels and waits once. Exact: the packed key (float
+// bits of d2 << 32 | target index) min picks the smallest squared distance, smallest index on ties
+// (DESIGN.md convention for FLANN's traversal-dependent tie), independent of the reduction order.
 //
 // Iteration 0 (k_icp_lists, a wave per source): the exact 1-NN at the source's starting position
 // q0, and a candidate list: every target within R of q0, R = d0 + {3000, 1500, 750, 350} mm (the
 // largest whose count fits the list capacity; d0 = the NN distance), sorted by distance from q0.
-// Iterations >= 1 (k_icp_iterations, one persistent launch, a lane per source): the source moves
-// rigidly by the step transform; its NN among the list is the global NN whenever
+// The loop (k_icp_loop, one workgroup): each iteration's Umeyama + convergence test, then the sources
+// move rigidly by the step; a source's NN among its list is the global NN whenever
 // dm + |q - q0| < R (with float slack): a target outside the list lies at least R from q0, so at
 // least R - |q - q0| from q, farther than the list's best. Sources failing the test (moved too far,
 // no list, non-finite) take the exact grid search of iteration 0 (a wave each) and get a new list.
@@ -82,18 +82,6 @@ __device__ __forceinline__ void icp_stream_level(const IcpGrids& G, int L, CandL
     else if (L == 1) for_candidates(G.g[1], cs, qx, qy, qz, rs, rs2, f);
     else if (L == 2) for_candidates(G.g[2], cs, qx, qy, qz, rs, rs2, f);
     else for_candidates(G.g[3], cs, qx, qy, qz, rs, rs2, f);
-}
-
-// Hand-over stores to pinned host memory are system-scope relaxed stores (written through to the
-// host, never held in L2), ordered by waiting for their completion (vmcnt 0, which on gfx9 counts
-// stores) before the flag is written. No release fence: at system scope a fence writes back the
-// XCD's whole L2, tens of us with the lookahead's kernels' dirty lines in it.
-__device__ __forceinline__ void icp_put_key(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void icp_put_flag(int* p, int v) {
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's key stores have completed
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Candidate list of source q (the whole wave) around its exact NN key m: every target within R of
@@ -171,8 +159,7 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
                                                               const float4* __restrict__ tgt4, int nt, int cap,
                                                               float4* __restrict__ lst, float* __restrict__ lsd,
                                                               int* __restrict__ lcnt, float* __restrict__ lrad,
-                                                              unsigned long long* __restrict__ best_out,
-                                                              int* __restrict__ done) {
+                                                              unsigned long long* __restrict__ best_out) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     __shared__ CandLds cl[ICP_WAVES];
     __shared__ unsigned long long skl[ICP_WAVES][ICP_LIST_CAP];
@@ -182,7 +169,7 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
     for (int i = blockIdx.x * ICP_WAVES + wave; i < ns; i += gridDim.x * ICP_WAVES) {
         const float qx = src0[3 * i], qy = src0[3 * i + 1], qz = src0[3 * i + 2];
         const unsigned long long m = icp_wave_nn(G, cs, qx, qy, qz, tgt4, nt);
-        if (lane == 0) icp_put_key(&best_out[i], m);
+        if (lane == 0) best_out[i] = m;
         int count;
         float R;
         icp_build_list(G, cs, qx, qy, qz, m, tgt4, lst + i, lsd + i, ns, cap, skl[wave], &count, &R);  // entry e at [e * ns + i]
@@ -192,141 +179,265 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
         }
         __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_s_waitcnt(0);  // every wave's key stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0) icp_put_flag(&done[blockIdx.x], 1);
 }
 
-// Iterations >= 1, one persistent launch: a workgroup (one wave) per 64 sources, a lane per source
-// holding its position. For iteration j the wave waits until the host has released it (IcpSync.go
-// >= j after the host's Umeyama step of iteration j - 1; -1 = stop), moves its source by the step
-// (pcl::transformPointCloud's float expression, as the host's bg::xform), takes the NN among the
-// source's list when the bound proves it global and queues the others for the grid search (which
-// also rebuilds the source's list around its current position), stores
-// the keys in pinned host memory and sets its flag done[w] = j. No launch, no stream sync per
-// iteration: the host and the waves hand over through coherent host memory (the per-iteration
-// launch + wait cost ~40 us under the lookahead's load, 10 times per sweep). Every wave exits on
-// go = -1, after max_iter - 1 iterations, or when a wait exceeds ICP_WAIT_TICKS (wall clock).
-#define ICPN_THREADS 64
-#define ICP_WAIT_TICKS 100000000ll  // 1 s at the 100 MHz wall clock
-__global__ void __launch_bounds__(ICPN_THREADS) k_icp_iterations(const float* __restrict__ src0, int ns,
-                                                                 const float4* lst, const float* lsd,
-                                                                 const int* __restrict__ lcnt,
-                                                                 const float* __restrict__ lrad, int cap, IcpGrids G,
-                                                                 const float4* __restrict__ tgt4, int nt, int max_iter,
-                                                                 const bsh::IcpSync* sy, int* done,
-                                                                 unsigned long long* best) {
-    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
-    __shared__ CandLds cl;
-    __shared__ float4 q_queue[ICPN_THREADS];
-    __shared__ float4 q_new[ICPN_THREADS];  // rebuilt lists: new centre (xyz) and radius (w)
-    __shared__ int n_new[ICPN_THREADS];     // their counts; -2 = unchanged
-    __shared__ int nq;
-    __shared__ unsigned long long skl[ICP_LIST_CAP];
-    const int lane = lane_id();
-    cand_init(&cl);
-    n_new[lane] = -2;
-    const int i = blockIdx.x * ICPN_THREADS + lane;
-    const bool have = i < ns;
-    float x0 = 0.f, y0 = 0.f, z0 = 0.f;
-    if (have) { x0 = src0[3 * i]; y0 = src0[3 * i + 1]; z0 = src0[3 * i + 2]; }
-    float qx = x0, qy = y0, qz = z0;
-    int n = have ? lcnt[i] : -1;
-    float R = have ? lrad[i] : 0.f;
-    float4* lst_w = const_cast<float4*>(lst);
-    float* lsd_w = const_cast<float*>(lsd);
-    const float4* L = lst + (have ? i : 0);  // entry e at L[e * ns]: the wave's lanes read one 1 KB row
-    const float* Ld = lsd + (have ? i : 0);
-    for (int j = 1; j < max_iter; ++j) {
-        int g = 0;
-        if (lane == 0) {
-            const long long t0 = wall_clock64();
-            while (true) {
-                g = __hip_atomic_load(&sy->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (g < 0 || g >= j) break;
-                if (wall_clock64() - t0 > ICP_WAIT_TICKS) { g = -1; break; }
-                __builtin_amdgcn_s_sleep(2);
+// The whole of PCL's loop after iteration 0's neighbours, on the device (one launch, one workgroup of
+// ICPL_THREADS): per iteration the float Umeyama of (current sources, their NN targets), PCL's
+// convergence test, then every source moved by the step and its exact 1-NN found for the next
+// iteration. One workgroup keeps every hand-over inside one CU (LDS + __syncthreads): no host round
+// trip, no grid barrier, no cross-XCD coherence traffic, and nothing waits for another workgroup to
+// be scheduled.
+//
+// Umeyama (bm::umeyama_seq<float>, Eigen::umeyama's order): the means are 6 sequential float sums in
+// source order, the cross-covariance 9 sequential sums of (d_r - dm_r)(s_c - sm_c), each sum on its
+// own lane of wave 0 (the sums' own orders are the host's, so the bits are); the per-source terms
+// are staged in LDS as 7 arrays (s xyz, d xyz, d2), centred in place by the whole workgroup between
+// the two passes. PCL's MSE (a sequential double sum of the keys' d2) runs on wave 1 meanwhile.
+// Sources beyond ICPL_CH are staged chunk by chunk from HBM (rec_g) instead.
+//
+// Neighbours: a thread per source scans the source's candidate list (k_icp_lists) while the bound
+// proves the list's best global (dm + |q - q0| < R with float slack); the others are queued and the
+// exact grid search runs on ICPL_SW waves (a wave per queued source), which also rebuilds the
+// source's list around its current position.
+#define ICPL_THREADS 512
+#define ICPL_SW 8      // waves that run the queued grid searches
+#define ICPL_CH 2048   // sources whose Umeyama terms are staged in LDS at once (7 floats each)
+
+__global__ void __launch_bounds__(ICPL_THREADS) k_icp_loop(const float* __restrict__ src0, int ns, float4* lst, float* lsd,
+                                                           int* lcnt, float* lrad, int cap, IcpGrids G,
+                                                           const float4* __restrict__ tgt4, int nt, int max_iter,
+                                                           const unsigned long long* __restrict__ best0,
+                                                           float4* __restrict__ pos, float4* __restrict__ lcen,
+                                                           int* __restrict__ queue, float* __restrict__ rec_g,
+                                                           bsh::IcpOut* out, int seq) {
+    extern __shared__ __attribute__((aligned(16))) float rec[];  // 7 x chs floats
+    __shared__ CandLds cl[ICPL_SW];
+    __shared__ unsigned long long skl[ICPL_SW][ICP_LIST_CAP];
+    __shared__ float sT[16];
+    __shared__ float smean[6];
+    __shared__ float sacc[9];
+    __shared__ double smse;
+    __shared__ int sstop, nq;
+    const int tid = threadIdx.x, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool big = ns > ICPL_CH;
+    const int chs = big ? ICPL_CH : ((ns + 3) & ~3);  // LDS row stride (16-B aligned rows)
+    if (wave < ICPL_SW) cand_init(&cl[wave]);
+    // record c of source i: LDS row c (small) or HBM row c (big: staged per chunk)
+    auto put = [&](int c, int i, float v) {
+        if (big) rec_g[(size_t)c * ns + i] = v;
+        else rec[c * chs + i] = v;
+    };
+    // iteration 0: the sources as given, the keys of k_icp_lists
+    for (int i = tid; i < ns; i += ICPL_THREADS) {
+        const float x = src0[3 * i], y = src0[3 * i + 1], z = src0[3 * i + 2];
+        pos[i] = make_float4(x, y, z, 0.f);
+        lcen[i] = make_float4(x, y, z, lrad[i]);
+        const unsigned long long m = best0[i];
+        const float4 t = tgt4[(unsigned)(m & 0xFFFFFFFFu)];
+        put(0, i, x); put(1, i, y); put(2, i, z);
+        put(3, i, t.x); put(4, i, t.y); put(5, i, t.z);
+        put(6, i, __uint_as_float((unsigned)(m >> 32)));
+    }
+    // thread 0's loop state: the composed transform (LDS), the previous MSE
+    __shared__ float fin[16];
+    if (tid < 16) fin[tid] = (tid % 5 == 0) ? 1.f : 0.f;
+    double prev_mse = 1.7976931348623157e308;
+    const float one_over_n = 1.f / (float)ns;
+    int it = 0;
+    __syncthreads();
+    while (true) {
+        // ---- means: lanes 0..5 of wave 0, source order (the first element starts the sum)
+        float acc = 0.f;
+        for (int c0 = 0; c0 < ns; c0 += chs) {
+            const int cn = ns - c0 < chs ? ns - c0 : chs;
+            if (big) {
+                __syncthreads();
+                for (int t = tid; t < 7 * cn; t += ICPL_THREADS) {
+                    const int c = t / cn, k = t - c * cn;
+                    rec[c * chs + k] = rec_g[(size_t)c * ns + c0 + k];
+                }
+                __syncthreads();
+            }
+            if (wave == 0 && lane < 6) {
+                const float* a = rec + lane * chs;
+                int k = 0;
+                if (c0 == 0) { acc = a[0]; k = 1; }
+                for (; k < cn && (k & 3); ++k) acc = acc + a[k];
+                for (; k + 4 <= cn; k += 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(a + k);
+                    acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
+                }
+                for (; k < cn; ++k) acc = acc + a[k];
             }
         }
-        g = __shfl(g, 0, 64);
-        if (g < 0) break;
-        float Tl = lane < 16 ? __hip_atomic_load(&sy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0.f;
+        if (wave == 0 && lane < 6) smean[lane] = acc * one_over_n;
+        __syncthreads();
+        // ---- cross-covariance (wave 0, lane r * 3 + c) and PCL's MSE (wave 1, lane 0)
+        const float sm0 = smean[0], sm1 = smean[1], sm2 = smean[2], dm0 = smean[3], dm1 = smean[4], dm2 = smean[5];
+        float cov = 0.f;
+        double mse = 0.0;
+        for (int c0 = 0; c0 < ns; c0 += chs) {
+            const int cn = ns - c0 < chs ? ns - c0 : chs;
+            if (big) {
+                __syncthreads();
+                for (int t = tid; t < 7 * cn; t += ICPL_THREADS) {
+                    const int c = t / cn, k = t - c * cn;
+                    rec[c * chs + k] = rec_g[(size_t)c * ns + c0 + k];
+                }
+                __syncthreads();
+            }
+            // centre in place: s - sm, d - dm (the host's s0..s2, d0..d2)
+            for (int t = tid; t < 6 * cn; t += ICPL_THREADS) {
+                const int c = t / cn, k = t - c * cn;
+                const float m = c == 0 ? sm0 : c == 1 ? sm1 : c == 2 ? sm2 : c == 3 ? dm0 : c == 4 ? dm1 : dm2;
+                rec[c * chs + k] = rec[c * chs + k] - m;
+            }
+            __syncthreads();
+            if (wave == 0 && lane < 9) {
+                const float* e = rec + (3 + lane / 3) * chs;  // d_r - dm_r
+                const float* f = rec + (lane % 3) * chs;      // s_c - sm_c
+                int k = 0;
+                if (c0 == 0) { cov = e[0] * f[0]; k = 1; }
+                for (; k < cn && (k & 3); ++k) cov = cov + e[k] * f[k];
+                for (; k + 4 <= cn; k += 4) {
+                    const float4 u = *reinterpret_cast<const float4*>(e + k);
+                    const float4 v = *reinterpret_cast<const float4*>(f + k);
+                    const float p0 = u.x * v.x, p1 = u.y * v.y, p2 = u.z * v.z, p3 = u.w * v.w;
+                    cov = cov + p0; cov = cov + p1; cov = cov + p2; cov = cov + p3;
+                }
+                for (; k < cn; ++k) cov = cov + e[k] * f[k];
+            } else if (wave == 1 && lane == 0) {
+                const float* d2 = rec + 6 * chs;
+                int k = 0;
+                for (; k < cn && (k & 3); ++k) mse += (double)d2[k];
+                for (; k + 4 <= cn; k += 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(d2 + k);
+                    mse += (double)v.x; mse += (double)v.y; mse += (double)v.z; mse += (double)v.w;
+                }
+                for (; k < cn; ++k) mse += (double)d2[k];
+            }
+        }
+        if (wave == 0 && lane < 9) sacc[lane] = cov;
+        if (wave == 1 && lane == 0) smse = mse;
+        __syncthreads();
+        // ---- the step, PCL's convergence test (the host loop's order: the step is applied and
+        // composed first, then max_iter, the transformation epsilon and the MSE epsilon)
+        if (tid == 0) {
+            float sigma[9], sm[3] = {sm0, sm1, sm2}, dm[3] = {dm0, dm1, dm2}, o[16];
+#pragma unroll
+            for (int u = 0; u < 9; ++u) sigma[u] = sacc[u] * one_over_n;
+            bm::umeyama_finish<float>(sigma, sm, dm, o);
+            float f2[16];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    f2[r * 4 + c] = ((o[r * 4] * fin[c] + o[r * 4 + 1] * fin[4 + c]) + o[r * 4 + 2] * fin[8 + c]) +
+                                    o[r * 4 + 3] * fin[12 + c];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) { fin[u] = f2[u]; sT[u] = o[u]; }
+            ++it;
+            int stop = it >= max_iter;
+            if (!stop) {
+                const double cos_angle = 0.5 * (double)(((o[0] + o[5]) + o[10]) - 1.0f);
+                const double tsq = (double)((o[3] * o[3] + o[7] * o[7]) + o[11] * o[11]);
+                if (cos_angle >= 1.0 && tsq <= 0.0) stop = 1;
+            }
+            if (!stop) {
+                const double m = smse / (double)ns;
+                if (__builtin_fabs(m - prev_mse) < 1e-12) stop = 1;
+                prev_mse = m;
+            }
+            sstop = stop;
+            nq = 0;
+        }
+        __syncthreads();
+        if (sstop) break;  // (it, fin and prev_mse live in thread 0)
         float T[12];
 #pragma unroll
-        for (int u = 0; u < 12; ++u) T[u] = __shfl(Tl, u, 64);
-        if (lane == 0) nq = 0;
-        __builtin_amdgcn_wave_barrier();
-        if (have) {
-            const float x = qx, y = qy, z = qz;
-            qx = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
-            qy = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
-            qz = ((T[8] * x + T[9] * y) + T[10] * z) + T[11];
+        for (int u = 0; u < 12; ++u) T[u] = sT[u];
+        // ---- every source moved by the step (pcl::transformPointCloud's float expression, as the
+        // host's bg::xform), its NN from its list when the bound proves it global, else queued
+        for (int i = tid; i < ns; i += ICPL_THREADS) {
+            const float4 p = pos[i];
+            const float qx = ((T[0] * p.x + T[1] * p.y) + T[2] * p.z) + T[3];
+            const float qy = ((T[4] * p.x + T[5] * p.y) + T[6] * p.z) + T[7];
+            const float qz = ((T[8] * p.x + T[9] * p.y) + T[10] * p.z) + T[11];
+            pos[i] = make_float4(qx, qy, qz, 0.f);
+            const float4 c0 = lcen[i];
+            const int n = lcnt[i];
+            const float R = c0.w;
             bool ok = false;
             unsigned long long m = ~0ull;
+            float4 best = make_float4(0.f, 0.f, 0.f, 0.f);
             if (n >= 0 && __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz)) {
-                // entries in ascending distance from the list's centre q0: an entry e with
-                // |e - q0| - |q - q0| beyond the best distance so far (with float slack) lies farther
-                // from q than the best, and so do all later ones -- the scan stops there
-                const double ex = (double)qx - (double)x0, ey = (double)qy - (double)y0, ez = (double)qz - (double)z0;
+                const float4* L = lst + i;  // entry e at L[e * ns]
+                const float* Ld = lsd + i;
+                const double ex = (double)qx - (double)c0.x, ey = (double)qy - (double)c0.y, ez = (double)qz - (double)c0.z;
                 const double delta = sqrt(ex * ex + ey * ey + ez * ez);
-                double stop = 1e300;
+                double stopd = 1e300;
                 for (int k = 0; k < n; k += 4) {
-                    float4 p[4];
+                    float4 pp[4];
                     float dd[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int e = k + u < n ? k + u : n - 1;
-                        p[u] = L[(size_t)e * ns];
+                        pp[u] = L[(size_t)e * ns];
                         dd[u] = Ld[(size_t)e * ns];
                     }
-                    if ((double)dd[0] - delta > stop) break;
+                    if ((double)dd[0] - delta > stopd) break;
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         if (k + u < n) {
-                            const float d2 = d2_flann(qx, qy, qz, p[u].x, p[u].y, p[u].z);
-                            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | __float_as_uint(p[u].w);
-                            m = key < m ? key : m;
+                            const float d2 = d2_flann(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z);
+                            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | __float_as_uint(pp[u].w);
+                            if (key < m) { m = key; best = pp[u]; }
                         }
                     }
-                    stop = sqrt((double)__uint_as_float((unsigned)(m >> 32))) * (1.0 + 1e-5) + 1.0;
+                    stopd = sqrt((double)__uint_as_float((unsigned)(m >> 32))) * (1.0 + 1e-5) + 1.0;
                 }
                 if (m != ~0ull) {
-                    // |q - q0| + (the list best's distance) < R with slack for float rounding: relative
-                    // 1e-5 on the distances, 1 mm absolute gap between the best and any outside target
                     const double dm = sqrt((double)__uint_as_float((unsigned)(m >> 32)));
                     ok = dm * (1.0 + 1e-5) + delta + 1.0 < (double)R * (1.0 - 1e-5);
                 }
             }
-            if (ok) icp_put_key(&best[(size_t)(j & 1) * ns + i], m);
-            else q_queue[atomicAdd(&nq, 1)] = make_float4(qx, qy, qz, __int_as_float(i));
+            put(0, i, qx); put(1, i, qy); put(2, i, qz);
+            if (ok) {
+                put(3, i, best.x); put(4, i, best.y); put(5, i, best.z);
+                put(6, i, __uint_as_float((unsigned)(m >> 32)));
+            } else {
+                queue[atomicAdd(&nq, 1)] = i;
+            }
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        // ---- the queued sources: exact grid search + a new list around the current position
         const int nqueued = nq;
-        for (int t = 0; t < nqueued; ++t) {
-            // the exact grid search, then a new list around the current position (its owner lane
-            // takes over the new centre, count and radius below), so a source that outgrew its list
-            // pays the search once
-            const float4 q = q_queue[t];
-            const int qi = __float_as_int(q.w);
-            const unsigned long long m = icp_wave_nn(G, &cl, q.x, q.y, q.z, tgt4, nt);
-            if (lane == 0) icp_put_key(&best[(size_t)(j & 1) * ns + qi], m);
-            int cnt2;
-            float R2;
-            icp_build_list(G, &cl, q.x, q.y, q.z, m, tgt4, lst_w + qi, lsd_w + qi, ns, cap, skl, &cnt2, &R2);
-            if (lane == 0) { q_new[qi - (int)blockIdx.x * ICPN_THREADS] = make_float4(q.x, q.y, q.z, R2); n_new[qi - (int)blockIdx.x * ICPN_THREADS] = cnt2; }
+        if (wave < ICPL_SW) {
+            for (int t = wave; t < nqueued; t += ICPL_SW) {
+                const int qi = queue[t];
+                const float4 q = pos[qi];
+                const unsigned long long m = icp_wave_nn(G, &cl[wave], q.x, q.y, q.z, tgt4, nt);
+                int cnt2;
+                float R2;
+                icp_build_list(G, &cl[wave], q.x, q.y, q.z, m, tgt4, lst + qi, lsd + qi, ns, cap, skl[wave], &cnt2, &R2);
+                if (lane == 0) {
+                    const float4 tp = tgt4[(unsigned)(m & 0xFFFFFFFFu)];
+                    put(3, qi, tp.x); put(4, qi, tp.y); put(5, qi, tp.z);
+                    put(6, qi, __uint_as_float((unsigned)(m >> 32)));
+                    lcnt[qi] = cnt2;
+                    lcen[qi] = make_float4(q.x, q.y, q.z, R2);
+                }
+            }
         }
-        // the rebuilt lists (stored by this wave) are read by their owner lanes from the next iteration on
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        if (have && n_new[lane] != -2) {
-            const float4 c = q_new[lane];
-            x0 = c.x; y0 = c.y; z0 = c.z; R = c.w;
-            n = n_new[lane];
-            n_new[lane] = -2;
-        }
-        __builtin_amdgcn_wave_barrier();
-        icp_put_flag(&done[blockIdx.x], j);
+        __syncthreads();
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) __hip_atomic_store(&out->T[u], fin[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&out->iters, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_waitcnt(0);  // T and the count have reached host memory before the flag
+        __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -366,26 +477,28 @@ static bsk::IcpGrids icp_views(const DevGrid* const* g4) {
 }
 
 int icp_lists_blocks(int ns) { return (ns + ICP_WAVES - 1) / ICP_WAVES; }
-int icp_iter_blocks(int ns) { return (ns + ICPN_THREADS - 1) / ICPN_THREADS; }
 
 hipError_t launch_icp_lists(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
-                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, int* done,
-                            hipStream_t s) {
+                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, hipStream_t s) {
     if (ns <= 0 || nt <= 0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
     bsk::k_icp_lists<<<icp_lists_blocks(ns), 64 * ICP_WAVES, 0, s>>>(src0, ns, icp_views(g4), tgt4, nt, cap, lst, lsd, lcnt,
-                                                                     lrad, best_out, done);
+                                                                     lrad, best_out);
     return hipGetLastError();
 }
 
-hipError_t launch_icp_iterations(const float* src0, int ns, const float4* lst, const float* lsd, const int* lcnt,
-                                 const float* lrad, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
-                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s) {
-    if (ns <= 0 || nt <= 0 || max_iter <= 1) return hipSuccess;
+size_t icp_loop_rec_floats(int ns) { return ns > ICPL_CH ? (size_t)7 * ns : 0; }
+
+hipError_t launch_icp_loop(const float* src0, int ns, float4* lst, float* lsd, int* lcnt, float* lrad, int cap,
+                           const DevGrid* const* g4, const float4* tgt4, int nt, int max_iter,
+                           const unsigned long long* best0, float4* pos, float4* lcen, int* queue, float* rec_g,
+                           IcpOut* out, int seq, hipStream_t s) {
+    if (ns <= 0 || nt <= 0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
-    if (max_iter > ICP_MAX_ITER) return hipErrorInvalidValue;
-    bsk::k_icp_iterations<<<icp_iter_blocks(ns), ICPN_THREADS, 0, s>>>(src0, ns, lst, lsd, lcnt, lrad, cap, icp_views(g4), tgt4,
-                                                                      nt, max_iter, sy, done, best);
+    const int chs = ns > ICPL_CH ? ICPL_CH : ((ns + 3) & ~3);
+    const size_t lds = sizeof(float) * 7 * (size_t)chs;
+    bsk::k_icp_loop<<<1, ICPL_THREADS, lds, s>>>(src0, ns, lst, lsd, lcnt, lrad, cap, icp_views(g4), tgt4, nt, max_iter, best0,
+                                                 pos, lcen, queue, rec_g, out, seq);
     return hipGetLastError();
 }
 

@@ -51,28 +51,28 @@ hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, 
 // count (-1: none) and radius. Iteration >= 1: the sources moved by T16 (src_in -> src_out) and
 // their exact 1-NN keys; keys (d2 bits << 32 | index) land in best_out (pinned host memory).
 #define ICP_LIST_CAP 128
-#define ICP_MAX_ITER 64
-// host <-> device hand-over of one ICP call (coherent pinned host memory, csrc/icp.hip): the host
-// releases iteration j (step transform T, then go = j; go = -1 stops the kernel). Every workgroup
-// writes its own completion flag once its keys are stored (no atomics, no cache write-back).
-struct IcpSync {
-    int go;
-    int pad0[31];
+// the result of one ICP call (coherent pinned host memory): the composed transform, the iteration
+// count, then seq (written last, after the others have reached host memory)
+struct IcpOut {
     float T[16];
+    int iters;
+    int seq;
+    int pad[14];
 };
-// iteration 0 (one launch, a wave per source): keys of src0 into best_out (pinned), the candidate
-// lists; workgroup w sets done[w] = 1. Returns its workgroup count.
+// iteration 0 (one launch, a wave per source): the exact 1-NN keys of src0 into best_out (HBM) and
+// every source's candidate list
 int icp_lists_blocks(int ns);
 hipError_t launch_icp_lists(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
-                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, int* done,
-                            hipStream_t s);
-// iterations 1 .. max_iter - 1 (one persistent launch, a lane per source): each waits for the host's
-// release of the iteration (or go = -1), moves its source by T, stores the exact 1-NN key in
-// best[(j & 1) * ns + i] (pinned) and sets done[w] = j.
-int icp_iter_blocks(int ns);
-hipError_t launch_icp_iterations(const float* src0, int ns, const float4* lst, const float* lsd, const int* lcnt,
-                                 const float* lrad, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
-                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s);
+                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, hipStream_t s);
+// PCL's loop from iteration 0's keys on (one launch, one workgroup, csrc/icp.hip k_icp_loop): per
+// iteration the float Umeyama, the convergence test, the step and the next keys; the composed
+// transform and the iteration count land in *out, seq last. Scratch (HBM): pos, lcen (ns float4 each),
+// queue (ns ints), rec_g (icp_loop_rec_floats(ns) floats: 0 unless ns exceeds the LDS staging).
+size_t icp_loop_rec_floats(int ns);
+hipError_t launch_icp_loop(const float* src0, int ns, float4* lst, float* lsd, int* lcnt, float* lrad, int cap,
+                           const DevGrid* const* g4, const float4* tgt4, int nt, int max_iter,
+                           const unsigned long long* best0, float4* pos, float4* lcen, int* queue, float* rec_g,
+                           IcpOut* out, int seq, hipStream_t s);
 // load-balanced SHOT (describe2.hip): in-bucket rank, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;

@@ -157,25 +157,40 @@ __device__ __forceinline__ void rank_in_place(KnnLds* L, int tot, float sc0) {
     __builtin_amdgcn_wave_barrier();
 }
 
+// level-0 d2 histogram of list[0, total): every in-radius key of the delivering ladder step. Built
+// after the step instead of per streamed chunk, so steps that fall short cost no LDS atomics.
+__device__ __forceinline__ void hist_of_list(KnnLds* L, int total, float sc0) {
+    const int lane = lane_id();
+    hist_clear(L);
+    for (int i = lane; i < total; i += 64)
+        atomicAdd(&L->hist[bucket_of(__uint_as_float((unsigned)(L->list[i] >> 32)), 0.f, sc0)], 1u);
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool DIAG>
 __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
                            int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
                            unsigned long long ts1, const unsigned long long** sorted);
 
 // Exact selection: leaves the `*need` nearest (d2, idx) sorted in (*sorted)[0, *need).
 // Returns false when > KNN_CAP keys tie at the boundary after 3 refinement levels (reported).
-// kst (nullable): diagnostic work counters, see bshot_debug_knn_stats()
+// DIAG: the instantiation behind bshot_debug_knn_stats() accumulates work counters into kst; the
+// product instantiation has no counters, cycle stamps or chunk tallies at all (they cost registers
+// and, at one query per wave, spill stores in every wave's prologue).
 //
 // Fast path: the ladder step that first holds >= max_nn points also stored every in-radius key
-// in LDS (ballot compaction while histogramming), so when they fit (<= KNN_CAP) the selection is
-// a counting sort over LDS only -- no second pass over the candidates.
+// in LDS (ballot compaction), so when they fit (<= KNN_CAP) the selection is a histogram of that
+// list plus a counting sort over LDS only -- no second pass over the candidates.
 // start_step: first ladder step tried (any step is exact; a later start only costs work);
 // *step_out: the step whose radius delivered the result; *total_out: in-radius count there.
+template <bool DIAG>
 __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
                            int start_step, int* need_out, int* step_out, int* total_out, unsigned long long* kst,
                            const unsigned long long** sorted) {
     unsigned long long chunks = 0, chunks_before = 0;
     const int lane = lane_id();
-    const unsigned long long ts0 = kst ? cycle_stamp() : 0ull;
+    unsigned long long ts0 = 0ull;
+    if constexpr (DIAG) ts0 = cycle_stamp();
     const float r2 = (float)((double)r * (double)r);
     float rs = r, rs2 = r2;
     int total = 0;
@@ -185,13 +200,10 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
     for (; step <= last; ++step) {
         rs = step == last ? r : r * lg.frac[step];
         rs2 = step == last ? r2 : (float)((double)rs * (double)rs);
-        hist_clear(L);
-        const float sc = (float)KNN_NB / rs2;
         int cnt = 0;
         // a step whose cube holds fewer than max_nn candidates cannot deliver: skipped unstreamed
         const bool went = for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
-            ++chunks;
-            if (v) atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
+            if constexpr (DIAG) ++chunks;
             const unsigned long long m = __ballot(v);
             if (v) {
                 const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
@@ -201,32 +213,40 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
             cnt += __popcll(m);
         }, step == last ? 0 : max_nn);
         __builtin_amdgcn_wave_barrier();
-        if (!went && kst && lane == 0) atomicAdd(&kst[6], 1ull);
         total = cnt;
-        if (total >= max_nn) break;
-        if (went && step < last && kst && lane == 0) {
-            atomicAdd(&kst[25], 1ull);
-            atomicAdd(&kst[26], chunks - chunks_before);
+        if constexpr (DIAG) {
+            if (!went && lane == 0) atomicAdd(&kst[6], 1ull);
         }
-        chunks_before = chunks;
+        if (total >= max_nn) break;
+        if constexpr (DIAG) {
+            if (went && step < last && lane == 0) {
+                atomicAdd(&kst[25], 1ull);
+                atomicAdd(&kst[26], chunks - chunks_before);
+            }
+            chunks_before = chunks;
+        }
     }
     if (step > last) step = last;
     *step_out = step;
     *total_out = total;
-    const unsigned long long ts1 = kst ? cycle_stamp() : 0ull;
-    if (kst && lane == 0) {
-        atomicAdd(&kst[12], ts1 - ts0);
-        atomicAdd(&kst[0], 1ull);
-        atomicAdd(&kst[16 + step], 1ull);
-        atomicAdd(&kst[9], (unsigned long long)(total < max_nn ? total : max_nn));
-        atomicAdd(&kst[10], (unsigned long long)total);
+    unsigned long long ts1 = 0ull;
+    if constexpr (DIAG) {
+        ts1 = cycle_stamp();
+        if (lane == 0) {
+            atomicAdd(&kst[12], ts1 - ts0);
+            atomicAdd(&kst[0], 1ull);
+            atomicAdd(&kst[16 + step], 1ull);
+            atomicAdd(&kst[9], (unsigned long long)(total < max_nn ? total : max_nn));
+            atomicAdd(&kst[10], (unsigned long long)total);
+        }
     }
-    return knn_finish(lg, L, qx, qy, qz, r, max_nn, step, total, need_out, kst, chunks, ts1, sorted);
+    return knn_finish<DIAG>(lg, L, qx, qy, qz, r, max_nn, step, total, need_out, kst, chunks, ts1, sorted);
 }
 
 // The selection once a ladder step has delivered (>= max_nn keys in radius, or the last step):
-// L->hist holds that step's level-0 d2 histogram over [0, rs^2) and L->list its first KNN_CAP
-// in-radius keys, in any candidate order (the result does not depend on it).
+// L->list holds that step's first KNN_CAP in-radius keys, in any candidate order (the result does
+// not depend on it).
+template <bool DIAG>
 __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
                            int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
                            unsigned long long ts1, const unsigned long long** sorted) {
@@ -240,9 +260,12 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
     *need_out = need;
     if (need == 0) return true;
     const float sc0 = (float)KNN_NB / rs2;
+    bool hist0 = false;  // L->hist holds the level-0 histogram of the whole ball
 
     // ---- fast path: every in-radius key is in L->list
     if (total <= KNN_CAP) {
+        hist_of_list(L, total, sc0);
+        hist0 = true;
         int Bmax = KNN_NB - 1;
         if (total > need) {
             int below;
@@ -268,7 +291,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
             __builtin_amdgcn_wave_barrier();
             rank_in_place(L, tot, sc0);
             *sorted = L->list;
-            if (kst) {
+            if constexpr (DIAG) {
                 const unsigned long long ts2 = cycle_stamp();
                 if (lane == 0) { atomicAdd(&kst[5], chunks); atomicAdd(&kst[13], ts2 - ts1); }
             }
@@ -276,29 +299,34 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
         }
         // a boundary bucket too crowded for the in-place counting sort: refine by streaming (rare)
     }
-    if (kst && lane == 0) atomicAdd(&kst[11], 1ull);
+    if constexpr (DIAG) {
+        if (lane == 0) atomicAdd(&kst[11], 1ull);
+    }
 
-    // ---- streaming path: > KNN_CAP keys in radius, or a crowded boundary bucket
+    // ---- streaming path: > KNN_CAP keys in radius, or a crowded boundary bucket (total > need
+    // here: the prefix of a ball with total <= need <= KNN_PRE always fits the counting sort).
+    // Rare, so its passes stream 2 chunks at a time: fewer live registers, no spills.
     int B[3] = {KNN_NB, KNN_NB, KNN_NB};
     float lo[3] = {0.f, 0.f, 0.f}, sc[3] = {sc0, 0.f, 0.f};
     int levels = 0;
-    if (total > need) {
-        // the level-0 histogram of the final ladder step is intact here: prefix_offsets only
-        // rewrites it when the prefix fits the counting sort
+    {
         int below_acc = 0;
         float w = rs2;
+#pragma unroll
         for (int lev = 0; lev < 3; ++lev) {
-            if (lev > 0) {
+            if (lev > 0 || !hist0) {
                 hist_clear(L);
-                const int lv = lev;
-                if (kst && lane == 0) atomicAdd(&kst[7], 1ull);
-                for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
-                    ++chunks;
+                if constexpr (DIAG) {
+                    if (lev > 0 && lane == 0) atomicAdd(&kst[7], 1ull);
+                }
+                for_candidates<2>(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+                    if constexpr (DIAG) ++chunks;
                     if (!v) return;
                     int b = bucket_of(d2, lo[0], sc[0]);
+                    if (lev == 0) { atomicAdd(&L->hist[b], 1u); return; }
                     if (b != B[0]) return;
                     b = bucket_of(d2, lo[1], sc[1]);
-                    if (lv == 1) { atomicAdd(&L->hist[b], 1u); return; }
+                    if (lev == 1) { atomicAdd(&L->hist[b], 1u); return; }
                     if (b != B[1]) return;
                     atomicAdd(&L->hist[bucket_of(d2, lo[2], sc[2])], 1u);
                 });
@@ -326,8 +354,8 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
         const int Bmax = lv >= 1 ? B[0] : KNN_NB - 1;
         const int tot = prefix_offsets(L, Bmax);
         if (tot <= KNN_PRE) {
-            for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
-                ++chunks;
+            for_candidates<2>(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+                if constexpr (DIAG) ++chunks;
                 if (v) {
                     const int b = bucket_of(d2, 0.f, sc0);
                     if (b <= Bmax) L->list[atomicAdd(&L->hist[b], 1u)] = knn_key(d2, idx);
@@ -336,7 +364,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
             __builtin_amdgcn_wave_barrier();
             rank_in_place(L, tot, sc0);
             *sorted = L->list;
-            if (kst) {
+            if constexpr (DIAG) {
                 const unsigned long long ts2 = cycle_stamp();
                 if (lane == 0) { atomicAdd(&kst[5], chunks); atomicAdd(&kst[14], ts2 - ts1); }
             }
@@ -345,8 +373,8 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
     }
     // general path: collect the (refined) prefix and bitonic-sort it
     int cnt = 0;
-    for_candidates(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
-        ++chunks;
+    for_candidates<2>(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        if constexpr (DIAG) ++chunks;
         bool take = v;
         if (take && lv > 0) {
             const int b0 = bucket_of(d2, lo[0], sc[0]);
@@ -370,7 +398,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
     if (cnt > KNN_CAP) return false;
     int P = 64;
     while (P < cnt) P <<= 1;
-    if (kst) {
+    if constexpr (DIAG) {
         const unsigned long long ts2 = cycle_stamp();
         if (lane == 0) {
             atomicAdd(&kst[5], chunks);
@@ -546,6 +574,9 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
 // (runs of several cell-order queries per wave, each starting its ladder at its predecessor's
 // step, streamed 11-18 % fewer candidates but were slower in the pipeline,
 // profiles/r03_ab_sr_order_runs.txt).
+// DIAG (bshot_debug_knn_stats only): kst work counters and cycle stamps; the product launch is the
+// DIAG = false instantiation, which has none.
+template <bool DIAG>
 __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
                                                               float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
@@ -568,14 +599,15 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
             int need = 0, used = 0, tot = 0;
             const unsigned long long* sorted = nullptr;
             const int start = hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
-            const bool ok = knn_select(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
-            const unsigned long long tm0 = kst ? cycle_stamp() : 0ull;
+            const bool ok = knn_select<DIAG>(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
+            unsigned long long tm0 = 0ull;
+            if constexpr (DIAG) tm0 = cycle_stamp();
             if (!ok) {
                 if (lane == 0) atomicOr(err, 1);
             } else if (need > 0) {
                 out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
             }
-            if (kst) {
+            if constexpr (DIAG) {
                 const unsigned long long tm1 = cycle_stamp();
                 if (lane == 0) atomicAdd(&kst[15], tm1 - tm0);
             }
@@ -603,7 +635,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(LadderGrids lg, cons
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
             int need = 0, used = 0, tot = 0;
             const unsigned long long* sorted = nullptr;
-            if (!knn_select(lg, L, kx, ky, kz, radius, max_nn, 0, &need, &used, &tot, nullptr, &sorted)) {
+            if (!knn_select<false>(lg, L, kx, ky, kz, radius, max_nn, 0, &need, &used, &tot, nullptr, &sorted)) {
                 if (lane == 0) atomicOr(err, 2);
             } else if (need > 0) {
                 if (need >= 3) {
@@ -684,8 +716,12 @@ hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const flo
     // fewer, longer-lived waves cost less dispatch; more, short-lived ones let high-priority
     // kernels of other streams in sooner
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    bsk::k_seg_ratio<<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type, hint,
-                                                         ratio, err, kst);
+    if (kst)
+        bsk::k_seg_ratio<true><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
+                                                                   hint, ratio, err, kst);
+    else
+        bsk::k_seg_ratio<false><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
+                                                                    hint, ratio, err, nullptr);
     return hipGetLastError();
 }
 

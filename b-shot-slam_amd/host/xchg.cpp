@@ -6,15 +6,16 @@
 // library has no link-time dependency on it and shares the copy PyTorch has already loaded.
 #include <dlfcn.h>
 
-#include <condition_variable>
-#include <mutex>
-#include <thread>
-
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../csrc/ctx.h"
 #include "../csrc/gmap.h"
+#include "../csrc/kernels.h"
 #include "../../include/bshot/lidar_odometry.h"
 #include "../../include/bshot_abi.h"
 
@@ -66,74 +67,65 @@ struct bshot_xchg {
     int nranks = 0, rank = 0, device = 0, kmax = 0;
     float* send = nullptr;  // GM_REC_HDR + GM_REC_W * kmax floats
     float* recv = nullptr;  // nranks x that
-    hipEvent_t ev_gathered = nullptr;  // the all-gather has landed in recv (main stream)
-    hipEvent_t ev_inserted = nullptr;  // the replica inserts reading recv are done (their stream)
+    // Received offers, append-only in HBM: one gathered recv image per exchange, copied off recv on
+    // the main stream right after the all-gather. The replicas index them only when something reads
+    // a replica (bshot_odom_gpu_replica_*, the Python transport's insert, or xseq_targets, which
+    // inserts every exchange at once): the per-sweep cost without a reader is the all-gather and one
+    // HBM copy. A full log is indexed (replayed in exchange order) before it takes more.
+    float* log = nullptr;
+    size_t log_cap = 0;                             // floats
+    std::vector<std::pair<int, int>> log_entries;   // per logged exchange: include_self, sim_peers
+    hipEvent_t ev_inserted = nullptr;  // the replica inserts reading the log (or recv) are done (their stream)
     bool inserts_queued = false;
-    std::string err;
-    // the replica inserts of an exchange are queued by this thread (settle the previous ones, reserve,
-    // ~10 launches per replica), so the odometry's main thread hands them over and goes on
-    std::thread worker;
-    std::mutex mu;
-    std::condition_variable cv;
-    bool job = false, busy = false, stop = false;
-    bshot_ctx* jc = nullptr;
-    int j_self = 0, j_sim = 0;
-    int werr = 0;
-    std::string werr_msg;
+    bshot_ctx* jc = nullptr;  // the context whose replicas the log feeds
 };
 
 namespace {
 
-// settle the previous inserts, then queue this exchange's on the iss stream behind the all-gather
-int queue_inserts(bshot_ctx* c, bshot_xchg* x, int include_self, int sim_peers) {
-    const size_t per = bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * x->kmax;
-    int rc = bsh::gmap_settle_replicas_noquiesce(c);
-    if (rc) return rc;
-    hipStream_t xs = c->iss;
-    if (hipStreamWaitEvent(xs, x->ev_gathered, 0) != hipSuccess) return c->fail("exchange: stream wait", BSHOT_EHIP);
+size_t per_rank(const bshot_xchg* x) { return bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * x->kmax; }
+
+// insert one gathered image (nranks x per floats) into the replicas, in rank order, on stream xs
+int insert_image(bshot_ctx* c, bshot_xchg* x, const float* img, int include_self, int sim_peers, hipStream_t xs) {
+    const size_t per = per_rank(x);
     for (int r = 0; r < x->nranks; ++r) {
         if (r == x->rank && !include_self) continue;
-        rc = bsh::gmap_insert_records(c, r, x->recv + per * r, x->kmax, false, xs);
-        if (rc) return rc;
+        if (int rc = bsh::gmap_insert_records(c, r, img + per * r, x->kmax, false, xs)) return rc;
     }
-    for (int p = 0; p < sim_peers; ++p) {
-        rc = bsh::gmap_insert_records(c, x->nranks + p, x->recv + per * x->rank, x->kmax, false, xs);
-        if (rc) return rc;
-    }
+    for (int p = 0; p < sim_peers; ++p)
+        if (int rc = bsh::gmap_insert_records(c, x->nranks + p, img + per * x->rank, x->kmax, false, xs)) return rc;
+    return BSHOT_OK;
+}
+
+// index every logged exchange (owner order kept: exchange order per replica), queued on the iss
+// stream behind the main stream's copies into the log; the log is empty afterwards
+int replay_log(bshot_ctx* c, bshot_xchg* x) {
+    if (x->log_entries.empty()) return BSHOT_OK;
+    hipStream_t xs = c->iss;
+    if (int rc = bsh::gmap_settle_replicas_noquiesce(c)) return rc;
+    if (hipEventRecord(x->ev_inserted, c->stream) != hipSuccess || hipStreamWaitEvent(xs, x->ev_inserted, 0) != hipSuccess)
+        return c->fail("exchange: stream wait", BSHOT_EHIP);
+    const size_t img = per_rank(x) * x->nranks;
+    for (size_t e = 0; e < x->log_entries.size(); ++e)
+        if (int rc = insert_image(c, x, x->log + img * e, x->log_entries[e].first, x->log_entries[e].second, xs)) {
+            x->log_entries.clear();
+            return rc;
+        }
+    x->log_entries.clear();
     if (hipEventRecord(x->ev_inserted, xs) != hipSuccess) return c->fail("exchange: event", BSHOT_EHIP);
     x->inserts_queued = true;
     return BSHOT_OK;
 }
 
-void worker_loop(bshot_xchg* x) {
-    std::unique_lock<std::mutex> lk(x->mu);
-    while (true) {
-        x->cv.wait(lk, [x] { return x->job || x->stop; });
-        if (!x->job) break;  // stop
-        x->job = false;
-        x->busy = true;
-        bshot_ctx* c = x->jc;
-        const int self = x->j_self, sim = x->j_sim;
-        lk.unlock();
-        (void)hipSetDevice(x->device);
-        const int rc = queue_inserts(c, x, self, sim);
-        lk.lock();
-        if (rc && !x->werr) {
-            x->werr = rc;
-            x->werr_msg = bshot_last_error(c);
-        }
-        x->busy = false;
-        x->cv.notify_all();
-    }
-}
-
-// the worker has queued every insert handed to it (called before any host access to the replicas);
-// detach: the context is being destroyed, the exchange must not reach it any more
-void quiesce(void* arg, int detach) {
+// before any access to the replicas: index the log; detach: the context is being destroyed, the
+// exchange must not reach it any more (the log is dropped)
+int quiesce(void* arg, int detach) {
     auto* x = static_cast<bshot_xchg*>(arg);
-    std::unique_lock<std::mutex> lk(x->mu);
-    x->cv.wait(lk, [x] { return !x->job && !x->busy; });
-    if (detach) x->jc = nullptr;
+    if (detach) {
+        x->log_entries.clear();
+        x->jc = nullptr;
+        return BSHOT_OK;
+    }
+    return x->jc ? replay_log(x->jc, x) : BSHOT_OK;
 }
 
 }  // namespace
@@ -162,7 +154,6 @@ int bshot_xchg_create(bshot_xchg** out, const void* id128, int nranks, int rank,
     const size_t per = bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * kmax;
     if (hipMalloc(&x->send, sizeof(float) * per) != hipSuccess ||
         hipMalloc(&x->recv, sizeof(float) * per * nranks) != hipSuccess ||
-        hipEventCreateWithFlags(&x->ev_gathered, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&x->ev_inserted, hipEventDisableTiming) != hipSuccess) {
         bshot_xchg_destroy(x);
         return BSHOT_EHIP;
@@ -180,24 +171,20 @@ int bshot_xchg_create(bshot_xchg** out, const void* id128, int nranks, int rank,
 
 void bshot_xchg_destroy(bshot_xchg* x) {
     if (!x) return;
-    if (x->worker.joinable()) {
-        {
-            std::lock_guard<std::mutex> lk(x->mu);
-            x->stop = true;
-        }
-        x->cv.notify_all();
-        x->worker.join();
+    // the context (still alive: its teardown would have detached it) must not call back into x; the
+    // log's offers are indexed first, so its replicas stay complete
+    if (x->jc && x->jc->replica_quiesce_arg == x) {
+        (void)replay_log(x->jc, x);
+        x->jc->replica_quiesce = nullptr;
     }
-    // the context (still alive: its teardown would have detached it) must not call back into x
-    if (x->jc && x->jc->replica_quiesce_arg == x) x->jc->replica_quiesce = nullptr;
     if (x->comm) rccl().destroy(x->comm);
     if (x->ev_inserted) {
         (void)hipEventSynchronize(x->ev_inserted);
         (void)hipEventDestroy(x->ev_inserted);
     }
-    if (x->ev_gathered) (void)hipEventDestroy(x->ev_gathered);
     if (x->send) (void)hipFree(x->send);
     if (x->recv) (void)hipFree(x->recv);
+    if (x->log) (void)hipFree(x->log);
     delete x;
 }
 
@@ -209,41 +196,49 @@ void bshot_xchg_destroy(bshot_xchg* x) {
 int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self, int sim_peers) {
     if (!c || !x) return BSHOT_EINVAL;
     if (!c->gmap) return BSHOT_ESTATE;
-    const size_t per = bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * x->kmax;
+    if (x->jc && x->jc != c) return c->fail("exchange: already feeding another odometry's replicas", BSHOT_EINVAL);
+    const size_t per = per_rank(x), img = per * x->nranks;
     c->hmark("M_x_begin");
-    // the previous exchange's inserts are queued (the worker is idle) and reported no error
-    quiesce(x, 0);
-    if (x->werr) {
-        const int e = x->werr;
-        x->werr = 0;
-        return c->fail(x->werr_msg, e);
-    }
-    c->hmark("M_x_settled");
     int rc = bsh::gmap_pack_delta(c, x->kmax, x->send);
     if (rc) return rc;
-    // recv is read by the previous exchange's inserts until they are done
-    if (x->inserts_queued && hipStreamWaitEvent(c->stream, x->ev_inserted, 0) != hipSuccess)
-        return c->fail("exchange: stream wait", BSHOT_EHIP);
     const int e = rccl().all_gather(x->send, x->recv, per, kNcclFloat32, x->comm, c->stream);
     if (e != 0) return c->fail(std::string("ncclAllGather: ") + (rccl().err ? rccl().err(e) : "error"), BSHOT_EHIP);
-    // The replica inserts run on the low-priority iss stream, off the main stream: the next sweep's
-    // map query and matching (the odometry's critical chain) do not queue behind them, and the
-    // worker thread queues them (the main thread hands over and goes on). Only the cross-sequence
-    // targets (xseq_targets) read the replicas: then they are queued here and the main stream waits.
-    if (hipEventRecord(x->ev_gathered, c->stream) != hipSuccess) return c->fail("exchange: event", BSHOT_EHIP);
+    x->jc = c;
+    c->replica_quiesce = quiesce;
+    c->replica_quiesce_arg = x;
     if (c->opt_xseq_targets) {
-        if ((rc = queue_inserts(c, x, include_self, sim_peers))) return rc;
-        if (hipStreamWaitEvent(c->stream, x->ev_inserted, 0) != hipSuccess) return c->fail("exchange: stream wait", BSHOT_EHIP);
+        // the matching reads the replicas: index this exchange now (after anything logged), on the iss
+        // stream, and let the main stream wait for it
+        if ((rc = replay_log(c, x))) return rc;
+        if ((rc = bsh::gmap_settle_replicas_noquiesce(c))) return rc;
+        if (hipEventRecord(x->ev_inserted, c->stream) != hipSuccess || hipStreamWaitEvent(c->iss, x->ev_inserted, 0) != hipSuccess)
+            return c->fail("exchange: stream wait", BSHOT_EHIP);
+        if ((rc = insert_image(c, x, x->recv, include_self, sim_peers, c->iss))) return rc;
+        if (hipEventRecord(x->ev_inserted, c->iss) != hipSuccess || hipStreamWaitEvent(c->stream, x->ev_inserted, 0) != hipSuccess)
+            return c->fail("exchange: stream wait", BSHOT_EHIP);
+        x->inserts_queued = true;
     } else {
-        std::lock_guard<std::mutex> lk(x->mu);
-        if (!x->worker.joinable()) x->worker = std::thread(worker_loop, x);
-        x->jc = c;
-        c->replica_quiesce = quiesce;
-        c->replica_quiesce_arg = x;
-        x->j_self = include_self;
-        x->j_sim = sim_peers;
-        x->job = true;
-        x->cv.notify_all();
+        // append the gathered image to the log (a full log is indexed first; its inserts read it, so
+        // the copy waits for them)
+        if ((x->log_entries.size() + 1) * img > x->log_cap) {
+            if ((rc = replay_log(c, x))) return rc;
+            if (img > x->log_cap) {
+                size_t want = (size_t)256 << 20;  // floats: 1 GiB
+                if (const char* v = std::getenv("BSHOT_XCHG_LOG_MB")) want = (size_t)std::max(1L, std::atol(v)) << 18;
+                if (want < 4 * img) want = 4 * img;
+                if (x->inserts_queued) (void)hipEventSynchronize(x->ev_inserted);
+                if (x->log) (void)hipFree(x->log);
+                x->log = nullptr;
+                x->log_cap = 0;
+                if (hipMalloc(&x->log, sizeof(float) * want) != hipSuccess) return c->fail("exchange: log alloc", BSHOT_EHIP);
+                x->log_cap = want;
+            }
+        }
+        if (x->log_entries.empty() && x->inserts_queued && hipStreamWaitEvent(c->stream, x->ev_inserted, 0) != hipSuccess)
+            return c->fail("exchange: stream wait", BSHOT_EHIP);
+        if (bsh::kcopy(x->log + img * x->log_entries.size(), x->recv, sizeof(float) * img, c->stream) != hipSuccess)
+            return c->fail("exchange: log copy", BSHOT_EHIP);
+        x->log_entries.emplace_back(include_self, sim_peers);
     }
     c->hmark("M_x_queued");
     return BSHOT_OK;

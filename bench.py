@@ -45,7 +45,9 @@ def pmc_kernel(stage, path=None):
     if not files:
         return None, None
     try:
-        k = json.load(open(files[-1]))["kernels"].get(f"bsk::k_{stage}")
+        ks = json.load(open(files[-1]))["kernels"]
+        # the product instantiation of a kernel templated on its diagnostic counters (k_seg_ratio<false>)
+        k = ks.get(f"bsk::k_{stage}<false>") or ks.get(f"bsk::k_{stage}")
         return (k or None), os.path.relpath(files[-1], ROOT)
     except (OSError, ValueError, KeyError):
         return None, None

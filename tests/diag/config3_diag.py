@@ -68,7 +68,25 @@ def rel_err(Ta, Tb):
     return float(np.linalg.norm(D[:3, 3])), float(np.degrees(np.arccos(c)))
 
 
-def run(frames, fix_normals, aperiodic, gt_override, k, threads, run_icp=1):
+def gt_pose(frame):
+    """tools/synth.cpp's sensor pose at frame t (both synth_sweep and synth_lasers): yaw 0.5 deg *
+    sin(2 pi t / 200), position (0, 800 t, 0); float32 like synth_sweep's pose_out"""
+    yaw = 0.5 * np.pi / 180.0 * np.sin(2 * np.pi * frame / 200.0)
+    c, s = np.cos(yaw), np.sin(yaw)
+    P = np.array([[c, -s, 0, 0], [s, c, 0, 800.0 * frame], [0, 0, 1, 0], [0, 0, 0, 1]], np.float32)
+    return P.astype(np.float64)
+
+
+def laser_sweep(frame, sensor, seed):
+    """odometry_test's input chain on synthetic laser returns: one rotation of the sensor
+    (synth_lasers) through the oracle Preprocessor (test/odometry_test.cpp:32-33: vertical initial
+    -0.6 rad, low-point threshold -1950 mm)."""
+    L = bshot_py.synth_lasers(frame, sensor=sensor, seed=seed)
+    xyz, _ = orc.preprocess(L, bshot_py.sensor_vertical_angles(sensor), -0.6, -1950.0)
+    return xyz
+
+
+def run(frames, fix_normals, aperiodic, gt_override, k, threads, run_icp=1, lasers=-1):
     od = orc.Odometry(orc.params(num_keypoints=k, run_icp=run_icp))
     orc.lib().oracle_diag_fix_normals(od.h, int(fix_normals))
     seed = 42 | (APERIODIC if aperiodic else 0)
@@ -78,8 +96,11 @@ def run(frames, fix_normals, aperiodic, gt_override, k, threads, run_icp=1):
     prev_pose = None
     t0 = time.time()
     for f in range(frames):
-        xyz, gt = bshot_py.synth_sweep(f, seed=seed)
-        gt = np.asarray(gt, np.float64).reshape(4, 4)
+        if lasers >= 0:
+            xyz, gt = laser_sweep(f, lasers, seed), gt_pose(f)
+        else:
+            xyz, gt = bshot_py.synth_sweep(f, seed=seed)
+            gt = np.asarray(gt, np.float64).reshape(4, 4)
         if gt_override:
             G = np.ascontiguousarray(gt.astype(np.float32).reshape(16))
             orc.lib().oracle_diag_pose_override(od.h, G.ctypes.data_as(orc.P))
@@ -159,6 +180,9 @@ def main():
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--cases", default="ref_gt,fixn_gt,aper_gt,ref_free,fixn_free,aper_free,fixn_aper_free")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03_config3_diag.json"))
+    ap.add_argument("--lasers", type=int, default=-1,
+                    help="sensor of synth_lasers (2: HDL-32E, the reference's own) fed through the oracle "
+                         "Preprocessor, as odometry_test does; default: synth_sweep's HDL-64 point clouds")
     a = ap.parse_args()
     orc.set_point_threads(a.threads)
     orc.set_threads(a.threads)
@@ -171,14 +195,14 @@ def main():
         # per-frame under-estimate of the motion the keypoint ICP's?
         "ref_noicp_free": (False, False, False, 0), "fixn_noicp_free": (True, False, False, 0),
     }
-    out = {"frames": a.frames, "keypoints": a.keypoints, "cases": {}}
+    out = {"frames": a.frames, "keypoints": a.keypoints, "lasers": a.lasers, "cases": {}}
     if os.path.exists(a.out):
         out = json.load(open(a.out))
     for c in a.cases.split(","):
         fixn, aper, gto = defs[c][:3]
         icp = defs[c][3] if len(defs[c]) > 3 else 1
         print(f"case {c}: fix_normals={fixn} aperiodic={aper} gt_override={gto} run_icp={icp}", flush=True)
-        rows = run(a.frames, fixn, aper, gto, a.keypoints, a.threads, icp)
+        rows = run(a.frames, fixn, aper, gto, a.keypoints, a.threads, icp, a.lasers)
         out["cases"][c] = {"fix_normals": fixn, "aperiodic": aper, "gt_override": gto, "run_icp": icp,
                            "summary": summary(rows), "per_frame": rows}
         print(json.dumps({c: out["cases"][c]["summary"]}), flush=True)

@@ -161,18 +161,27 @@ def test_describe_device_plan(ctx, cloud, sr_ref, hint):
 
 
 def test_match_exact_random_and_ties(ctx):
+    """A9 (one-pass k_ham_pair: row and column minima from one distance tile) vs the oracle: sizes
+    across the row tiles (512 rows per workgroup), the reference splits and the LDS tiles (128),
+    duplicated rows on both sides (first index must win in both directions), all-equal distances."""
     rng = np.random.default_rng(7)
-    for na, nb in ((1, 1), (5, 300), (600, 1800), (2048, 4096), (257, 1)):
+    for na, nb in ((1, 1), (5, 300), (600, 1800), (2048, 4096), (257, 1), (513, 129), (2047, 15001), (4100, 37),
+                   (1, 20000), (3000, 3000)):
         a = rng.integers(0, 2**32, (na, 11), dtype=np.uint64).astype(np.uint32)
         b = rng.integers(0, 2**32, (nb, 11), dtype=np.uint64).astype(np.uint32)
         # sparse descriptors (like the degenerate B-SHOT bits) -> many distance ties
         a &= rng.integers(0, 2**32, (na, 11), dtype=np.uint64).astype(np.uint32) & 0x11111111
         b &= rng.integers(0, 2**32, (nb, 11), dtype=np.uint64).astype(np.uint32) & 0x11111111
         b[nb // 2:] = b[: nb - nb // 2]  # duplicated rows: first index must win
+        a[na // 2:] = a[: na - na // 2]
         got = ctx.match(a, b)
         ref = orc.match(a, b)
         for g, r in zip(got, ref):
             np.testing.assert_array_equal(g, r)
+    a = np.zeros((700, 11), np.uint32)  # every distance 0: left = 0, right = 0, only row 0 mutual
+    b = np.zeros((900, 11), np.uint32)
+    for g, r in zip(ctx.match(a, b), orc.match(a, b)):
+        np.testing.assert_array_equal(g, r)
 
 
 def test_icp_exact(ctx, cloud, sr_ref):
@@ -188,6 +197,24 @@ def test_icp_exact(ctx, cloud, sr_ref):
     Tr, itr = orc.icp(src, tgt)
     assert it == itr
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+
+
+def test_icp_iteration_counts_and_sizes(ctx, cloud, sr_ref):
+    """A11 device loop (k_icp_loop) vs the oracle's host loop: PCL's iteration cap at 0, 1, 2 and
+    beyond the old hand-over's 64 (200: the loop stops on its own convergence test), source counts
+    not a multiple of 4 (LDS row tails) and just past the LDS staging (2049: the HBM-chunked
+    Umeyama)."""
+    ridx, rrat = sr_ref
+    kidx, _ = orc.select_topk(ridx, rrat, 2100)
+    tgt = cloud[kidx]
+    c, s = np.cos(0.02), np.sin(0.02)
+    rot = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], np.float32)
+    for ns, it_cap in ((2100, 0), (2100, 1), (2100, 2), (2100, 200), (1001, 10), (2049, 10), (2048, 10), (3, 10)):
+        src = (tgt[:ns] @ rot.T + np.array([700, -400, 90], np.float32)).astype(np.float32)
+        T, it = ctx.icp(src, tgt, max_iter=it_cap)
+        Tr, itr = orc.icp(src, tgt, max_iter=it_cap)
+        assert it == itr, (ns, it_cap)
+        np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
 
 
 @pytest.mark.parametrize("big", [False, True])
