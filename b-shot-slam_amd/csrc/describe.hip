@@ -6,7 +6,8 @@
 //   k_desc_plan     one workgroup: segment offsets, 64-rank chunk bases, LPT order, on the device
 //   k_excl_scan     one workgroup: segment offsets (host-planned describe after a plan overflow)
 //   k_shot_gather_b workgroup/keypoint: keys (d2 bits << 32 | idx) scattered bucket-grouped
-//   k_shot_rank     wave per 64-rank chunk: exact rank inside each bucket -> FLANN's sorted order
+//   k_shot_rank_wg  workgroup per keypoint: exact rank inside each bucket, span by span in LDS ->
+//                   FLANN's sorted order (k_shot_rank: the wave-per-64-rank-chunk variant)
 #include <hip/hip_runtime.h>
 
 #include "bshot_math.h"
@@ -248,6 +249,77 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
     }();
 }
 
+// Workgroup per keypoint (LPT order): the keypoint's bucket-grouped segment is ranked span by span,
+// a span being whole buckets holding <= RK_SPAN keys: staged in LDS with coalesced loads (with its
+// bucket starts), every key ranked inside its bucket from LDS, its index written to its sorted slot.
+// Two dependent global round trips per span instead of ~5 per 64-rank chunk (owner, offsets, keys,
+// bucket starts, bucket keys): the kernel streams a large neighbourhood (config 5: ~28k keys per
+// keypoint) instead of waiting on it. A bucket alone larger than RK_SPAN is ranked from HBM.
+#define RK_T 256
+#define RK_SPAN 2048
+__global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int* __restrict__ perm,
+                                                      const long long* __restrict__ offs,
+                                                      const unsigned int* __restrict__ bstart,
+                                                      const unsigned long long* __restrict__ seg,
+                                                      unsigned int* __restrict__ out) {
+    __shared__ unsigned long long st[RK_SPAN];
+    __shared__ unsigned int sbs[SG_BUCKETS + 1];
+    __shared__ int s_e;
+    const int t = threadIdx.x;
+    const int q = perm[blockIdx.x];
+    const long long o = offs[q];
+    const int n = (int)(offs[q + 1] - o);
+    if (n <= 0) return;
+    const float R2 = (float)((double)R * (double)R);
+    const float sc = (float)SG_BUCKETS / R2;
+    const unsigned long long* sg = seg + o;
+    unsigned int* op = out + o;
+    // the bucket starts, and end(1024) = n
+    for (int b = t; b < SG_BUCKETS; b += RK_T) sbs[b] = bstart[(size_t)q * SG_BUCKETS + b];
+    if (t == 0) sbs[SG_BUCKETS] = (unsigned int)n;
+    __syncthreads();
+    int b0 = 0;
+    while (true) {
+        const unsigned int lo = sbs[b0];
+        if (lo >= (unsigned int)n) break;
+        // the span: buckets [b0, e) with e the largest bucket end within RK_SPAN keys of lo
+        if (t == 0) s_e = b0;
+        __syncthreads();
+        int best = b0;
+        for (int e = b0 + 1 + t; e <= SG_BUCKETS; e += RK_T)
+            if (sbs[e] - lo <= RK_SPAN) best = e;  // monotone in e: the per-thread max is a prefix bound
+        if (best > b0) atomicMax(&s_e, best);
+        __syncthreads();
+        int e = s_e;
+        if (e == b0) {
+            // bucket b0 alone exceeds the span: rank it from HBM
+            const unsigned int s0 = lo, e0 = sbs[b0 + 1];
+            for (unsigned int i = s0 + t; i < e0; i += RK_T) {
+                const unsigned long long key = sg[i];
+                unsigned int rank = 0;
+                for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
+                op[s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
+            }
+            e = b0 + 1;
+        } else {
+            const unsigned int hi = sbs[e], m = hi - lo;
+            for (unsigned int i = t; i < m; i += RK_T) st[i] = sg[lo + i];
+            __syncthreads();
+            for (unsigned int i = t; i < m; i += RK_T) {
+                const unsigned long long key = st[i];
+                const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
+                const unsigned int s0 = sbs[b] - lo, e0 = sbs[b + 1] - lo;
+                unsigned int rank = 0;
+                for (unsigned int j = s0; j < e0; ++j) rank += st[j] < key ? 1u : 0u;
+                op[lo + s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
+            }
+        }
+        __syncthreads();  // st and s_e are rewritten for the next span
+        b0 = e;
+        if (b0 >= SG_BUCKETS) break;
+    }
+}
+
 }  // namespace bsk
 
 namespace bsh {
@@ -275,6 +347,13 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
                                 const int* err) {
     if (k <= 0) return hipSuccess;
     bsk::k_shot_gather_b<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long* offs, const unsigned int* bstart,
+                               const unsigned long long* seg, unsigned int* out, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    bsk::k_shot_rank_wg<<<k, RK_T, 0, s>>>(k, R, perm, offs, bstart, seg, out);
     return hipGetLastError();
 }
 

@@ -99,10 +99,13 @@ __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ p
 // A4 from the SHOT neighbour lists (include/bshot_bits.h:63-80): with normal_radius == shot_radius
 // the normals' FLANN radius search (the normal_max_nn smallest (d2, idx) with d2 < r^2, in that
 // order) is the first min(n, normal_max_nn) entries of the keypoint's sorted SHOT segment, so no
-// search of its own is needed. One wave: the neighbours' coordinates in LDS (f: 3 x 512 floats), the
+// search of its own is needed. One wave: the neighbours' coordinates in LDS (f: 3 x NF_STRIDE floats), the
 // 9 accumulators of pcl::computeMeanAndCovarianceMatrix as sequential float sums in rank order
 // (lanes 0..5: xx xy xz yy yz zz products, lanes 6..8: x y z -- k_normals' order), then eigen33 and
 // the flip towards the origin. Returns (nx, ny, nz, curvature), NaN as k_normals.
+// the 3 coordinate arrays sit NF_STRIDE floats apart (512 + 4: the 9 summing lanes read x[r], y[r],
+// z[r] together from 3 different LDS banks; a 512 stride put them in one bank)
+#define NF_STRIDE 516
 __device__ __forceinline__ float4 segment_normal(const float4* __restrict__ pts4, float kx, float ky, float kz,
                                                  const unsigned int* __restrict__ sg, long long cnt, int max_nn,
                                                  float* f) {
@@ -116,15 +119,15 @@ __device__ __forceinline__ float4 segment_normal(const float4* __restrict__ pts4
             if (need >= 3) {
                 for (int r = lane; r < need; r += 64) {
                     const float4 p = pts4[sg[r]];
-                    f[r] = p.x; f[512 + r] = p.y; f[1024 + r] = p.z;
+                    f[r] = p.x; f[NF_STRIDE + r] = p.y; f[2 * NF_STRIDE + r] = p.z;
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (lane < 9) {
                     const bool prod = lane < 6;
                     const int a = prod ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
                     const int b = lane < 3 ? lane : (lane < 5 ? lane - 2 : 2);
-                    const float* pa = f + 512 * a;
-                    const float* pb = f + 512 * (prod ? b : a);
+                    const float* pa = f + NF_STRIDE * a;
+                    const float* pb = f + NF_STRIDE * (prod ? b : a);
                     int r = 0;
                     for (; r + 4 <= need; r += 4) {
                         float v[4];
@@ -199,7 +202,7 @@ __global__ void __launch_bounds__(64 * LE_WAVES) k_lrf_eig(int k, const int* __r
                                                            const long long* __restrict__ offs,
                                                            const unsigned int* __restrict__ seg, int nmax,
                                                            float4* __restrict__ normals) {
-    __shared__ float fl[LE_WAVES / 2][3 * 512];
+    __shared__ float fl[LE_WAVES / 2][3 * NF_STRIDE];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     // two waves per keypoint: the odd one computes the normal (nmax > 0), the even one the LRF eigen
     // system -- two independent sequential chains side by side instead of one after the other
@@ -481,8 +484,22 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 // adds in PCL's order), double-buffered, so the records never leave LDS. The CU's LDS float-atomic
 // unit (~3 cycles per lane-op) bounds the applying wave; keypoints launch in descending
 // neighbourhood size so the largest start first.
+#ifndef HF_NW
+#define HF_NW 8
+#endif
+#ifndef HF_WPE
+#define HF_WPE 0
+#endif
+#ifndef HF_APQ
+#define HF_APQ 4  // the applying wave reads a chunk's records in HF_APQ parts
+#endif
+#if HF_WPE > 0
+#define HF_ATTR __attribute__((amdgpu_waves_per_eu(HF_WPE)))
+#else
+#define HF_ATTR
+#endif
 template <int HF_WAVES>
-__global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __restrict__ pts4,
+__global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const float4* __restrict__ pts4,
                                                               const float4* __restrict__ normals,
                                                               const float* __restrict__ kps, int k, float R,
                                                               const int* __restrict__ perm,
@@ -596,19 +613,21 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
             int use = 0;
             for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use |= suse[buf][bi];
             if (lane < 5 && ((use >> lane) & 1)) {
-                for (int half = 0; half < 2 * HF_B && b * HF_B + (half >> 1) < nch; ++half) {
-                    // 32 ranks of chunk half / 2 at a time (keeps the applying path's registers low)
-                    const int bi = half >> 1, r0 = 32 * (half & 1);
+                for (int part = 0; part < HF_APQ * HF_B && b * HF_B + part / HF_APQ < nch; ++part) {
+                    // 64 / HF_APQ ranks of chunk part / HF_APQ at a time (keeps the applying path's
+                    // registers low: the producers' FP64 code sets the kernel's VGPR budget)
+                    const int bi = part / HF_APQ, r0 = (64 / HF_APQ) * (part % HF_APQ);
                     const uint4* b4 = reinterpret_cast<const uint4*>(&sS[buf][bi][64 * lane + r0]);
                     const float4* v4 = reinterpret_cast<const float4*>(&sV[buf][bi][64 * lane + r0]);
-                    uint4 bw[4];
-                    float4 vw[8];
+                    constexpr int NB = 8 / HF_APQ;  // uint4 (8 ranks) per part
+                    uint4 bw[NB];
+                    float4 vw[2 * NB];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) bw[u] = b4[u];
+                    for (int u = 0; u < NB; ++u) bw[u] = b4[u];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) vw[u] = v4[u];
+                    for (int u = 0; u < 2 * NB; ++u) vw[u] = v4[u];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
+                    for (int u = 0; u < NB; ++u) {
                         const unsigned int w[4] = {bw[u].x, bw[u].y, bw[u].z, bw[u].w};
 #pragma unroll
                         for (int h = 0; h < 4; ++h) {
@@ -635,6 +654,9 @@ __global__ void __launch_bounds__(64 * HF_WAVES) k_hist_fused(const float4* __re
 
 namespace bsh {
 
+#ifndef SHOT_RANK_WG
+#define SHOT_RANK_WG 1  // 1: k_shot_rank_wg (workgroup per keypoint); 0: k_shot_rank (wave per chunk)
+#endif
 // part 0: in-bucket rank (sorted segments); 1: LRF; 2: histogram records + ordered apply
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.k <= 0) return hipSuccess;
@@ -644,9 +666,13 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (part == 0) {
         if (A.n_chunks > 0) {
             bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
+#if SHOT_RANK_WG
+            if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s))) return e;
+#else
             if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
                                         A.max_blocks)))
                 return e;
+#endif
         }
         return hipGetLastError();
     }
@@ -662,8 +688,8 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
         // the histogram kernel
         return hipGetLastError();
     }
-    // 8 waves per workgroup: 1 applies, 7 produce records
-    bsk::k_hist_fused<8><<<A.k, 64 * 8, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
+    // HF_NW waves per workgroup: 1 applies, HF_NW - 1 produce records
+    bsk::k_hist_fused<HF_NW><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
                                                  A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
     return hipGetLastError();
 }

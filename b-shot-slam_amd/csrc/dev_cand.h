@@ -89,17 +89,22 @@ __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs
     }
 }
 
-// lane's cell of round `base` of the query cube: its spts run (cnt = 0 when pruned or empty)
-__device__ __forceinline__ void cand_lookup(const GridView& g, double c, int x0, int y0, int z0, int ny, int nz,
-                                            int ncell, int cidx, float qx, float qy, float qz, double lim,
-                                            unsigned int& st, unsigned int& cnt) {
+// lane's cell of round `base` of the query cube: its spts run (cnt = 0 when pruned or empty). The
+// cube and the pruning only decide which cells are visited, never which points count (every
+// candidate is tested d2 < rs^2), so they run in float with a slack that covers float rounding:
+// lim = rs + slack, slack >= 1 mm and >= 2^-20 of the query's magnitude (a conservative cube:
+// never a cell with an in-ball point left out).
+__device__ __forceinline__ void cand_lookup(const GridView& g, int x0, int y0, int z0, int ny, int nz, int ncell,
+                                            int cidx, float qx, float qy, float qz, float lim, unsigned int& st,
+                                            unsigned int& cnt) {
     st = 0;
     cnt = 0;
     if (cidx < ncell) {
         const int iz = cidx % nz, t = cidx / nz, iy = t % ny, ix = t / ny;
         const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
-        const double bx0 = cx * c, by0 = cy * c, bz0 = cz * c;
-        double dx = 0, dy = 0, dz = 0;
+        const float c = g.cell;
+        const float bx0 = (float)cx * c, by0 = (float)cy * c, bz0 = (float)cz * c;
+        float dx = 0.f, dy = 0.f, dz = 0.f;
         if (qx < bx0) dx = bx0 - qx; else if (qx > bx0 + c) dx = qx - (bx0 + c);
         if (qy < by0) dy = by0 - qy; else if (qy > by0 + c) dy = qy - (by0 + c);
         if (qz < bz0) dz = bz0 - qz; else if (qz > bz0 + c) dz = qz - (bz0 + c);
@@ -107,6 +112,11 @@ __device__ __forceinline__ void cand_lookup(const GridView& g, double c, int x0,
             if (!grid_lookup(g, cell_key(cx, cy, cz), st, cnt)) cnt = 0;
         }
     }
+}
+
+// the float slack of a query's cube (see cand_lookup)
+__device__ __forceinline__ float cand_slack(float qx, float qy, float qz) {
+    return 1.f + fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz))) * 9.5367431640625e-07f;  // 2^-20
 }
 
 // Returns false (and streams nothing) when the cube holds fewer than min_total candidates -- the
@@ -117,19 +127,18 @@ template <int GROUP = CAND_GROUP, class F>
 __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, float qx, float qy, float qz, float rs,
                                                float rs2, F&& f, int min_total = 0, int part = 0, int nparts = 1) {
     const int lane = lane_id();
-    const double c = (double)g.cell;
-    const int x0 = (int)floor(((double)qx - rs) / c), x1 = (int)floor(((double)qx + rs) / c);
-    const int y0 = (int)floor(((double)qy - rs) / c), y1 = (int)floor(((double)qy + rs) / c);
-    const int z0 = (int)floor(((double)qz - rs) / c), z1 = (int)floor(((double)qz + rs) / c);
+    const float ic = g.inv_cell, lim = rs + cand_slack(qx, qy, qz);
+    const int x0 = (int)floorf((qx - lim) * ic), x1 = (int)floorf((qx + lim) * ic);
+    const int y0 = (int)floorf((qy - lim) * ic), y1 = (int)floorf((qy + lim) * ic);
+    const int z0 = (int)floorf((qz - lim) * ic), z1 = (int)floorf((qz + lim) * ic);
     const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
     const int ncell = nx * ny * nz;
-    const double lim = (double)rs + 1.0;
     int epoch = cs->epoch;
     bool streamed = true;
     if (ncell <= 128) {
         unsigned int st0, cnt0, st1 = 0, cnt1 = 0;
-        cand_lookup(g, c, x0, y0, z0, ny, nz, ncell, lane, qx, qy, qz, lim, st0, cnt0);
-        if (ncell > 64) cand_lookup(g, c, x0, y0, z0, ny, nz, ncell, 64 + lane, qx, qy, qz, lim, st1, cnt1);
+        cand_lookup(g, x0, y0, z0, ny, nz, ncell, lane, qx, qy, qz, lim, st0, cnt0);
+        if (ncell > 64) cand_lookup(g, x0, y0, z0, ny, nz, ncell, 64 + lane, qx, qy, qz, lim, st1, cnt1);
         int tot0, tot1 = 0;
         const int off0 = wave_excl_scan((int)cnt0, tot0);
         const int off1 = ncell > 64 ? wave_excl_scan((int)cnt1, tot1) : 0;
@@ -147,7 +156,7 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
     } else {
         for (int base = 0; base < ncell; base += 64) {
             unsigned int st, cnt;
-            cand_lookup(g, c, x0, y0, z0, ny, nz, ncell, base + lane, qx, qy, qz, lim, st, cnt);
+            cand_lookup(g, x0, y0, z0, ny, nz, ncell, base + lane, qx, qy, qz, lim, st, cnt);
             int total;
             const int off = wave_excl_scan((int)cnt, total);
             if (total == 0) continue;

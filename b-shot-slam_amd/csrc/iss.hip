@@ -177,10 +177,11 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
     int cnt = 0;
     if (fin) {
         const float r2 = (float)((double)salient * (double)salient);
-        const double cs = (double)g.cell;
-        const int x0 = (int)floor(((double)c.x - salient) / cs), x1 = (int)floor(((double)c.x + salient) / cs);
-        const int y0 = (int)floor(((double)c.y - salient) / cs), y1 = (int)floor(((double)c.y + salient) / cs);
-        const int z0 = (int)floor(((double)c.z - salient) / cs), z1 = (int)floor(((double)c.z + salient) / cs);
+        // the cube in float with for_candidates' slack (cells visited, never points counted)
+        const float ic = g.inv_cell, lim = salient + cand_slack(c.x, c.y, c.z);
+        const int x0 = (int)floorf((c.x - lim) * ic), x1 = (int)floorf((c.x + lim) * ic);
+        const int y0 = (int)floorf((c.y - lim) * ic), y1 = (int)floorf((c.y + lim) * ic);
+        const int z0 = (int)floorf((c.z - lim) * ic), z1 = (int)floorf((c.z + lim) * ic);
         auto take = [&](const float4& p) {
             if (d2_flann(c.x, c.y, c.z, p.x, p.y, p.z) < r2) {
                 if (cnt < ISS_LCAP)
@@ -292,16 +293,16 @@ __global__ void __launch_bounds__(256) k_iss_nms_wave(GridView g, const float4* 
     const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     const int cnt_pts = all ? n : ovf[0];
     const float r2 = (float)((double)nonmax * (double)nonmax);
-    const double cs = (double)g.cell;
     for (int oi = wv; oi < cnt_pts; oi += nw) {
         const int q = all ? oi : ovf[1 + oi];
         const double tq = third[q];
         const float4 c = pts4[q];
         unsigned char f = 0;
         if (tq > 0.0 && __builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
-            const int x0 = (int)floor(((double)c.x - nonmax) / cs), x1 = (int)floor(((double)c.x + nonmax) / cs);
-            const int y0 = (int)floor(((double)c.y - nonmax) / cs), y1 = (int)floor(((double)c.y + nonmax) / cs);
-            const int z0 = (int)floor(((double)c.z - nonmax) / cs), z1 = (int)floor(((double)c.z + nonmax) / cs);
+            const float ic = g.inv_cell, lim = nonmax + cand_slack(c.x, c.y, c.z);
+            const int x0 = (int)floorf((c.x - lim) * ic), x1 = (int)floorf((c.x + lim) * ic);
+            const int y0 = (int)floorf((c.y - lim) * ic), y1 = (int)floorf((c.y + lim) * ic);
+            const int z0 = (int)floorf((c.z - lim) * ic), z1 = (int)floorf((c.z + lim) * ic);
             int cnt = 0;
             bool bigger = false;
             for (int ix = x0; ix <= x1 && !bigger; ++ix)

@@ -37,6 +37,9 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
                                   hipStream_t s);
 // out: the neighbour indices of every segment in (d2, idx) order (4 B each; the consumers recompute
 // d2 from the points with the gather's expression, bit-identical)
+// the same, a workgroup per keypoint in perm's order (spans of whole buckets staged in LDS)
+hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long* offs, const unsigned int* bstart,
+                               const unsigned long long* seg, unsigned int* out, hipStream_t s);
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
                             hipStream_t s, int max_blocks = 0);

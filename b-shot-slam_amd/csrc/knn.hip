@@ -51,8 +51,11 @@ struct KnnLds {
     unsigned short boff[KNN_NB + 4];   // counting-sort bucket starts (<= KNN_PRE)
     CandLds cand;
 };
-static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 2 * (KNN_NB + 4) >= 3 * 512 * 4,
-              "list + hist + boff must hold 3 x 512 floats");
+// the finishing math's 3 coordinate arrays sit FL_STRIDE floats apart: 512 + 4, so lanes reading
+// x[r], y[r], z[r] together hit 3 different LDS banks (a 512 stride put all three in one bank)
+#define FL_STRIDE 516
+static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 2 * (KNN_NB + 4) >= 3 * FL_STRIDE * 4,
+              "list + hist + boff must hold 3 x FL_STRIDE floats");
 static_assert(KNN_CAP >= KNN_PRE, "the prefix must fit the list (and the bitonic sort's 512 keys)");
 static_assert(KNN_CAP % 64 == 0 && KNN_NB % 64 == 0, "lane-strided loops");
 
@@ -445,10 +448,10 @@ __device__ __forceinline__ int ladder_start(const LadderGrids& lg, float qx, flo
     const int lane = lane_id();
     unsigned int st = 0, cnt = 0;
     if (lane < 4) {
+        // the own cell in float (a boundary query may read a neighbour cell's count: speed only)
         const GridView& g = lg.g[lane];
-        const double c = (double)g.cell;
-        if (!grid_lookup(g, cell_key((int)floor((double)qx / c), (int)floor((double)qy / c), (int)floor((double)qz / c)),
-                         st, cnt))
+        const float ic = g.inv_cell;
+        if (!grid_lookup(g, cell_key((int)floorf(qx * ic), (int)floorf(qy * ic), (int)floorf(qz * ic)), st, cnt))
             cnt = 0;
     }
     const float c0 = (float)readlane_i((int)cnt, 0), c1 = (float)readlane_i((int)cnt, 1);
@@ -489,6 +492,7 @@ __device__ __forceinline__ float seq_dot(const float* a, const float* b, int n) 
 }
 
 // gather neighbour coordinates (rank order) into the LDS list region as 3 float arrays of 512
+// (FL_STRIDE apart)
 __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, const float4* __restrict__ pts4, int need,
                                            float* fl) {
     const int lane = lane_id();
@@ -504,7 +508,7 @@ __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, con
         const int r = lane + 64 * j;
         if (r < need) {
             const float4 p = pts4[myidx[j]];
-            fl[r] = p.x; fl[512 + r] = p.y; fl[1024 + r] = p.z;
+            fl[r] = p.x; fl[FL_STRIDE + r] = p.y; fl[2 * FL_STRIDE + r] = p.z;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -518,7 +522,7 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
     gather_xyz(sorted, pts4, need, fl);
     // pcl::computeCentroid: sequential float sums in rank order (lanes 0,1,2)
     float acc = 0.f;
-    if (lane < 3) acc = seq_sum(fl + 512 * lane, need);
+    if (lane < 3) acc = seq_sum(fl + FL_STRIDE * lane, need);
     const float fn = (float)need;
     const float cx = __shfl(acc, 0, 64) / fn, cy = __shfl(acc, 1, 64) / fn, cz = __shfl(acc, 2, 64) / fn;
     const float tx = sp.x - cx, ty = sp.y - cy, tz = sp.z - cz;
@@ -528,7 +532,7 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
             const int r = r0 + lane;
             bool p = false, m = false;
             if (r < need) {
-                const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
+                const float vx = fl[r] - sp.x, vy = fl[FL_STRIDE + r] - sp.y, vz = fl[2 * FL_STRIDE + r] - sp.z;
                 const float dot = tx * vx + (ty * vy + tz * vz);
                 p = dot > 0.f;
                 m = dot < 0.f;
@@ -548,7 +552,7 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
         for (int r0 = 0; r0 < need; r0 += 64) {
             const int r = r0 + lane;
             if (r < need) {
-                const float vx = fl[r] - sp.x, vy = fl[512 + r] - sp.y, vz = fl[1024 + r] - sp.z;
+                const float vx = fl[r] - sp.x, vy = fl[FL_STRIDE + r] - sp.y, vz = fl[2 * FL_STRIDE + r] - sp.z;
                 const float vn = sqrtf(vx * vx + (vy * vy + vz * vz));
                 const float dot = tx * vx + (ty * vy + tz * vz);
                 const bool use = !(ctn == 0.f || vn == 0.f);
@@ -645,7 +649,7 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(LadderGrids lg, cons
                     if (lane < 9) {
                         const int a = lane < 6 ? (lane < 3 ? 0 : (lane < 5 ? 1 : 2)) : lane - 6;
                         const int bsel = lane < 6 ? (lane < 3 ? lane : (lane < 5 ? lane - 2 : 2)) : -1;
-                        acc = bsel >= 0 ? seq_dot(fl + 512 * a, fl + 512 * bsel, need) : seq_sum(fl + 512 * a, need);
+                        acc = bsel >= 0 ? seq_dot(fl + FL_STRIDE * a, fl + FL_STRIDE * bsel, need) : seq_sum(fl + FL_STRIDE * a, need);
                     }
                     float ac[9];
 #pragma unroll

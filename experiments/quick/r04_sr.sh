@@ -11,7 +11,7 @@ for v in base new; do
   if [ $v = base ]; then L=experiments/ab/libbshot_base.so; else L=b-shot-slam_amd/lib/libbshot_amd.so; fi
   BSHOT_LIB=$L timeout -k 10 120 python b-shot-slam_amd/tools/sr_bench.py || exit 1
 done
-bash experiments/quick/ab_lib.sh $N || exit 1
+bash experiments/quick/ab_multi.sh $N experiments/ab/libbshot_base.so b-shot-slam_amd/lib/libbshot_amd.so b-shot-slam_amd/lib/exp/libbshot_hf4.so || exit 1
 cd /tmp && export TMPDIR=/tmp
 for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR"; do
   T=$(echo $P | cut -c1-5)
