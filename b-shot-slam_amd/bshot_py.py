@@ -68,6 +68,7 @@ ABI_SYMBOLS = [
     "bshot_odom_gpu_replica_insert", "bshot_queue_cloud_device", "bshot_odom_set_next2_device",
     "bshot_pre_default_params", "bshot_preprocess", "bshot_preprocess_device", "bshot_preprocess_cells",
     "bshot_pcap_load", "bshot_velodyne_decode", "bshot_velodyne_decode_device",
+    "bshot_odom_extract_device", "bshot_odom_process_record",
 ]
 
 # velodyne::Laser (include/VelodyneCapture.h:43-50) == bshot_laser: 32 B, int64 time at offset 24
@@ -435,6 +436,21 @@ class Odometry:
     def process_device(self, dptr, n):
         st = FrameStats()
         self._chk(self.L.bshot_odom_process_device(self.h, P(dptr), n, ctypes.byref(st)), "odom_process_device")
+        return st
+
+    def extract_device(self, dptr, n):
+        """Frame-sharded mode: the extraction half of a device sweep as a float32 record
+        (bshot_odom_extract_device); the set_next lookahead applies."""
+        cap = 8 + 15 * max(1, self.params.num_keypoints) + 3 * (n + 1)  # k <= K, ISS points <= n
+        rec = np.zeros(cap, np.float32)
+        ln = self._chk(self.L.bshot_odom_extract_device(self.h, P(dptr), n, _ptr(rec), cap), "odom_extract_device")
+        return rec[:ln].copy()
+
+    def process_record(self, rec):
+        """Frame-sharded mode: the chain half of the next sweep from an extraction record."""
+        rec = np.ascontiguousarray(rec, np.float32)
+        st = FrameStats()
+        self._chk(self.L.bshot_odom_process_record(self.h, _ptr(rec), len(rec), ctypes.byref(st)), "odom_process_record")
         return st
 
     def _get(self, fn, shape_cols, dtype, cap=1 << 20):

@@ -94,13 +94,16 @@ __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs
 // candidate is tested d2 < rs^2), so they run in float with a slack that covers float rounding:
 // lim = rs + slack, slack >= 1 mm and >= 2^-20 of the query's magnitude (a conservative cube:
 // never a cell with an in-ball point left out).
-__device__ __forceinline__ void cand_lookup(const GridView& g, int x0, int y0, int z0, int ny, int nz, int ncell,
-                                            int cidx, float qx, float qy, float qz, float lim, unsigned int& st,
-                                            unsigned int& cnt) {
+// rnz, rny: 1 / nz, 1 / ny (the cell index splits by float reciprocals: exact for these small
+// integers with the +0.5 bias, and no integer division sequence per lane)
+__device__ __forceinline__ void cand_lookup(const GridView& g, int x0, int y0, int z0, int ny, int nz, float rny,
+                                            float rnz, int ncell, int cidx, float qx, float qy, float qz, float lim,
+                                            unsigned int& st, unsigned int& cnt) {
     st = 0;
     cnt = 0;
     if (cidx < ncell) {
-        const int iz = cidx % nz, t = cidx / nz, iy = t % ny, ix = t / ny;
+        const int t = (int)(((float)cidx + 0.5f) * rnz), iz = cidx - t * nz;
+        const int ix = (int)(((float)t + 0.5f) * rny), iy = t - ix * ny;
         const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
         const float c = g.cell;
         const float bx0 = (float)cx * c, by0 = (float)cy * c, bz0 = (float)cz * c;
@@ -133,12 +136,13 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
     const int z0 = (int)floorf((qz - lim) * ic), z1 = (int)floorf((qz + lim) * ic);
     const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
     const int ncell = nx * ny * nz;
+    const float rny = 1.f / (float)ny, rnz = 1.f / (float)nz;
     int epoch = cs->epoch;
     bool streamed = true;
     if (ncell <= 128) {
         unsigned int st0, cnt0, st1 = 0, cnt1 = 0;
-        cand_lookup(g, x0, y0, z0, ny, nz, ncell, lane, qx, qy, qz, lim, st0, cnt0);
-        if (ncell > 64) cand_lookup(g, x0, y0, z0, ny, nz, ncell, 64 + lane, qx, qy, qz, lim, st1, cnt1);
+        cand_lookup(g, x0, y0, z0, ny, nz, rny, rnz, ncell, lane, qx, qy, qz, lim, st0, cnt0);
+        if (ncell > 64) cand_lookup(g, x0, y0, z0, ny, nz, rny, rnz, ncell, 64 + lane, qx, qy, qz, lim, st1, cnt1);
         int tot0, tot1 = 0;
         const int off0 = wave_excl_scan((int)cnt0, tot0);
         const int off1 = ncell > 64 ? wave_excl_scan((int)cnt1, tot1) : 0;
@@ -156,7 +160,7 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
     } else {
         for (int base = 0; base < ncell; base += 64) {
             unsigned int st, cnt;
-            cand_lookup(g, x0, y0, z0, ny, nz, ncell, base + lane, qx, qy, qz, lim, st, cnt);
+            cand_lookup(g, x0, y0, z0, ny, nz, rny, rnz, ncell, base + lane, qx, qy, qz, lim, st, cnt);
             int total;
             const int off = wave_excl_scan((int)cnt, total);
             if (total == 0) continue;

@@ -70,6 +70,7 @@ struct LidarOdometry::Lookahead {
     PointCloudXYZ kps, iss;
     std::vector<uint32_t> words;
     float ms[3] = {0.f, 0.f, 0.f};  // extract, iss, describe (worker-thread wall time)
+    bool external = false;  // another context's extraction (setSrcFrameExtracted): no normals state here
 };
 
 LidarOdometry::LidarOdometry()
@@ -121,8 +122,9 @@ void LidarOdometry::joinAhead() {
 // (include/bshot_bits.h:59) past the state the sweep actually described next must start from
 void LidarOdometry::dropReady() {
     if (!ready_) return;
+    const bool external = ready_->external;  // another context's record: nothing to restore here
     ready_.reset();
-    check(bsh::ctx_normals_restore(ctx_), "restore normals");
+    if (!external) check(bsh::ctx_normals_restore(ctx_), "restore normals");
 }
 
 void LidarOdometry::check(int rc, const char* where) {
@@ -169,6 +171,41 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
     src_dev_ = d_xyz;
     src_n_ = n;
     check(bshot_set_cloud_device(ctx_, d_xyz, n), "setSrcFrameDevice");
+}
+
+void LidarOdometry::setSrcFrameExtracted(Frame::Ptr src, std::shared_ptr<const Extracted> ex) {
+    if (!ex) throw std::runtime_error("setSrcFrameExtracted: no record");
+    joinAhead();
+    dropReady();
+    auto la = std::make_shared<Lookahead>();
+    la->external = true;
+    la->d_xyz = reinterpret_cast<const float*>(ex.get());  // the record's identity, matched below
+    la->n = ex->n_points;
+    la->nv = ex->n_valid;
+    la->kidx.resize(ex->kps.size());  // only its size is read (the keypoint count)
+    la->kr = ex->ratios;
+    la->kps = ex->kps;
+    la->iss = ex->iss;
+    la->words = ex->words;
+    if (la->kr.size() != la->kps.size() || la->words.size() != 11 * la->kps.size())
+        throw std::runtime_error("setSrcFrameExtracted: inconsistent record");
+    ready_ = la;
+    src_ = src;
+    src_pc_.clear();
+    src_dev_ = la->d_xyz;
+    src_n_ = la->n;
+}
+
+LidarOdometry::Extracted LidarOdometry::extracted() const {
+    Extracted e;
+    e.n_points = stats_.n_points;
+    e.n_valid = stats_.n_valid_ratios;
+    e.kps = cloud1_kps_;
+    e.iss = isskps_src;
+    e.ratios = seg_ratios_;
+    e.words.resize(11 * cloud1_bshot_.size());
+    for (size_t i = 0; i < cloud1_bshot_.size(); ++i) bits_to_words(cloud1_bshot_[i].bits, &e.words[11 * i]);
+    return e;
 }
 
 void LidarOdometry::prefetchFrameDevice(const float* d_xyz, int n) {
@@ -400,8 +437,9 @@ void LidarOdometry::computeDescriptors() {
             desc->push_back(cloud1_bshot_[i].bits);
         }
         src_->setDescriptors(desc);
+        const bool external = ready_->external;
         ready_.reset();
-        bsh::ctx_normals_discard(ctx_);  // adopted: its normals are the state to continue from
+        if (!external) bsh::ctx_normals_discard(ctx_);  // adopted: its normals are the state to continue from
         stats_.host_ms[2] = (float)t_d.toc();
         return;
     }

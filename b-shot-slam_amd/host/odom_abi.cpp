@@ -72,7 +72,22 @@ void write_metrics(bshot_odom* o, const bshot_frame_stats& s, double wall_ms) {
     std::fflush(o->metrics);
 }
 
-int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_frame_stats* st) {
+// the lookahead set by bshot_odom_set_next[2]_device: the next sweep's grids/SR/ISS (side stream)
+// and top-K/describe (worker thread) run while this one is matched, RANSAC-gated, ICP-refined and
+// merged into the map (or, extracting only, packed)
+void start_lookahead(bshot_odom* o) {
+    myslam::LidarOdometry& lo = *o->lo;
+    if (o->next_d) {
+        lo.prefetchFrameDevice(o->next_d, o->next_n);
+        o->next_d = nullptr;
+        if (o->next2_d) lo.queueFrameDevice(o->next2_d, o->next2_n);
+    }
+    o->next2_d = nullptr;
+}
+
+// ex: another context's extraction of this sweep (bshot_odom_process_record), else the cloud
+int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_frame_stats* st,
+              std::shared_ptr<const myslam::LidarOdometry::Extracted> ex = nullptr) {
     const auto t0 = std::chrono::steady_clock::now();
     myslam::LidarOdometry& lo = *o->lo;
     myslam::Frame::Ptr f = myslam::Frame::createFrame();
@@ -82,18 +97,12 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
         f->setPointCloud(pc);
     }
     if (!lo.isInitial()) lo.passSrc2Ref();
-    if (xyz) lo.setSrcFrame(f);
+    if (ex) lo.setSrcFrameExtracted(f, ex);
+    else if (xyz) lo.setSrcFrame(f);
     else lo.setSrcFrameDevice(f, d_xyz, n);
     lo.extractKeypoints();
     lo.computeDescriptors();
-    if (o->next_d) {
-        // the next sweep's grids/SR/ISS (side stream) and top-K/describe (worker thread) run while
-        // this one is matched, RANSAC-gated, ICP-refined and merged into the map
-        lo.prefetchFrameDevice(o->next_d, o->next_n);
-        o->next_d = nullptr;
-        if (o->next2_d) lo.queueFrameDevice(o->next2_d, o->next2_n);
-    }
-    o->next2_d = nullptr;
+    start_lookahead(o);
     lo.featureMatching();
     lo.evaluateEstimation();
     lo.poseEstimation();
@@ -254,6 +263,67 @@ int bshot_odom_gpu_replica_query(bshot_odom* o, int replica, const float pos[3],
     if (!o || !pos || !xyz || !bits) return BSHOT_EINVAL;
     bshot_ctx* c = o->lo->context();
     return bsh::gmap_replica_query(c, replica, pos, range, c->opt_gpu_map == 2, xyz, bits, cap);
+}
+
+// frame-sharded single sequence: record layout (floats): [0] magic, [1] n_points, [2] n_valid,
+// [3] k, [4] n_iss (int bits), [5..7] 0; k x 3 keypoints, k ratios, k x 11 descriptor words (bit
+// patterns), n_iss x 3 ISS points
+static constexpr int kRecMagic = 0x42534852;  // "RHSB"
+static constexpr int kRecHdr = 8;
+
+int bshot_odom_extract_device(bshot_odom* o, const float* d_xyz, int n, float* rec, int cap) {
+    if (!o || n < 0 || (n > 0 && !d_xyz) || cap < 0 || (cap > 0 && !rec)) return BSHOT_EINVAL;
+    int len = 0;
+    const int rc = guard(o, [&]() {
+        myslam::LidarOdometry& lo = *o->lo;
+        myslam::Frame::Ptr f = myslam::Frame::createFrame();
+        lo.setSrcFrameDevice(f, d_xyz, n);
+        lo.extractKeypoints();
+        lo.computeDescriptors();
+        start_lookahead(o);
+        const myslam::LidarOdometry::Extracted e = lo.extracted();
+        const int k = (int)e.kps.size(), ni = (int)e.iss.size();
+        len = kRecHdr + 15 * k + 3 * ni;
+        if (len > cap) return;
+        const int hdr[kRecHdr] = {kRecMagic, e.n_points, e.n_valid, k, ni, 0, 0, 0};
+        std::memcpy(rec, hdr, sizeof(hdr));
+        float* p = rec + kRecHdr;
+        if (k) std::memcpy(p, e.kps[0].v, sizeof(float) * 3 * k);
+        p += 3 * k;
+        if (k) std::memcpy(p, e.ratios.data(), sizeof(float) * k);
+        p += k;
+        if (k) std::memcpy(p, e.words.data(), sizeof(uint32_t) * 11 * k);
+        p += 11 * k;
+        if (ni) std::memcpy(p, e.iss[0].v, sizeof(float) * 3 * ni);
+    });
+    if (rc < 0) return rc;
+    return len > cap ? -len : len;
+}
+
+int bshot_odom_process_record(bshot_odom* o, const float* rec, int len, bshot_frame_stats* st) {
+    if (!o || !rec || len < kRecHdr) return BSHOT_EINVAL;
+    int hdr[kRecHdr];
+    std::memcpy(hdr, rec, sizeof(hdr));
+    const int k = hdr[3], ni = hdr[4];
+    if (hdr[0] != kRecMagic || k < 0 || ni < 0 || len != kRecHdr + 15 * k + 3 * ni) {
+        o->err = "bshot_odom_process_record: not an extraction record";
+        return BSHOT_EINVAL;
+    }
+    auto e = std::make_shared<myslam::LidarOdometry::Extracted>();
+    e->n_points = hdr[1];
+    e->n_valid = hdr[2];
+    const float* p = rec + kRecHdr;
+    e->kps.resize(k);
+    if (k) std::memcpy(&e->kps[0][0], p, sizeof(float) * 3 * k);
+    p += 3 * k;
+    e->ratios.assign(p, p + k);
+    p += k;
+    e->words.resize(11 * (size_t)k);
+    if (k) std::memcpy(e->words.data(), p, sizeof(uint32_t) * 11 * k);
+    p += 11 * k;
+    e->iss.resize(ni);
+    if (ni) std::memcpy(&e->iss[0][0], p, sizeof(float) * 3 * ni);
+    return guard(o, [&]() { run_frame(o, nullptr, nullptr, e->n_points, st, e); });
 }
 
 int bshot_odom_drain(bshot_odom* o) {

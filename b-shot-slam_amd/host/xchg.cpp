@@ -223,8 +223,8 @@ int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self, int s
         if ((x->log_entries.size() + 1) * img > x->log_cap) {
             if ((rc = replay_log(c, x))) return rc;
             if (img > x->log_cap) {
-                size_t want = (size_t)256 << 20;  // floats: 1 GiB
-                if (const char* v = std::getenv("BSHOT_XCHG_LOG_MB")) want = (size_t)std::max(1L, std::atol(v)) << 18;
+                size_t want = (size_t)256 << 20;  // floats: 1 GiB (BSHOT_XCHG_LOG_KB: tests of the full-log path)
+                if (const char* v = std::getenv("BSHOT_XCHG_LOG_KB")) want = (size_t)std::max(1L, std::atol(v)) << 8;
                 if (want < 4 * img) want = 4 * img;
                 if (x->inserts_queued) (void)hipEventSynchronize(x->ev_inserted);
                 if (x->log) (void)hipFree(x->log);

@@ -87,6 +87,10 @@ def parse():
     ap.add_argument("--map-sync", action="store_true",
                     help="wait for every GPU map insert and read the map size back per sweep (odometry_test never "
                          "reads it; default: the insert stays stream-ordered before the next sweep's map query)")
+    ap.add_argument("--shard-frames", action="store_true",
+                    help="N > 1: ONE sequence over the ranks (BASELINE config 3 scaled, strong scaling): ranks 1..N-1 "
+                         "extract every (N-1)-th sweep (A0-A7 + ISS) and send its record to rank 0, which runs the "
+                         "chain (matching, RANSAC, ICP, map) in sweep order")
     ap.add_argument("--from-lasers", action="store_true",
                     help="each sweep starts as HBM-resident laser returns and runs the GPU preprocessor "
                          "(SURVEY 8f row 3: range image, ground + occlusion removal) before the odometry")
@@ -108,6 +112,99 @@ def spawn_ranks(a):
     return subprocess.call(cmd, env=env)
 
 
+def run_shard(a, json_out, rank, world, local, dist, torch):
+    """--shard-frames: one synthetic sequence (seed 42) over `world` ranks. Rank r >= 1 extracts the
+    sweeps f with f mod (world - 1) == r - 1 (bshot_odom_extract_device, with its own lookahead over
+    its sweeps) and sends each record (K x 60 B + ISS points) to rank 0 over a gloo group; rank 0 runs
+    the chain half on the records in sweep order (bshot_odom_process_record). value = timed sweeps /
+    the max over ranks of the time from the shared start barrier to each rank's last sweep."""
+    dev = torch.device("cuda", local)
+    g = dist.new_group(backend="gloo")
+    W = world - 1
+    params = bshot_py.default_params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
+    nframes = a.warmup + a.steps
+    odo = bshot_py.Odometry(device=local, params=params)
+    odo.set_option("map_sync", 0)
+    stats = []
+    npts = 0
+    if rank == 0:
+        def recv(f):
+            src = 1 + f % W
+            ln = torch.zeros(1, dtype=torch.int64)
+            dist.recv(ln, src, group=g, tag=f)
+            buf = torch.empty(int(ln.item()), dtype=torch.float32)
+            dist.recv(buf, src, group=g, tag=f)
+            return buf.numpy()
+        for f in range(a.warmup):
+            odo.process_record(recv(f))
+        dist.barrier(group=g)
+        t0 = time.perf_counter()
+        for f in range(a.warmup, nframes):
+            st = odo.process_record(recv(f))
+            stats.append(st)
+            npts += st.n_points
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+    else:
+        mine = [f for f in range(nframes) if f % W == rank - 1]
+        frames = {}
+        for f in mine:
+            pc, _ = bshot_py.synth_sweep(f, sensor=a.sensor, seed=42)
+            frames[f] = torch.from_numpy(pc).to(dev)
+        torch.cuda.synchronize(dev)
+        pending = []
+
+        def extract(i):
+            f = mine[i]
+            if i + 1 < len(mine):
+                nx = frames[mine[i + 1]]
+                odo.set_next_device(nx.data_ptr(), int(nx.shape[0]))
+            rec = torch.from_numpy(odo.extract_device(frames[f].data_ptr(), int(frames[f].shape[0])))
+            ln = torch.tensor([rec.numel()], dtype=torch.int64)
+            pending.append((dist.isend(ln, 0, group=g, tag=f), dist.isend(rec, 0, group=g, tag=f), ln, rec))
+
+        nw = sum(1 for f in mine if f < a.warmup)
+        for i in range(nw):
+            extract(i)
+        dist.barrier(group=g)
+        t0 = time.perf_counter()
+        for i in range(nw, len(mine)):
+            extract(i)
+        for w1, w2, _, _ in pending:
+            w1.wait()
+            w2.wait()
+        odo.drain()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+    el_max = float(t.item())
+    if rank == 0:
+        hm = np.mean([list(s.host_ms) for s in stats], axis=0)
+        line = {
+            "metric": "Velodyne-64 sweeps/sec (extract+match+ICP)",
+            "value": round(a.steps / el_max, 3),
+            "unit": "sweeps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el_max / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{['HDL-64', 'VLP-128', 'HDL-32E'][a.sensor]} synthetic sequence (one), "
+                                   f"{int(npts / max(1, len(stats)))} pts/sweep, K={a.keypoints}, SHOT r={a.shot_radius:g} mm, "
+                                   "full extract+describe+match+RANSAC+ICP+map per sweep",
+                       "keypoints": a.keypoints, "parallelism": f"frame-sharded: extract x{W} ranks, chain on rank 0"},
+            "host_ms_per_sweep": dict(zip(bshot_py.FrameStats.HOST_PHASES, np.round(hm, 3).tolist())),
+        }
+        print(json.dumps(line), file=json_out, flush=True)
+    odo.close()
+    dist.destroy_process_group()
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -127,10 +224,18 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
+        ndev = torch.cuda.device_count()
+        if 0 < ndev < world:
+            # a rehearsal on fewer GPUs than ranks (ranks share devices): flow only, no scaling claim
+            print(f"bench.py: {world} ranks on {ndev} GPU(s): ranks share devices", file=sys.stderr)
+            local %= ndev
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import torch
 
+    if a.shard_frames and world > 1:
+        run_shard(a, json_out, rank, world, local, dist, torch)
+        return
     dev = torch.device("cuda", local)
     params = bshot_py.default_params(num_keypoints=a.keypoints, shot_radius=a.shot_radius)
     # steady state at both edges of the timed region: the last warm-up sweep starts the first timed

@@ -30,3 +30,6 @@ for f in glob.glob(o + "/r04pmc_*/**/*counter_collection.csv", recursive=True):
 for n, d in agg.items():
     print(n, {k: round(sum(v) / len(v)) for k, v in d.items()})
 PY
+cd $R
+# frame-sharded single sequence, rehearsed with 3 ranks sharing the box's GPU (flow, not scaling)
+timeout -k 10 300 python bench.py --gpus 3 --shard-frames --steps 40 --warmup 6 > $O/r04_shard3.json 2> $O/r04_shard3.err && cat $O/r04_shard3.json

@@ -72,6 +72,21 @@ class LidarOdometry {
     void setEvaluateICP(bool eval_icp) { evaluate_icp_ = eval_icp; }
     void setRunICP(bool run_icp) { run_icp_ = run_icp; }
 
+    // extension (frame-sharded single sequence): the extraction half of a sweep
+    // (A0-A7 + ISS: extractKeypoints + computeDescriptors) as data, so one context can extract a
+    // sweep and another -- another GPU's -- run the chain on it
+    struct Extracted {
+        int n_points = 0, n_valid = 0;
+        PointCloudXYZ kps, iss;
+        std::vector<float> ratios;
+        std::vector<uint32_t> words;  // 11 per keypoint (bits_to_words)
+    };
+    // the current sweep's extraction half (after computeDescriptors)
+    Extracted extracted() const;
+    // adopt another context's extraction of this sweep: the next extractKeypoints/computeDescriptors
+    // take it as computed here (matching, RANSAC, ICP and the map update then run as usual)
+    void setSrcFrameExtracted(Frame::Ptr src, std::shared_ptr<const Extracted> ex);
+
     // extensions (not in the reference)
     const bshot_frame_stats& lastStats() const { return stats_; }
     const bshot_params& params() const { return prm_; }

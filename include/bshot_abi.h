@@ -239,6 +239,18 @@ int bshot_odom_gpu_replica_size(bshot_odom* o, int replica);
 int bshot_odom_gpu_replica_insert(bshot_odom* o, int replica, const float* rec, int n);
 int bshot_odom_gpu_replica_query(bshot_odom* o, int replica, const float pos[3], float range, float* xyz,
                                  uint32_t* bits, int cap);
+/* frame-sharded single sequence (extension; BASELINE config 3 over several GPUs):
+ * a sweep's extraction half (A0-A7 + ISS: extractKeypoints + computeDescriptors,
+ * src/lidar_odometry.cpp:51-184) on one context, packed as a record of floats -- [0] magic, [1]
+ * n_points, [2] n_valid, [3] k, [4] n_iss (int bits), [5..7] 0, then k x 3 keypoints, k ratios, k x 11
+ * descriptor words (bit patterns), n_iss x 3 ISS points -- and the chain half (A8-A13,
+ * :186-376) of the sequence on another, in sweep order. The set_next[2]_device lookahead applies to
+ * the extracting context. Returns the record length in floats, or -length when cap is too small.
+ * The reference's persistent normals array (include/bshot_bits.h:58-87) carries state from one
+ * describe to the next only through a sweep with fewer keypoints than the one after it; across
+ * sweeps with K keypoints each, records from independent contexts equal the sequential ones. */
+int bshot_odom_extract_device(bshot_odom* o, const float* d_xyz, int n, float* rec, int cap);
+int bshot_odom_process_record(bshot_odom* o, const float* rec, int len, bshot_frame_stats* st);
 /* wait for the lookahead work started by the last process call (the prefetched sweep's describe on
  * its worker thread, the queued sweep's launches and top-K) to be issued and finished; the results
  * stay ready for the next process call. Extension (no reference counterpart). */

@@ -77,6 +77,35 @@ def test_exchange_sim_peers_replicas():
         x.close()
 
 
+def test_exchange_log_replayed_in_order(monkeypatch):
+    """The exchange logs every gathered offer in HBM and indexes the replicas only when one is read:
+    nine sweeps' offers accumulate (a 200 KB log holds four: it is replayed into the replicas three
+    times on the way), and the replica read before the last sweep must equal the own map the last
+    sweep's matching reads (entries, libstdc++ block order, descriptors)."""
+    monkeypatch.setenv("BSHOT_XCHG_LOG_KB", "200")
+    uid = bshot_py.Exchange.unique_id()
+    x = bshot_py.Exchange(uid, 1, 0, 0, K)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+    try:
+        frames = _frames(n=10)
+        prev = None
+        for f, xyz in enumerate(frames):
+            rq = od.gpu_replica_query(0, prev[0][:3, 3]) if f == len(frames) - 1 else None
+            st = od.process(xyz)
+            if rq is not None:
+                tx, tb = od.target()
+                m = len(tx) - prev[1]
+                assert m == len(rq[0]) and m > 0
+                assert np.array_equal(_u(tx[:m]), _u(rq[0])) and np.array_equal(tb[:m], rq[1])
+            else:
+                od.exchange(x, include_self=True)
+            prev = (np.array(st.pose, np.float32).reshape(4, 4), st.n_keypoints)
+        assert od.gpu_replica_size(0) > 0
+    finally:
+        od.close()
+        x.close()
+
+
 def test_xseq_targets_append_replicas():
     uid = bshot_py.Exchange.unique_id()
     x = bshot_py.Exchange(uid, 1, 0, 0, K)
