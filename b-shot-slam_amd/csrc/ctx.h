@@ -140,6 +140,8 @@ struct bshot_ctx {
     int opt_map_sync = 1;       // GPU map insert: wait for it and report the map size per sweep (0: stream-ordered, size -1)
     int opt_host_map_log = 1;   // LidarOdometry keeps the GPU map's insert log for the host Map view (bshot_odom: 0)
     int opt_normals_seg = 1;    // normals from the SHOT neighbour lists when normal_radius == shot_radius
+    int opt_diag_skip_icp = 0;  // diagnostic only: ICP returns the identity without running (never in a bench line)
+    int opt_rank_wg = 2;        // SHOT rank kernel: 0 wave per 64-rank chunk, 1 workgroup per keypoint, 2 by neighbourhood size
     int opt_sr_start = 40;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
 
@@ -213,15 +215,21 @@ struct bshot_ctx {
     void hmark(const char* name);
 
     // icp
+    PinBuf<bsh::IcpSync> p_isync;        // ICP host loop: host <-> kernel hand-over (coherent)
+    PinBuf<unsigned long long> p_ibest;  // ICP host loop: NN keys, two iterations' worth (coherent)
+    PinBuf<int> p_idone;                 // ICP host loop: per-workgroup completion flags (coherent)
+    PinBuf<float> p_src2;                // ICP host loop: the current positions after a restart
+    int opt_icp_device = 0;        // 1: PCL's ICP loop entirely on the device (k_icp_run); 0: the host's float Umeyama
+    int opt_icp_host_delay_ms = 0;  // tests: the host loop sleeps this long before releasing iteration 3
     PinBuf<bsh::IcpOut> p_iout;  // ICP result: composed transform, iteration count, seq (coherent)
     int icp_seq = 0;             // seq of the last ICP call
     DBuf<float4> ipos, ilcen;    // ICP loop: current source positions, list centres (xyz) + radii (w)
-    DBuf<int> iqueue;            // ICP loop: sources queued for the grid search
-    DBuf<float> irec;            // ICP loop: Umeyama terms in HBM when the sources exceed the LDS staging
+    DBuf<float> irec;            // ICP loop: the iteration's Umeyama records (7 x ns floats)
+    DBuf<bsh::IcpCtl> ictl;      // ICP loop state
+    DBuf<unsigned int> isync;    // ICP loop: arrival counter, released iteration
     DBuf<float4> ilst;  // ICP candidate lists (ICP_LIST_CAP per source)
     DBuf<float> ilsd;   // their entries' distances from the list centre (ascending)
     DBuf<int> ilcnt;    // their counts (-1: none)
-    DBuf<float> ilrad;  // their radii
     int opt_ransac_dev = 1;  // 1: RANSAC hypotheses scored on the GPU (bshot_ransac_dev); 0: on the host
     int opt_topk_thread = 1;   // LidarOdometry: top-K of a queued sweep on its own host thread once its SR lands
     int opt_pre_fast = 1;  // preprocessor: one 32-bit sort for azimuth-ordered lasers with tabled verticals

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <thread>
 #include <tuple>
 #include <mutex>
 #include <string>
@@ -391,6 +392,14 @@ int ctx_normals_restore(bshot_ctx* c) {
 void ctx_normals_discard(bshot_ctx* c) { c->normals_snap_size = -1; }
 
 // keypoints already in c->kps (device, k x 3)
+// the SHOT rank kernel for k keypoints with about `total` neighbours: the workgroup-per-keypoint
+// kernel streams large neighbourhoods (config 5: ~28k per keypoint, 2.0 -> ? ms), the wave-per-chunk
+// kernel has more parallelism for small ones (config 2: ~7.8k, 0.15 vs 0.39 ms in the pipeline)
+static int rank_wg_for(const bshot_ctx* c, int k, long long total) {
+    if (c->opt_rank_wg != 2) return c->opt_rank_wg;
+    return k > 0 && total / k > 16384 ? 1 : 0;
+}
+
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > 512)
         return c->fail("normal_max_nn must be in [1, 512]", BSHOT_EINVAL);
@@ -462,6 +471,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
         A.bstart = c->sbst.p;
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
+        A.rank_wg = rank_wg_for(c, k, c->seg_hint);
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
@@ -528,6 +538,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.shot = c->shot.p; A.bits = c->bits.p; A.err = c->errw.p;
     A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
+    A.rank_wg = rank_wg_for(c, k, total);
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -642,7 +653,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
     c->icp_prep_tgt = nullptr;
     bg::Mat4f fin = bg::Mat4f::identity();
     int it = 0;
-    if (ns >= 3 && nt > 0) {
+    if (ns >= 3 && nt > 0 && !c->opt_diag_skip_icp) {
         // the source (host, already moved by T_est) in pinned memory, read there by the kernels; the
         // targets are in HBM already (gmap) or go through pinned staging
         HIPCHK(c->p_src.ensure(3 * (size_t)ns), "alloc pinned src");
@@ -661,50 +672,171 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         HIPCHK(c->ilst.ensure((size_t)ICP_LIST_CAP * ns), "alloc icp lists");
         HIPCHK(c->ilsd.ensure((size_t)ICP_LIST_CAP * ns), "alloc icp list distances");
         HIPCHK(c->ilcnt.ensure(ns), "alloc icp list counts");
-        HIPCHK(c->ilrad.ensure(ns), "alloc icp list radii");
         const DevGrid* g4[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
-        // PCL's loop on the device (csrc/icp.hip): k_icp_lists finds iteration 0's exact 1-NN and every
-        // source's candidate list, k_icp_loop runs the rest in one workgroup (float Umeyama, the
-        // convergence test, the step, the next keys) and writes the composed transform and the
-        // iteration count to coherent pinned memory, seq last. The host waits once.
-        HIPCHK(c->ibest.ensure(ns), "alloc icp keys");
-        HIPCHK(c->ipos.ensure(ns), "alloc icp positions");
         HIPCHK(c->ilcen.ensure(ns), "alloc icp list centres");
-        HIPCHK(c->iqueue.ensure(ns), "alloc icp queue");
-        const size_t nrec = icp_loop_rec_floats(ns);
-        if (nrec) HIPCHK(c->irec.ensure(nrec), "alloc icp terms");
-        c->p_iout.coherent = true;
-        HIPCHK(c->p_iout.ensure(1), "alloc icp result");
-        IcpOut* out = c->p_iout.p;
-        const int seq = ++c->icp_seq;
         const float* d_src0 = c->p_src.p;
-        const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
-        HIPCHK(launch_icp_lists(d_src0, ns, g4, c->itgt.p, nt, ICP_LIST_CAP, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p,
-                                c->ibest.p, c->stream),
-               "icp lists");
-        HIPCHK(launch_icp_loop(d_src0, ns, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilrad.p, ICP_LIST_CAP, g4, c->itgt.p, nt,
-                               max_iter, c->ibest.p, c->ipos.p, c->ilcen.p, c->iqueue.p, nrec ? c->irec.p : nullptr, out,
-                               seq, c->stream),
-               "icp loop");
-        c->stage_end(sg14);
-        // spin briefly on seq (the loop takes ~0.1-0.3 ms), then block on the stream: a slow GPU
-        // (contention, a profiler) only makes the call wait longer, it never fails it
-        const long long t_a = ns_now();
-        bool seen = false;
-        for (unsigned spins = 0;; ++spins) {
-            if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) == seq) { seen = true; break; }
-            if ((spins & 255) == 0 && ns_now() - t_a > 5000000ll) break;
-            __builtin_ia32_pause();
-        }
-        if (!seen) {
+        if (c->opt_icp_device) {
+            // PCL's loop on the device (csrc/icp.hip): k_icp_lists finds iteration 0's exact 1-NN and
+            // every source's candidate list, then one persistent k_icp_run iterates (per iteration:
+            // every source's step and NN, then the float Umeyama and the convergence test on the last
+            // workgroup to arrive); the stopping step writes the composed transform and the iteration
+            // count to coherent pinned memory, seq last. The host waits once.
+            HIPCHK(c->ipos.ensure(ns), "alloc icp positions");
+            HIPCHK(c->irec.ensure(7 * (size_t)ns), "alloc icp records");
+            HIPCHK(c->ictl.ensure(1), "alloc icp state");
+            HIPCHK(c->isync.ensure(2), "alloc icp sync");
+            c->p_iout.coherent = true;
+            HIPCHK(c->p_iout.ensure(1), "alloc icp result");
+            IcpOut* out = c->p_iout.p;
+            const int seq = ++c->icp_seq;
+            const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
+            HIPCHK(launch_icp(d_src0, ns, c->ilst.p, c->ilsd.p, c->ilcnt.p, ICP_LIST_CAP, g4, c->itgt.p, nt, max_iter,
+                              c->ipos.p, c->ilcen.p, c->irec.p, c->ictl.p, c->isync.p, out, seq, c->stream),
+                   "icp launch");
+            c->stage_end(sg14);
+            // spin briefly on seq, then block on the stream: a slow GPU (contention, a profiler) only
+            // makes the call wait longer, it never fails it
+            const long long t_a = ns_now();
+            bool seen = false;
+            for (unsigned spins = 0;; ++spins) {
+                if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) == seq) { seen = true; break; }
+                if ((spins & 255) == 0 && ns_now() - t_a > 5000000ll) break;
+                __builtin_ia32_pause();
+            }
+            if (!seen) {
+                HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
+                if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) != seq)
+                    return c->fail("icp: the loop kernel finished without its result", BSHOT_EHIP);
+            }
+            c->work[2] += ns_now() - t_a;  // host wait for the device loop
+            std::memcpy(fin.m, out->T, sizeof(fin.m));
+            it = out->iters;
+            c->work[5] += it;
+        } else {
+            // PCL's loop on the host (float Umeyama, convergence), the exact 1-NN of every iteration on
+            // the device: one launch for iteration 0 (keys + every source's candidate list) and one
+            // persistent launch for the rest, handed over through coherent pinned memory: the host
+            // releases iteration j with its step transform, the kernel stores the keys
+            // (double-buffered by iteration parity) and flags them done. One stream sync per call.
+            std::vector<float> cur(src, src + 3 * (size_t)ns), tb(3 * (size_t)ns);
+            c->p_isync.coherent = true;
+            c->p_ibest.coherent = true;
+            HIPCHK(c->p_isync.ensure(1), "alloc icp sync");
+            HIPCHK(c->p_ibest.ensure(2 * (size_t)ns), "alloc icp keys");
+            const int nb0 = icp_lists_blocks(ns), nb1 = icp_iter_blocks(ns);
+            c->p_idone.coherent = true;
+            HIPCHK(c->p_idone.ensure((size_t)nb0 + nb1), "alloc icp flags");
+            HIPCHK(c->p_src2.ensure(3 * (size_t)ns), "alloc pinned icp positions");
+            int* done0 = c->p_idone.p;
+            int* done1 = c->p_idone.p + nb0;
+            std::memset(c->p_idone.p, 0, sizeof(int) * ((size_t)nb0 + nb1));
+            // host copy of the targets (the Umeyama step's pairs), before the persistent kernel is queued
+            const float* tg = tgt;
+            std::vector<float> h_tgt;
+            if (!tg) {
+                h_tgt.resize(3 * (size_t)nt);
+                HIPCHK(c->p_tgt.ensure(3 * (size_t)nt), "alloc pinned tgt");
+                HIPCHK(kcopy(c->p_tgt.p, d_tgt, sizeof(float) * 3 * nt, c->stream), "D2H icp targets");
+                HIPCHK(hipStreamSynchronize(c->stream), "sync icp targets");
+                std::memcpy(h_tgt.data(), c->p_tgt.p, sizeof(float) * 3 * nt);
+                tg = h_tgt.data();
+            }
+            IcpSync* sy = c->p_isync.p;
+            std::memset(sy, 0, sizeof(IcpSync));
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            const int sg14 = c->stage_begin(BSHOT_STAGE_ICP);
+            HIPCHK(launch_icp_lists_host(d_src0, ns, g4, c->itgt.p, nt, ICP_LIST_CAP, c->ilst.p, c->ilsd.p, c->ilcnt.p,
+                                         c->ilcen.p, c->p_ibest.p, done0, c->stream),
+                   "icp lists");
+            HIPCHK(launch_icp_iterations(d_src0, ns, 1, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilcen.p, ICP_LIST_CAP, g4,
+                                         c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p, c->stream),
+                   "icp iterations");
+            c->stage_end(sg14);
+            auto release = [&](int go) { __atomic_store_n(&sy->go, go, __ATOMIC_RELEASE); };
+            int j_lists = 0;  // the iteration whose keys the lists kernel delivers (0, or a restart's)
+            // iteration j's keys are complete when every workgroup's flag says so. false: the device
+            // went idle without them (its kernel outwaited a slow host and exited): the
+            // caller restarts the iterations from the current positions. A busy GPU is waited for.
+            auto wait_keys = [&](int j) -> bool {
+                const int nb = j == j_lists ? nb0 : nb1;
+                int* flags = j == j_lists ? done0 : done1;
+                const int want = j == j_lists ? 1 : j;
+                const long long t0 = ns_now();
+                unsigned spins = 0;
+                for (int w = 0; w < nb; ++w) {
+                    while (__atomic_load_n(&flags[w], __ATOMIC_ACQUIRE) < want) {
+                        if ((++spins & 1023) == 0 && ns_now() - t0 > 2000000ll &&
+                            hipStreamQuery(c->stream) == hipSuccess && __atomic_load_n(&flags[w], __ATOMIC_ACQUIRE) < want)
+                            return false;
+                        __builtin_ia32_pause();
+                    }
+                }
+                return true;
+            };
+            // restart at iteration j from the host's current positions: the lists kernel gives
+            // iteration j's keys (exact 1-NN at cur) and lists around cur; the persistent kernel then
+            // runs iterations j + 1 .. (the NN are exact from any list state, so the keys are unchanged)
+            auto restart = [&](int j) -> int {
+                (void)hipStreamSynchronize(c->stream);
+                std::memcpy(c->p_src2.p, cur.data(), sizeof(float) * 3 * ns);
+                std::memset(c->p_idone.p, 0, sizeof(int) * ((size_t)nb0 + nb1));
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                j_lists = j;
+                ++c->work[3];  // ICP restarts
+                HIPCHK(launch_icp_lists_host(c->p_src2.p, ns, g4, c->itgt.p, nt, ICP_LIST_CAP, c->ilst.p, c->ilsd.p,
+                                             c->ilcnt.p, c->ilcen.p, c->p_ibest.p + (size_t)ns * (j & 1), done0,
+                                             c->stream),
+                       "icp lists (restart)");
+                HIPCHK(launch_icp_iterations(c->p_src2.p, ns, j + 1, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilcen.p,
+                                             ICP_LIST_CAP, g4, c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p,
+                                             c->stream),
+                       "icp iterations (restart)");
+                return BSHOT_OK;
+            };
+            double prev_mse = 1.7976931348623157e308;
+            bg::Mat4f Ts = bg::Mat4f::identity();
+            long long tw = ns_now();
+            while (true) {
+                const long long t_a = ns_now();
+                if (!wait_keys(it)) {
+                    if (int rc = restart(it)) return rc;
+                    continue;
+                }
+                const long long t_b = ns_now();
+                c->work[2] += t_b - t_a;              // host wait for the keys
+                if (it > 0) c->work[4] += t_a - tw;  // host step between two waits
+                const unsigned long long* best = c->p_ibest.p + (size_t)ns * (it & 1);
+                for (int i = 0; i < ns; ++i) {
+                    const unsigned j = (unsigned)(best[i] & 0xFFFFFFFFu);
+                    tb[3 * i] = tg[3 * j]; tb[3 * i + 1] = tg[3 * j + 1]; tb[3 * i + 2] = tg[3 * j + 2];
+                }
+                Ts = bg::umeyama<float>(cur.data(), tb.data(), ns);
+                ++it;
+                if (it == 3 && c->opt_icp_host_delay_ms > 0)
+                    std::this_thread::sleep_for(std::chrono::milliseconds(c->opt_icp_host_delay_ms));
+                // the next iteration is released before this one's bookkeeping and convergence test
+                // (PCL decides after the step); if the test stops the loop, its keys are never read
+                if (it < max_iter) {
+                    std::memcpy(sy->T, Ts.m, sizeof(Ts.m));
+                    release(it);
+                }
+                for (int i = 0; i < ns; ++i) bg::xform(Ts, &cur[3 * i], &cur[3 * i]);  // the device applies Ts too
+                fin = bg::mul(Ts, fin);
+                if (it >= max_iter) break;
+                const double cos_angle = 0.5 * (double)(((Ts.m[0] + Ts.m[5]) + Ts.m[10]) - 1.0f);
+                const double tsq = (double)((Ts.m[3] * Ts.m[3] + Ts.m[7] * Ts.m[7]) + Ts.m[11] * Ts.m[11]);
+                if (cos_angle >= 1.0 && tsq <= 0.0) break;
+                double mse = 0;
+                for (int i = 0; i < ns; ++i) mse += (double)__builtin_bit_cast(float, (unsigned)(best[i] >> 32));
+                mse /= (double)ns;
+                if (__builtin_fabs(mse - prev_mse) < 1e-12) break;
+                prev_mse = mse;
+                tw = t_b;
+            }
+            c->work[5] += it;
+            release(-1);  // the persistent kernel's waves exit
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
-            if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) != seq)
-                return c->fail("icp: the loop kernel finished without its result", BSHOT_EHIP);
         }
-        c->work[2] += ns_now() - t_a;  // host wait for the device loop
-        std::memcpy(fin.m, out->T, sizeof(fin.m));
-        it = out->iters;
-        c->work[5] += it;
     }
     std::memcpy(T, fin.m, sizeof(float) * 16);
     *iters = it;
@@ -794,7 +926,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->prep = nullptr;
     bsh::velo_free(c->velo);
     c->velo = nullptr;
-    c->gidx.release(); c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->ilrad.release(); c->p_iout.release(); c->ipos.release(); c->ilcen.release(); c->iqueue.release(); c->irec.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gidx.release(); c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->p_iout.release(); c->p_isync.release(); c->p_ibest.release(); c->p_idone.release(); c->p_src2.release(); c->ipos.release(); c->ilcen.release(); c->irec.release(); c->ictl.release(); c->isync.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
@@ -1051,6 +1183,10 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "map_sync") c->opt_map_sync = value ? 1 : 0;
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
+    else if (k == "icp_device") c->opt_icp_device = value ? 1 : 0;
+    else if (k == "icp_host_delay_ms") c->opt_icp_host_delay_ms = value < 0 ? 0 : value;
+    else if (k == "diag_skip_icp") c->opt_diag_skip_icp = value ? 1 : 0;  // diagnostic: the period without ICP
+    else if (k == "rank_wg") c->opt_rank_wg = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;

@@ -654,9 +654,6 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
 
 namespace bsh {
 
-#ifndef SHOT_RANK_WG
-#define SHOT_RANK_WG 1  // 1: k_shot_rank_wg (workgroup per keypoint); 0: k_shot_rank (wave per chunk)
-#endif
 // part 0: in-bucket rank (sorted segments); 1: LRF; 2: histogram records + ordered apply
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.k <= 0) return hipSuccess;
@@ -666,13 +663,12 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (part == 0) {
         if (A.n_chunks > 0) {
             bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
-#if SHOT_RANK_WG
-            if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s))) return e;
-#else
-            if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
-                                        A.max_blocks)))
+            if (A.rank_wg) {
+                if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s))) return e;
+            } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
+                                             A.max_blocks))) {
                 return e;
-#endif
+            }
         }
         return hipGetLastError();
     }

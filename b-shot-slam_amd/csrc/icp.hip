@@ -9,11 +9,12 @@
 // Iteration 0 (k_icp_lists, a wave per source): the exact 1-NN at the source's starting position
 // q0, and a candidate list: every target within R of q0, R = d0 + {3000, 1500, 750, 350} mm (the
 // largest whose count fits the list capacity; d0 = the NN distance), sorted by distance from q0.
-// The loop (k_icp_loop, one workgroup): each iteration's Umeyama + convergence test, then the sources
-// move rigidly by the step; a source's NN among its list is the global NN whenever
-// dm + |q - q0| < R (with float slack): a target outside the list lies at least R from q0, so at
-// least R - |q - q0| from q, farther than the list's best. Sources failing the test (moved too far,
-// no list, non-finite) take the exact grid search of iteration 0 (a wave each) and get a new list.
+// Iterations (k_icp_step + k_icp_nn per iteration, queued back to back): each iteration's Umeyama
+// + convergence test on one workgroup, then the sources move rigidly by the step; a source's NN
+// among its list is the global NN whenever dm + |q - q0| < R (with float slack): a target outside
+// the list lies at least R from q0, so at least R - |q - q0| from q, farther than the list's best.
+// Sources failing the test (moved too far, no list, non-finite) take the exact grid search of
+// iteration 0 (a wave each) and get a new list.
 // The targets' nested grids (cells 1000, 2000, 4000, 8000 mm) are built once per ICP call, queued
 // ahead of RANSAC (ctx_icp_prepare).
 #include <hip/hip_runtime.h>
@@ -154,290 +155,560 @@ __device__ __forceinline__ void icp_build_list(const IcpGrids& G, CandLds* cs, f
     *R_out = R;
 }
 
+// Hand-over stores to pinned host memory (the host's loop) are system-scope relaxed stores (written
+// through to the host, never held in L2), ordered by waiting for their completion (vmcnt 0, which on
+// gfx9 counts stores) before the flag is written. No release fence: at system scope a fence writes
+// back the XCD's whole L2, tens of us with the lookahead's kernels' dirty lines in it.
+__device__ __forceinline__ void icp_put_key(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void icp_put_flag(int* p, int v) {
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's key stores have completed
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 #define ICP_WAVES 4
+// per-source Umeyama record of an iteration, SoA rows of ns floats in rec: source xyz (the source's
+// current position), its NN target xyz, the NN's d2
+__device__ __forceinline__ void icp_put_rec(float* rec, int ns, int i, float qx, float qy, float qz, float4 t,
+                                            unsigned long long m) {
+    rec[i] = qx;
+    rec[(size_t)ns + i] = qy;
+    rec[2 * (size_t)ns + i] = qz;
+    rec[3 * (size_t)ns + i] = t.x;
+    rec[4 * (size_t)ns + i] = t.y;
+    rec[5 * (size_t)ns + i] = t.z;
+    rec[6 * (size_t)ns + i] = __uint_as_float((unsigned)(m >> 32));
+}
+
+__device__ __forceinline__ void icp_ctl_init(bsh::IcpCtl* ctl) {
+    for (int u = 0; u < 16; ++u) {
+        ctl->fin[u] = (u % 5 == 0) ? 1.f : 0.f;
+        ctl->T[u] = ctl->fin[u];
+    }
+    ctl->prev_mse = 1.7976931348623157e308;
+    ctl->it = 0;
+    ctl->stop = 0;
+}
+
+// iteration 0: the exact 1-NN of every source at its starting position, its candidate list, its
+// Umeyama record and its loop state (position, list centre + radius)
+// rec != null (the device loop): also the records, positions, loop state; best != null (the host's
+// loop): the keys in pinned memory (system-scope stores) and per-workgroup done flags
 __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __restrict__ src0, int ns, IcpGrids G,
                                                               const float4* __restrict__ tgt4, int nt, int cap,
                                                               float4* __restrict__ lst, float* __restrict__ lsd,
-                                                              int* __restrict__ lcnt, float* __restrict__ lrad,
-                                                              unsigned long long* __restrict__ best_out) {
+                                                              int* __restrict__ lcnt, float4* __restrict__ lcen,
+                                                              float4* __restrict__ pos, float* __restrict__ rec,
+                                                              bsh::IcpCtl* ctl, unsigned int* __restrict__ sync,
+                                                              unsigned long long* __restrict__ best, int* done) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     __shared__ CandLds cl[ICP_WAVES];
     __shared__ unsigned long long skl[ICP_WAVES][ICP_LIST_CAP];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     CandLds* cs = &cl[wave];
     cand_init(cs);
+    if (rec && blockIdx.x == 0 && threadIdx.x == 0) {
+        icp_ctl_init(ctl);
+        sync[0] = 0u;
+        sync[1] = 0u;
+    }
     for (int i = blockIdx.x * ICP_WAVES + wave; i < ns; i += gridDim.x * ICP_WAVES) {
         const float qx = src0[3 * i], qy = src0[3 * i + 1], qz = src0[3 * i + 2];
         const unsigned long long m = icp_wave_nn(G, cs, qx, qy, qz, tgt4, nt);
-        if (lane == 0) best_out[i] = m;
         int count;
         float R;
         icp_build_list(G, cs, qx, qy, qz, m, tgt4, lst + i, lsd + i, ns, cap, skl[wave], &count, &R);  // entry e at [e * ns + i]
         if (lane == 0) {
             lcnt[i] = count;
-            lrad[i] = R;
+            lcen[i] = make_float4(qx, qy, qz, R);
+            if (rec) {
+                pos[i] = make_float4(qx, qy, qz, 0.f);
+                icp_put_rec(rec, ns, i, qx, qy, qz, tgt4[(unsigned)(m & 0xFFFFFFFFu)], m);
+            }
+            if (best) icp_put_key(&best[i], m);
         }
         __builtin_amdgcn_wave_barrier();
     }
+    if (done) {
+        __builtin_amdgcn_s_waitcnt(0);  // every wave's key stores have completed
+        __syncthreads();
+        if (threadIdx.x == 0) icp_put_flag(&done[blockIdx.x], 1);
+    }
 }
 
-// The whole of PCL's loop after iteration 0's neighbours, on the device (one launch, one workgroup of
-// ICPL_THREADS): per iteration the float Umeyama of (current sources, their NN targets), PCL's
-// convergence test, then every source moved by the step and its exact 1-NN found for the next
-// iteration. One workgroup keeps every hand-over inside one CU (LDS + __syncthreads): no host round
-// trip, no grid barrier, no cross-XCD coherence traffic, and nothing waits for another workgroup to
-// be scheduled.
-//
-// Umeyama (bm::umeyama_seq<float>, Eigen::umeyama's order): the means are 6 sequential float sums in
-// source order, the cross-covariance 9 sequential sums of (d_r - dm_r)(s_c - sm_c), each sum on its
-// own lane of wave 0 (the sums' own orders are the host's, so the bits are); the per-source terms
-// are staged in LDS as 7 arrays (s xyz, d xyz, d2), centred in place by the whole workgroup between
-// the two passes. PCL's MSE (a sequential double sum of the keys' d2) runs on wave 1 meanwhile.
-// Sources beyond ICPL_CH are staged chunk by chunk from HBM (rec_g) instead.
-//
-// Neighbours: a thread per source scans the source's candidate list (k_icp_lists) while the bound
-// proves the list's best global (dm + |q - q0| < R with float slack); the others are queued and the
-// exact grid search runs on ICPL_SW waves (a wave per queued source), which also rebuilds the
-// source's list around its current position.
-#define ICPL_THREADS 512
-#define ICPL_SW 8      // waves that run the queued grid searches
-#define ICPL_CH 2048   // sources whose Umeyama terms are staged in LDS at once (7 floats each)
-
-__global__ void __launch_bounds__(ICPL_THREADS) k_icp_loop(const float* __restrict__ src0, int ns, float4* lst, float* lsd,
-                                                           int* lcnt, float* lrad, int cap, IcpGrids G,
-                                                           const float4* __restrict__ tgt4, int nt, int max_iter,
-                                                           const unsigned long long* __restrict__ best0,
-                                                           float4* __restrict__ pos, float4* __restrict__ lcen,
-                                                           int* __restrict__ queue, float* __restrict__ rec_g,
-                                                           bsh::IcpOut* out, int seq) {
-    extern __shared__ __attribute__((aligned(16))) float rec[];  // 7 x chs floats
-    __shared__ CandLds cl[ICPL_SW];
-    __shared__ unsigned long long skl[ICPL_SW][ICP_LIST_CAP];
-    __shared__ float sT[16];
-    __shared__ float smean[6];
-    __shared__ float sacc[9];
-    __shared__ double smse;
-    __shared__ int sstop, nq;
-    const int tid = threadIdx.x, lane = lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool big = ns > ICPL_CH;
-    const int chs = big ? ICPL_CH : ((ns + 3) & ~3);  // LDS row stride (16-B aligned rows)
-    if (wave < ICPL_SW) cand_init(&cl[wave]);
-    // record c of source i: LDS row c (small) or HBM row c (big: staged per chunk)
-    auto put = [&](int c, int i, float v) {
-        if (big) rec_g[(size_t)c * ns + i] = v;
-        else rec[c * chs + i] = v;
-    };
-    // iteration 0: the sources as given, the keys of k_icp_lists
-    for (int i = tid; i < ns; i += ICPL_THREADS) {
-        const float x = src0[3 * i], y = src0[3 * i + 1], z = src0[3 * i + 2];
-        pos[i] = make_float4(x, y, z, 0.f);
-        lcen[i] = make_float4(x, y, z, lrad[i]);
-        const unsigned long long m = best0[i];
-        const float4 t = tgt4[(unsigned)(m & 0xFFFFFFFFu)];
-        put(0, i, x); put(1, i, y); put(2, i, z);
-        put(3, i, t.x); put(4, i, t.y); put(5, i, t.z);
-        put(6, i, __uint_as_float((unsigned)(m >> 32)));
+// The host's loop (the default): iterations >= 1 in one persistent launch, a
+// workgroup (one wave) per 64 sources, a lane per source holding its position. For iteration j the
+// wave waits until the host has released it (IcpSync.go >= j after the host's float Umeyama step of
+// iteration j - 1; -1 = stop), moves its source by the step (pcl::transformPointCloud's float
+// expression, as the host's bg::xform), takes the NN among the source's list when the bound proves
+// it global and queues the others for the grid search (which also rebuilds the source's list
+// around its current position), stores the keys in pinned host memory and sets its flag done[w] =
+// j. Its LDS (~4 KB) fits beside a CU the SR kernel fills (7 KB left of 160): the device loop's
+// larger workgroups waited for CUs to drain under the lookahead's load. Every wave exits on go = -1,
+// after max_iter - 1 iterations, or when a wait exceeds ICP_WAIT_TICKS; the host then restarts the
+// iterations from the current positions (ctx_icp).
+#define ICPH_THREADS 64
+#define ICP_WAIT_TICKS 100000000ll  // 1 s at the 100 MHz wall clock: a launch that cannot finish exits
+__global__ void __launch_bounds__(ICPH_THREADS) k_icp_iterations(const float* __restrict__ src0, int ns, int j0,
+                                                                 const float4* lst, const float* lsd,
+                                                                 const int* __restrict__ lcnt,
+                                                                 const float4* __restrict__ lcen, int cap, IcpGrids G,
+                                                                 const float4* __restrict__ tgt4, int nt, int max_iter,
+                                                                 const bsh::IcpSync* sy, int* done,
+                                                                 unsigned long long* best) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
+    __shared__ CandLds cl;
+    __shared__ float4 q_queue[ICPH_THREADS];
+    __shared__ float4 q_new[ICPH_THREADS];  // rebuilt lists: new centre (xyz) and radius (w)
+    __shared__ int n_new[ICPH_THREADS];     // their counts; -2 = unchanged
+    __shared__ int nq;
+    __shared__ unsigned long long skl[ICP_LIST_CAP];
+    const int lane = lane_id();
+    cand_init(&cl);
+    n_new[lane] = -2;
+    const int i = blockIdx.x * ICPH_THREADS + lane;
+    const bool have = i < ns;
+    float qx = 0.f, qy = 0.f, qz = 0.f, x0 = 0.f, y0 = 0.f, z0 = 0.f, R = 0.f;
+    int n = -1;
+    if (have) {
+        qx = src0[3 * i]; qy = src0[3 * i + 1]; qz = src0[3 * i + 2];
+        const float4 c0 = lcen[i];
+        x0 = c0.x; y0 = c0.y; z0 = c0.z; R = c0.w;
+        n = lcnt[i];
     }
-    // thread 0's loop state: the composed transform (LDS), the previous MSE
-    __shared__ float fin[16];
-    if (tid < 16) fin[tid] = (tid % 5 == 0) ? 1.f : 0.f;
-    double prev_mse = 1.7976931348623157e308;
-    const float one_over_n = 1.f / (float)ns;
-    int it = 0;
-    __syncthreads();
-    while (true) {
-        // ---- means: lanes 0..5 of wave 0, source order (the first element starts the sum)
-        float acc = 0.f;
-        for (int c0 = 0; c0 < ns; c0 += chs) {
-            const int cn = ns - c0 < chs ? ns - c0 : chs;
-            if (big) {
-                __syncthreads();
-                for (int t = tid; t < 7 * cn; t += ICPL_THREADS) {
-                    const int c = t / cn, k = t - c * cn;
-                    rec[c * chs + k] = rec_g[(size_t)c * ns + c0 + k];
-                }
-                __syncthreads();
-            }
-            if (wave == 0 && lane < 6) {
-                const float* a = rec + lane * chs;
-                int k = 0;
-                if (c0 == 0) { acc = a[0]; k = 1; }
-                for (; k < cn && (k & 3); ++k) acc = acc + a[k];
-                for (; k + 4 <= cn; k += 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(a + k);
-                    acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
-                }
-                for (; k < cn; ++k) acc = acc + a[k];
+    float4* lst_w = const_cast<float4*>(lst);
+    float* lsd_w = const_cast<float*>(lsd);
+    const float4* L = lst + (have ? i : 0);  // entry e at L[e * ns]: the wave's lanes read one 1 KB row
+    const float* Ld = lsd + (have ? i : 0);
+    for (int j = j0; j < max_iter; ++j) {
+        int g = 0;
+        if (lane == 0) {
+            const long long t0 = wall_clock64();
+            while (true) {
+                g = __hip_atomic_load(&sy->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (g < 0 || g >= j) break;
+                if (wall_clock64() - t0 > ICP_WAIT_TICKS) { g = -1; break; }
+                __builtin_amdgcn_s_sleep(2);
             }
         }
-        if (wave == 0 && lane < 6) smean[lane] = acc * one_over_n;
-        __syncthreads();
-        // ---- cross-covariance (wave 0, lane r * 3 + c) and PCL's MSE (wave 1, lane 0)
-        const float sm0 = smean[0], sm1 = smean[1], sm2 = smean[2], dm0 = smean[3], dm1 = smean[4], dm2 = smean[5];
-        float cov = 0.f;
-        double mse = 0.0;
-        for (int c0 = 0; c0 < ns; c0 += chs) {
-            const int cn = ns - c0 < chs ? ns - c0 : chs;
-            if (big) {
-                __syncthreads();
-                for (int t = tid; t < 7 * cn; t += ICPL_THREADS) {
-                    const int c = t / cn, k = t - c * cn;
-                    rec[c * chs + k] = rec_g[(size_t)c * ns + c0 + k];
-                }
-                __syncthreads();
-            }
-            // centre in place: s - sm, d - dm (the host's s0..s2, d0..d2)
-            for (int t = tid; t < 6 * cn; t += ICPL_THREADS) {
-                const int c = t / cn, k = t - c * cn;
-                const float m = c == 0 ? sm0 : c == 1 ? sm1 : c == 2 ? sm2 : c == 3 ? dm0 : c == 4 ? dm1 : dm2;
-                rec[c * chs + k] = rec[c * chs + k] - m;
-            }
-            __syncthreads();
-            if (wave == 0 && lane < 9) {
-                const float* e = rec + (3 + lane / 3) * chs;  // d_r - dm_r
-                const float* f = rec + (lane % 3) * chs;      // s_c - sm_c
-                int k = 0;
-                if (c0 == 0) { cov = e[0] * f[0]; k = 1; }
-                for (; k < cn && (k & 3); ++k) cov = cov + e[k] * f[k];
-                for (; k + 4 <= cn; k += 4) {
-                    const float4 u = *reinterpret_cast<const float4*>(e + k);
-                    const float4 v = *reinterpret_cast<const float4*>(f + k);
-                    const float p0 = u.x * v.x, p1 = u.y * v.y, p2 = u.z * v.z, p3 = u.w * v.w;
-                    cov = cov + p0; cov = cov + p1; cov = cov + p2; cov = cov + p3;
-                }
-                for (; k < cn; ++k) cov = cov + e[k] * f[k];
-            } else if (wave == 1 && lane == 0) {
-                const float* d2 = rec + 6 * chs;
-                int k = 0;
-                for (; k < cn && (k & 3); ++k) mse += (double)d2[k];
-                for (; k + 4 <= cn; k += 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(d2 + k);
-                    mse += (double)v.x; mse += (double)v.y; mse += (double)v.z; mse += (double)v.w;
-                }
-                for (; k < cn; ++k) mse += (double)d2[k];
-            }
-        }
-        if (wave == 0 && lane < 9) sacc[lane] = cov;
-        if (wave == 1 && lane == 0) smse = mse;
-        __syncthreads();
-        // ---- the step, PCL's convergence test (the host loop's order: the step is applied and
-        // composed first, then max_iter, the transformation epsilon and the MSE epsilon)
-        if (tid == 0) {
-            float sigma[9], sm[3] = {sm0, sm1, sm2}, dm[3] = {dm0, dm1, dm2}, o[16];
-#pragma unroll
-            for (int u = 0; u < 9; ++u) sigma[u] = sacc[u] * one_over_n;
-            bm::umeyama_finish<float>(sigma, sm, dm, o);
-            float f2[16];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    f2[r * 4 + c] = ((o[r * 4] * fin[c] + o[r * 4 + 1] * fin[4 + c]) + o[r * 4 + 2] * fin[8 + c]) +
-                                    o[r * 4 + 3] * fin[12 + c];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) { fin[u] = f2[u]; sT[u] = o[u]; }
-            ++it;
-            int stop = it >= max_iter;
-            if (!stop) {
-                const double cos_angle = 0.5 * (double)(((o[0] + o[5]) + o[10]) - 1.0f);
-                const double tsq = (double)((o[3] * o[3] + o[7] * o[7]) + o[11] * o[11]);
-                if (cos_angle >= 1.0 && tsq <= 0.0) stop = 1;
-            }
-            if (!stop) {
-                const double m = smse / (double)ns;
-                if (__builtin_fabs(m - prev_mse) < 1e-12) stop = 1;
-                prev_mse = m;
-            }
-            sstop = stop;
-            nq = 0;
-        }
-        __syncthreads();
-        if (sstop) break;  // (it, fin and prev_mse live in thread 0)
+        g = __shfl(g, 0, 64);
+        if (g < 0) break;
+        float Tl = lane < 16 ? __hip_atomic_load(&sy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0.f;
         float T[12];
 #pragma unroll
-        for (int u = 0; u < 12; ++u) T[u] = sT[u];
-        // ---- every source moved by the step (pcl::transformPointCloud's float expression, as the
-        // host's bg::xform), its NN from its list when the bound proves it global, else queued
-        for (int i = tid; i < ns; i += ICPL_THREADS) {
-            const float4 p = pos[i];
-            const float qx = ((T[0] * p.x + T[1] * p.y) + T[2] * p.z) + T[3];
-            const float qy = ((T[4] * p.x + T[5] * p.y) + T[6] * p.z) + T[7];
-            const float qz = ((T[8] * p.x + T[9] * p.y) + T[10] * p.z) + T[11];
-            pos[i] = make_float4(qx, qy, qz, 0.f);
-            const float4 c0 = lcen[i];
-            const int n = lcnt[i];
-            const float R = c0.w;
+        for (int u = 0; u < 12; ++u) T[u] = __shfl(Tl, u, 64);
+        if (lane == 0) nq = 0;
+        __builtin_amdgcn_wave_barrier();
+        if (have) {
+            const float x = qx, y = qy, z = qz;
+            qx = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
+            qy = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
+            qz = ((T[8] * x + T[9] * y) + T[10] * z) + T[11];
             bool ok = false;
             unsigned long long m = ~0ull;
-            float4 best = make_float4(0.f, 0.f, 0.f, 0.f);
             if (n >= 0 && __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz)) {
-                const float4* L = lst + i;  // entry e at L[e * ns]
-                const float* Ld = lsd + i;
-                const double ex = (double)qx - (double)c0.x, ey = (double)qy - (double)c0.y, ez = (double)qz - (double)c0.z;
+                // entries in ascending distance from the list's centre q0: an entry e with
+                // |e - q0| - |q - q0| beyond the best distance so far (with float slack) lies farther
+                // from q than the best, and so do all later ones -- the scan stops there
+                const double ex = (double)qx - (double)x0, ey = (double)qy - (double)y0, ez = (double)qz - (double)z0;
                 const double delta = sqrt(ex * ex + ey * ey + ez * ez);
-                double stopd = 1e300;
+                double stop = 1e300;
                 for (int k = 0; k < n; k += 4) {
-                    float4 pp[4];
+                    float4 p[4];
                     float dd[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int e = k + u < n ? k + u : n - 1;
-                        pp[u] = L[(size_t)e * ns];
+                        p[u] = L[(size_t)e * ns];
                         dd[u] = Ld[(size_t)e * ns];
                     }
-                    if ((double)dd[0] - delta > stopd) break;
+                    if ((double)dd[0] - delta > stop) break;
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         if (k + u < n) {
-                            const float d2 = d2_flann(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z);
-                            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | __float_as_uint(pp[u].w);
-                            if (key < m) { m = key; best = pp[u]; }
+                            const float d2 = d2_flann(qx, qy, qz, p[u].x, p[u].y, p[u].z);
+                            const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | __float_as_uint(p[u].w);
+                            m = key < m ? key : m;
                         }
                     }
-                    stopd = sqrt((double)__uint_as_float((unsigned)(m >> 32))) * (1.0 + 1e-5) + 1.0;
+                    stop = sqrt((double)__uint_as_float((unsigned)(m >> 32))) * (1.0 + 1e-5) + 1.0;
                 }
                 if (m != ~0ull) {
+                    // |q - q0| + (the list best's distance) < R with slack for float rounding: relative
+                    // 1e-5 on the distances, 1 mm absolute gap between the best and any outside target
                     const double dm = sqrt((double)__uint_as_float((unsigned)(m >> 32)));
                     ok = dm * (1.0 + 1e-5) + delta + 1.0 < (double)R * (1.0 - 1e-5);
                 }
             }
-            put(0, i, qx); put(1, i, qy); put(2, i, qz);
-            if (ok) {
-                put(3, i, best.x); put(4, i, best.y); put(5, i, best.z);
-                put(6, i, __uint_as_float((unsigned)(m >> 32)));
-            } else {
-                queue[atomicAdd(&nq, 1)] = i;
-            }
+            if (ok) icp_put_key(&best[(size_t)(j & 1) * ns + i], m);
+            else q_queue[atomicAdd(&nq, 1)] = make_float4(qx, qy, qz, __int_as_float(i));
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int nqueued = nq;
+        for (int t = 0; t < nqueued; ++t) {
+            // the exact grid search, then a new list around the current position (its owner lane
+            // takes over the new centre, count and radius below), so a source that outgrew its list
+            // pays the search once
+            const float4 q = q_queue[t];
+            const int qi = __float_as_int(q.w);
+            const unsigned long long m = icp_wave_nn(G, &cl, q.x, q.y, q.z, tgt4, nt);
+            if (lane == 0) icp_put_key(&best[(size_t)(j & 1) * ns + qi], m);
+            int cnt2;
+            float R2;
+            icp_build_list(G, &cl, q.x, q.y, q.z, m, tgt4, lst_w + qi, lsd_w + qi, ns, cap, skl, &cnt2, &R2);
+            if (lane == 0) { q_new[qi - (int)blockIdx.x * ICPH_THREADS] = make_float4(q.x, q.y, q.z, R2); n_new[qi - (int)blockIdx.x * ICPH_THREADS] = cnt2; }
+        }
+        // the rebuilt lists (stored by this wave) are read by their owner lanes from the next iteration on
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        if (have && n_new[lane] != -2) {
+            const float4 c = q_new[lane];
+            x0 = c.x; y0 = c.y; z0 = c.z; R = c.w;
+            n = n_new[lane];
+            n_new[lane] = -2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        icp_put_flag(&done[blockIdx.x], j);
+    }
+}
+
+// PCL's loop after iteration 0's neighbours: ONE persistent launch (k_icp_run) of a workgroup per
+// 256 sources. Per iteration every workgroup moves its sources by the last step and finds their NN
+// (the list scan below, else the grid search), writes the Umeyama records and arrives at a counter;
+// the LAST to arrive computes the step -- the float Umeyama in Eigen's order (the means as 6
+// sequential float sums in source order, the cross-covariance as 9 sequential sums of
+// (d_r - dm_r)(s_c - sm_c), each sum on its own lane of wave 0 over the records staged in LDS and
+// centred in place; PCL's MSE, a sequential double sum of the d2, on wave 1) and
+// DefaultConvergenceCriteria (max_iter, transformation epsilon 0, MSE epsilon 1e-12) -- and releases
+// the next iteration. No host round trip and no kernel boundary per iteration (under the lookahead's
+// load each queued launch waited tens of us to dispatch). Cross-workgroup data (records, the loop
+// state, the counters) moves with agent-scope relaxed loads and stores, ordered by waiting for the
+// stores' completion before the arrival: no L2 write-back fence (the workgroups sit on different
+// XCDs). A stop writes the result to pinned memory, seq last.
+//   NN of a moved source: its NN among its candidate list is the global NN when dm + |q - q0| < R
+//   (with float slack); otherwise the exact grid search by one of the workgroup's waves, which also
+//   rebuilds the source's list.
+// Sequential chains over LDS rows (the host's summation order): batches of 32 elements are read
+// 8 x ds_read_b128 ahead of the dependent adds, so the LDS latency overlaps the previous batch's
+// chain instead of stalling every 4 elements. Rows are 16-B aligned; k0 = the first index.
+__device__ __forceinline__ float chain_sum_f(const float* a, int k0, int n, float acc) {
+    int k = k0;
+    for (; k < n && (k & 3); ++k) acc = acc + a[k];
+    while (k + 32 <= n) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(a + k + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            acc = acc + v[u].x; acc = acc + v[u].y; acc = acc + v[u].z; acc = acc + v[u].w;
+        }
+        k += 32;
+    }
+    for (; k + 4 <= n; k += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(a + k);
+        acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
+    }
+    for (; k < n; ++k) acc = acc + a[k];
+    return acc;
+}
+
+__device__ __forceinline__ float chain_dot_f(const float* e, const float* f, int k0, int n, float acc) {
+    int k = k0;
+    for (; k < n && (k & 3); ++k) acc = acc + e[k] * f[k];
+    while (k + 32 <= n) {
+        float4 u[8], v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            u[j] = *reinterpret_cast<const float4*>(e + k + 4 * j);
+            v[j] = *reinterpret_cast<const float4*>(f + k + 4 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float p0 = u[j].x * v[j].x, p1 = u[j].y * v[j].y, p2 = u[j].z * v[j].z, p3 = u[j].w * v[j].w;
+            acc = acc + p0; acc = acc + p1; acc = acc + p2; acc = acc + p3;
+        }
+        k += 32;
+    }
+    for (; k + 4 <= n; k += 4) {
+        const float4 u = *reinterpret_cast<const float4*>(e + k);
+        const float4 v = *reinterpret_cast<const float4*>(f + k);
+        const float p0 = u.x * v.x, p1 = u.y * v.y, p2 = u.z * v.z, p3 = u.w * v.w;
+        acc = acc + p0; acc = acc + p1; acc = acc + p2; acc = acc + p3;
+    }
+    for (; k < n; ++k) acc = acc + e[k] * f[k];
+    return acc;
+}
+
+__device__ __forceinline__ double chain_sum_d(const float* a, int k0, int n, double acc) {
+    int k = k0;
+    for (; k < n && (k & 3); ++k) acc += (double)a[k];
+    while (k + 32 <= n) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(a + k + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            acc += (double)v[u].x; acc += (double)v[u].y; acc += (double)v[u].z; acc += (double)v[u].w;
+        }
+        k += 32;
+    }
+    for (; k + 4 <= n; k += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(a + k);
+        acc += (double)v.x; acc += (double)v.y; acc += (double)v.z; acc += (double)v.w;
+    }
+    for (; k < n; ++k) acc += (double)a[k];
+    return acc;
+}
+
+#define ICPR_THREADS 256
+#define ICPR_WAVES 4
+#ifndef ICPR_CH
+#define ICPR_CH 2048  // records staged in LDS at once by the stepping workgroup (7 floats each)
+#endif
+
+__device__ __forceinline__ void st_dev(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_dev(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_dev_i(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int ld_dev_i(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_dev_d(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ double ld_dev_d(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__device__ __forceinline__ void icp_put_rec_dev(float* rec, int ns, int i, float qx, float qy, float qz, float4 t,
+                                                unsigned long long m) {
+    st_dev(rec + i, qx);
+    st_dev(rec + (size_t)ns + i, qy);
+    st_dev(rec + 2 * (size_t)ns + i, qz);
+    st_dev(rec + 3 * (size_t)ns + i, t.x);
+    st_dev(rec + 4 * (size_t)ns + i, t.y);
+    st_dev(rec + 5 * (size_t)ns + i, t.z);
+    st_dev(rec + 6 * (size_t)ns + i, __uint_as_float((unsigned)(m >> 32)));
+}
+
+// the step of one iteration by the whole (last-arriving) workgroup: Umeyama of the records, the
+// composed transform and PCL's convergence test into ctl; a stop writes out
+__device__ __forceinline__ void icp_step(int ns, const float* rec, int max_iter, bsh::IcpCtl* ctl, bsh::IcpOut* out,
+                                         int seq, float* srec, float* smean, float* sacc, double* smse) {
+    const int tid = threadIdx.x, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool big = ns > ICPR_CH;
+    const int chs = big ? ICPR_CH : ((ns + 3) & ~3);  // LDS row stride (16-B aligned rows)
+    const float one_over_n = 1.f / (float)ns;
+    auto stage = [&](int c0, int cn) {
+        for (int c = 0; c < 7; ++c)
+            for (int k = tid; k < cn; k += ICPR_THREADS) srec[c * chs + k] = ld_dev(rec + (size_t)c * ns + c0 + k);
+    };
+    // ---- means: lanes 0..5 of wave 0, source order (the first element starts the sum)
+    float acc = 0.f;
+    for (int c0 = 0; c0 < ns; c0 += chs) {
+        const int cn = ns - c0 < chs ? ns - c0 : chs;
+        if (c0 > 0) __syncthreads();
+        stage(c0, cn);
+        __syncthreads();
+        if (wave == 0 && lane < 6) {
+            const float* a = srec + lane * chs;
+            if (c0 == 0) acc = chain_sum_f(a, 1, cn, a[0]);
+            else acc = chain_sum_f(a, 0, cn, acc);
+        }
+    }
+    if (wave == 0 && lane < 6) smean[lane] = acc * one_over_n;
+    __syncthreads();
+    // ---- cross-covariance (wave 0, lane r * 3 + c) and PCL's MSE (wave 1, lane 0)
+    const float sm0 = smean[0], sm1 = smean[1], sm2 = smean[2], dm0 = smean[3], dm1 = smean[4], dm2 = smean[5];
+    float cov = 0.f;
+    double mse = 0.0;
+    for (int c0 = 0; c0 < ns; c0 += chs) {
+        const int cn = ns - c0 < chs ? ns - c0 : chs;
+        if (big) {
+            __syncthreads();
+            stage(c0, cn);
+            __syncthreads();
+        }
+        // centre in place: s - sm, d - dm (the host's s0..s2, d0..d2)
+        for (int t = tid; t < 6 * cn; t += ICPR_THREADS) {
+            const int c = t / cn, k = t - c * cn;
+            const float m = c == 0 ? sm0 : c == 1 ? sm1 : c == 2 ? sm2 : c == 3 ? dm0 : c == 4 ? dm1 : dm2;
+            srec[c * chs + k] = srec[c * chs + k] - m;
         }
         __syncthreads();
-        // ---- the queued sources: exact grid search + a new list around the current position
-        const int nqueued = nq;
-        if (wave < ICPL_SW) {
-            for (int t = wave; t < nqueued; t += ICPL_SW) {
-                const int qi = queue[t];
-                const float4 q = pos[qi];
+        if (wave == 0 && lane < 9) {
+            const float* e = srec + (3 + lane / 3) * chs;  // d_r - dm_r
+            const float* f = srec + (lane % 3) * chs;      // s_c - sm_c
+            if (c0 == 0) cov = chain_dot_f(e, f, 1, cn, e[0] * f[0]);
+            else cov = chain_dot_f(e, f, 0, cn, cov);
+        } else if (wave == 1 && lane == 0) {
+            mse = chain_sum_d(srec + 6 * chs, 0, cn, mse);
+        }
+    }
+    if (wave == 0 && lane < 9) sacc[lane] = cov;
+    if (wave == 1 && lane == 0) *smse = mse;
+    __syncthreads();
+    // ---- the step, PCL's convergence test (the host loop's order: the step is composed first, then
+    // max_iter, the transformation epsilon, the MSE epsilon)
+    if (tid == 0) {
+        float sigma[9], sm[3] = {sm0, sm1, sm2}, dm[3] = {dm0, dm1, dm2}, o[16], fin[16], nf[16];
+#pragma unroll
+        for (int u = 0; u < 9; ++u) sigma[u] = sacc[u] * one_over_n;
+        bm::umeyama_finish<float>(sigma, sm, dm, o);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) fin[u] = ld_dev(&ctl->fin[u]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                nf[r * 4 + c] = ((o[r * 4] * fin[c] + o[r * 4 + 1] * fin[4 + c]) + o[r * 4 + 2] * fin[8 + c]) +
+                                o[r * 4 + 3] * fin[12 + c];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            st_dev(&ctl->fin[u], nf[u]);
+            st_dev(&ctl->T[u], o[u]);
+        }
+        const int it = ld_dev_i(&ctl->it) + 1;
+        st_dev_i(&ctl->it, it);
+        int stop = it >= max_iter;
+        if (!stop) {
+            const double cos_angle = 0.5 * (double)(((o[0] + o[5]) + o[10]) - 1.0f);
+            const double tsq = (double)((o[3] * o[3] + o[7] * o[7]) + o[11] * o[11]);
+            if (cos_angle >= 1.0 && tsq <= 0.0) stop = 1;
+        }
+        if (!stop) {
+            const double m = *smse / (double)ns;
+            if (__builtin_fabs(m - ld_dev_d(&ctl->prev_mse)) < 1e-12) stop = 1;
+            st_dev_d(&ctl->prev_mse, m);
+        }
+        st_dev_i(&ctl->stop, stop);
+        if (stop) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) __hip_atomic_store(&out->T[u], nf[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&out->iters, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_s_waitcnt(0);  // T and the count have reached host memory before seq
+            __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// sync[0]: arrivals (nb per iteration), sync[1]: the last released iteration (zeroed by k_icp_lists)
+__global__ void __launch_bounds__(ICPR_THREADS) k_icp_run(int ns, float4* lst, float* lsd, int* lcnt,
+                                                          float4* __restrict__ lcen, float4* __restrict__ pos, int cap,
+                                                          IcpGrids G, const float4* __restrict__ tgt4, int nt, float* rec,
+                                                          int max_iter, bsh::IcpCtl* ctl, unsigned int* sync,
+                                                          bsh::IcpOut* out, int seq) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
+    extern __shared__ __attribute__((aligned(16))) float srec[];  // the stepping workgroup's records
+    __shared__ CandLds cl[ICPR_WAVES];
+    __shared__ unsigned long long skl[ICPR_WAVES][ICP_LIST_CAP];
+    __shared__ float4 qq[ICPR_THREADS];
+    __shared__ int nq, s_last, s_stop;
+    __shared__ float sT[12];
+    __shared__ float smean[6];
+    __shared__ float sacc[9];
+    __shared__ double smse;
+    const int tid = threadIdx.x, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned int nb = gridDim.x;
+    cand_init(&cl[wave]);
+    const int i = blockIdx.x * ICPR_THREADS + tid;
+    for (int j = 0;; ++j) {
+        if (j > 0) {
+            // wait for step j - 1 (released by whichever workgroup arrived last)
+            if (tid == 0) {
+                const long long t0 = wall_clock64();
+                int stop = 0;
+                while ((int)__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < j) {
+                    if (wall_clock64() - t0 > ICP_WAIT_TICKS) { stop = 1; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                s_stop = stop || ld_dev_i(&ctl->stop);
+            }
+            if (tid < 12) sT[tid] = ld_dev(&ctl->T[tid]);
+            __syncthreads();
+            if (s_stop) break;
+            if (tid == 0) nq = 0;
+            __syncthreads();
+            if (i < ns) {
+                // pcl::transformPointCloud's float expression (the host's bg::xform)
+                const float4 p = pos[i];
+                const float qx = ((sT[0] * p.x + sT[1] * p.y) + sT[2] * p.z) + sT[3];
+                const float qy = ((sT[4] * p.x + sT[5] * p.y) + sT[6] * p.z) + sT[7];
+                const float qz = ((sT[8] * p.x + sT[9] * p.y) + sT[10] * p.z) + sT[11];
+                pos[i] = make_float4(qx, qy, qz, 0.f);
+                const float4 c0 = lcen[i];
+                const int n = lcnt[i];
+                bool ok = false;
+                unsigned long long m = ~0ull;
+                float4 best = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (n >= 0 && __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz)) {
+                    // entries ascend in distance from the list's centre q0: an entry e with
+                    // |e - q0| - |q - q0| beyond the best distance so far (with float slack) lies
+                    // farther from q than the best, and so do all later ones -- the scan stops there
+                    const float4* L = lst + i;  // entry e at L[e * ns]
+                    const float* Ld = lsd + i;
+                    const double ex = (double)qx - (double)c0.x, ey = (double)qy - (double)c0.y, ez = (double)qz - (double)c0.z;
+                    const double delta = sqrt(ex * ex + ey * ey + ez * ez);
+                    double stopd = 1e300;
+                    for (int k = 0; k < n; k += 4) {
+                        float4 pp[4];
+                        float dd[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int e = k + u < n ? k + u : n - 1;
+                            pp[u] = L[(size_t)e * ns];
+                            dd[u] = Ld[(size_t)e * ns];
+                        }
+                        if ((double)dd[0] - delta > stopd) break;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (k + u < n) {
+                                const float d2 = d2_flann(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z);
+                                const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | __float_as_uint(pp[u].w);
+                                if (key < m) { m = key; best = pp[u]; }
+                            }
+                        }
+                        stopd = sqrt((double)__uint_as_float((unsigned)(m >> 32))) * (1.0 + 1e-5) + 1.0;
+                    }
+                    if (m != ~0ull) {
+                        // |q - q0| + (the list best's distance) < R with slack for float rounding:
+                        // relative 1e-5 on the distances, 1 mm absolute gap to any outside target
+                        const double dm = sqrt((double)__uint_as_float((unsigned)(m >> 32)));
+                        ok = dm * (1.0 + 1e-5) + delta + 1.0 < (double)c0.w * (1.0 - 1e-5);
+                    }
+                }
+                if (ok) icp_put_rec_dev(rec, ns, i, qx, qy, qz, best, m);
+                else qq[atomicAdd(&nq, 1)] = make_float4(qx, qy, qz, __int_as_float(i));
+            }
+            __syncthreads();
+            const int nqueued = nq;
+            for (int t = wave; t < nqueued; t += ICPR_WAVES) {
+                // the exact grid search, then a new list around the current position, so a source
+                // that outgrew its list pays the search once
+                const float4 q = qq[t];
+                const int qi = __float_as_int(q.w);
                 const unsigned long long m = icp_wave_nn(G, &cl[wave], q.x, q.y, q.z, tgt4, nt);
                 int cnt2;
                 float R2;
                 icp_build_list(G, &cl[wave], q.x, q.y, q.z, m, tgt4, lst + qi, lsd + qi, ns, cap, skl[wave], &cnt2, &R2);
                 if (lane == 0) {
-                    const float4 tp = tgt4[(unsigned)(m & 0xFFFFFFFFu)];
-                    put(3, qi, tp.x); put(4, qi, tp.y); put(5, qi, tp.z);
-                    put(6, qi, __uint_as_float((unsigned)(m >> 32)));
+                    icp_put_rec_dev(rec, ns, qi, q.x, q.y, q.z, tgt4[(unsigned)(m & 0xFFFFFFFFu)], m);
                     lcnt[qi] = cnt2;
                     lcen[qi] = make_float4(q.x, q.y, q.z, R2);
                 }
             }
         }
+        // arrive: this workgroup's records have reached the coherence point first
+        __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-    }
-    if (tid == 0) {
-#pragma unroll
-        for (int u = 0; u < 16; ++u) __hip_atomic_store(&out->T[u], fin[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&out->iters, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_s_waitcnt(0);  // T and the count have reached host memory before the flag
-        __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) {
+            const unsigned int a = __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = a == nb * (unsigned)(j + 1) - 1u;
+        }
+        __syncthreads();
+        if (s_last) {
+            icp_step(ns, rec, max_iter, ctl, out, seq, srec, smean, sacc, &smse);
+            __builtin_amdgcn_s_waitcnt(0);  // the loop state has reached the coherence point
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&sync[1], (unsigned int)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -476,29 +747,46 @@ static bsk::IcpGrids icp_views(const DevGrid* const* g4) {
     return G;
 }
 
-int icp_lists_blocks(int ns) { return (ns + ICP_WAVES - 1) / ICP_WAVES; }
-
-hipError_t launch_icp_lists(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
-                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, hipStream_t s) {
+hipError_t launch_icp(const float* src0, int ns, float4* lst, float* lsd, int* lcnt, int cap, const DevGrid* const* g4,
+                      const float4* tgt4, int nt, int max_iter, float4* pos, float4* lcen, float* rec, IcpCtl* ctl,
+                      unsigned int* sync, IcpOut* out, int seq, hipStream_t s) {
     if (ns <= 0 || nt <= 0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
-    bsk::k_icp_lists<<<icp_lists_blocks(ns), 64 * ICP_WAVES, 0, s>>>(src0, ns, icp_views(g4), tgt4, nt, cap, lst, lsd, lcnt,
-                                                                     lrad, best_out);
+    const bsk::IcpGrids G = icp_views(g4);
+    bsk::k_icp_lists<<<(ns + ICP_WAVES - 1) / ICP_WAVES, 64 * ICP_WAVES, 0, s>>>(src0, ns, G, tgt4, nt, cap, lst, lsd, lcnt,
+                                                                               lcen, pos, rec, ctl, sync, nullptr,
+                                                                               nullptr);
+    const int chs = ns > ICPR_CH ? ICPR_CH : ((ns + 3) & ~3);
+    const size_t lds = sizeof(float) * 7 * (size_t)chs;
+    const int nb = (ns + ICPR_THREADS - 1) / ICPR_THREADS;
+    // every workgroup of the persistent launch must fit on the chip at once (they wait for each other)
+    if (nb > 256) return hipErrorInvalidValue;
+    bsk::k_icp_run<<<nb, ICPR_THREADS, lds, s>>>(ns, lst, lsd, lcnt, lcen, pos, cap, G, tgt4, nt, rec,
+                                                 max_iter > 1 ? max_iter : 1, ctl, sync, out, seq);
     return hipGetLastError();
 }
 
-size_t icp_loop_rec_floats(int ns) { return ns > ICPL_CH ? (size_t)7 * ns : 0; }
+int icp_lists_blocks(int ns) { return (ns + ICP_WAVES - 1) / ICP_WAVES; }
+int icp_iter_blocks(int ns) { return (ns + ICPH_THREADS - 1) / ICPH_THREADS; }
 
-hipError_t launch_icp_loop(const float* src0, int ns, float4* lst, float* lsd, int* lcnt, float* lrad, int cap,
-                           const DevGrid* const* g4, const float4* tgt4, int nt, int max_iter,
-                           const unsigned long long* best0, float4* pos, float4* lcen, int* queue, float* rec_g,
-                           IcpOut* out, int seq, hipStream_t s) {
+hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
+                                 float4* lst, float* lsd, int* lcnt, float4* lcen, unsigned long long* best_out,
+                                 int* done, hipStream_t s) {
     if (ns <= 0 || nt <= 0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
-    const int chs = ns > ICPL_CH ? ICPL_CH : ((ns + 3) & ~3);
-    const size_t lds = sizeof(float) * 7 * (size_t)chs;
-    bsk::k_icp_loop<<<1, ICPL_THREADS, lds, s>>>(src0, ns, lst, lsd, lcnt, lrad, cap, icp_views(g4), tgt4, nt, max_iter, best0,
-                                                 pos, lcen, queue, rec_g, out, seq);
+    bsk::k_icp_lists<<<icp_lists_blocks(ns), 64 * ICP_WAVES, 0, s>>>(src0, ns, icp_views(g4), tgt4, nt, cap, lst, lsd, lcnt,
+                                                                     lcen, nullptr, nullptr, nullptr, nullptr, best_out,
+                                                                     done);
+    return hipGetLastError();
+}
+
+hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4* lst, const float* lsd, const int* lcnt,
+                                 const float4* lcen, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
+                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s) {
+    if (ns <= 0 || nt <= 0 || max_iter <= j0) return hipSuccess;
+    if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
+    bsk::k_icp_iterations<<<icp_iter_blocks(ns), ICPH_THREADS, 0, s>>>(src0, ns, j0, lst, lsd, lcnt, lcen, cap, icp_views(g4),
+                                                                      tgt4, nt, max_iter, sy, done, best);
     return hipGetLastError();
 }
 

@@ -62,20 +62,44 @@ struct IcpOut {
     int seq;
     int pad[14];
 };
-// iteration 0 (one launch, a wave per source): the exact 1-NN keys of src0 into best_out (HBM) and
-// every source's candidate list
+// the host's ICP loop (the default): host <-> device hand-over in coherent pinned memory -- the host
+// releases iteration j (step transform T, then go = j; go = -1 stops the kernel); every workgroup
+// writes its own completion flag once its keys are stored
+struct IcpSync {
+    int go;
+    int pad0[31];
+    float T[16];
+};
 int icp_lists_blocks(int ns);
-hipError_t launch_icp_lists(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
-                            float4* lst, float* lsd, int* lcnt, float* lrad, unsigned long long* best_out, hipStream_t s);
-// PCL's loop from iteration 0's keys on (one launch, one workgroup, csrc/icp.hip k_icp_loop): per
-// iteration the float Umeyama, the convergence test, the step and the next keys; the composed
-// transform and the iteration count land in *out, seq last. Scratch (HBM): pos, lcen (ns float4 each),
-// queue (ns ints), rec_g (icp_loop_rec_floats(ns) floats: 0 unless ns exceeds the LDS staging).
-size_t icp_loop_rec_floats(int ns);
-hipError_t launch_icp_loop(const float* src0, int ns, float4* lst, float* lsd, int* lcnt, float* lrad, int cap,
-                           const DevGrid* const* g4, const float4* tgt4, int nt, int max_iter,
-                           const unsigned long long* best0, float4* pos, float4* lcen, int* queue, float* rec_g,
-                           IcpOut* out, int seq, hipStream_t s);
+int icp_iter_blocks(int ns);
+// iteration 0 (a wave per source): keys of src0 into best_out (pinned), the candidate lists (lcen:
+// centre + radius); workgroup w sets done[w] = 1
+hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
+                                 float4* lst, float* lsd, int* lcnt, float4* lcen, unsigned long long* best_out,
+                                 int* done, hipStream_t s);
+// iterations j0 .. max_iter - 1 (one persistent launch, a lane per source starting at src0): each
+// waits for the host's release of the iteration (or go = -1), moves its source by T, stores the exact
+// 1-NN key in best[(j & 1) * ns + i] (pinned) and sets done[w] = j
+hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4* lst, const float* lsd, const int* lcnt,
+                                 const float4* lcen, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
+                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s);
+// the loop state of one ICP call (device memory): the last step, the composed transform, PCL's
+// previous MSE, the iteration count and the stop flag every queued kernel checks first
+struct IcpCtl {
+    float T[16];
+    float fin[16];
+    double prev_mse;
+    int it;
+    int stop;
+};
+// PCL's ICP loop on the device (option icp_device, csrc/icp.hip): k_icp_lists (iteration 0: exact 1-NN, candidate lists,
+// records), then one persistent k_icp_run (per iteration: step + NN of every source on its
+// workgroup, the Umeyama step + convergence test on the last workgroup to arrive), queued on s; the
+// stopping step writes the composed transform and the count to *out, seq last. Scratch (HBM): lst /
+// lsd (cap x ns), lcnt (ns), pos / lcen (ns float4), rec (7 x ns floats), ctl, sync (2 u32).
+hipError_t launch_icp(const float* src0, int ns, float4* lst, float* lsd, int* lcnt, int cap, const DevGrid* const* g4,
+                      const float4* tgt4, int nt, int max_iter, float4* pos, float4* lcen, float* rec, IcpCtl* ctl,
+                      unsigned int* sync, IcpOut* out, int seq, hipStream_t s);
 // load-balanced SHOT (describe2.hip): in-bucket rank, LRF over 64-rank chunks, records + ordered apply
 struct Describe2Args {
     int k = 0, n_plan = 0, n_chunks = 0;
@@ -101,6 +125,7 @@ struct Describe2Args {
     int* err = nullptr;
     const unsigned int* bstart = nullptr;  // per-keypoint bucket starts of the bucket-grouped segment
     int max_blocks = 0;  // grid cap of the chunk kernels (0: one block per 4 chunks)
+    int rank_wg = 0;     // 1: k_shot_rank_wg (workgroup per keypoint, large neighbourhoods); 0: k_shot_rank
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 

@@ -325,8 +325,9 @@ void bshot_stage_reset(bshot_ctx* c);
 void bshot_set_timing(bshot_ctx* c, int enabled);
 /* work counters: [0] neighbourhood total of the last describe (SHOT pairs), [1] describes re-run with a
  * host plan after the device plan ran out of capacity (cumulative); ICP, cumulative: [2] ns the host
- * waited for the device loop's result, [3] / [4] unused (0), [5] iterations; [6] / [7] pool
- * regrowths (count / bytes) */
+ * waited for nearest neighbours (or, option icp_device, for the device loop's result), [3] restarts
+ * of the iterations after their kernel outwaited a stalled host, [4] ns of host work between two
+ * waits, [5] iterations; [6] / [7] pool regrowths (count / bytes) */
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
 /* instrumentation (outside timed regions): sum over all points of the current cloud of
  * |B(p, R)| (strict d2 < R^2, self included) -> the P_sr / P_iss work figures of SURVEY.md §8(d). */

@@ -184,19 +184,47 @@ def test_match_exact_random_and_ties(ctx):
         np.testing.assert_array_equal(g, r)
 
 
-def test_icp_exact(ctx, cloud, sr_ref):
+@pytest.mark.parametrize("device_loop", [0, 1])
+def test_icp_exact(ctx, cloud, sr_ref, device_loop):
     """A11: ICP (iteration 0 builds candidate lists, later iterations search them) vs the oracle,
-    bit for bit."""
+    bit for bit: the host's float Umeyama loop (default) and the device loop (option icp_device)."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 600)
     tgt = cloud[kidx]
     c, s = np.cos(0.01), np.sin(0.01)
     src = (tgt @ np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], np.float32).T + np.array([300, -200, 50], np.float32))
     src = src.astype(np.float32)
-    T, it = ctx.icp(src, tgt)
+    ctx.set_option("icp_device", device_loop)
+    try:
+        T, it = ctx.icp(src, tgt)
+    finally:
+        ctx.set_option("icp_device", 0)
     Tr, itr = orc.icp(src, tgt)
     assert it == itr
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+
+
+def test_icp_host_stall_restarts(ctx, cloud, sr_ref):
+    """a host stall longer than the persistent kernel's 1 s wait (the host sleeps 1.3 s
+    before releasing iteration 3) makes the kernel exit; the host restarts the iterations from its
+    current positions and the result is still the oracle's, bit for bit."""
+    ridx, rrat = sr_ref
+    kidx, _ = orc.select_topk(ridx, rrat, 600)
+    tgt = cloud[kidx]
+    c, s = np.cos(0.02), np.sin(0.02)
+    src = (tgt @ np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], np.float32).T + np.array([600, -300, 80], np.float32))
+    src = src.astype(np.float32)
+    w0 = ctx.work()
+    ctx.set_option("icp_host_delay_ms", 1300)
+    try:
+        T, it = ctx.icp(src, tgt)
+    finally:
+        ctx.set_option("icp_host_delay_ms", 0)
+    w1 = ctx.work()
+    Tr, itr = orc.icp(src, tgt)
+    assert it == itr and it > 3
+    np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+    assert w1[3] - w0[3] >= 1  # the restart happened
 
 
 def test_icp_iteration_counts_and_sizes(ctx, cloud, sr_ref):
@@ -209,12 +237,17 @@ def test_icp_iteration_counts_and_sizes(ctx, cloud, sr_ref):
     tgt = cloud[kidx]
     c, s = np.cos(0.02), np.sin(0.02)
     rot = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], np.float32)
-    for ns, it_cap in ((2100, 0), (2100, 1), (2100, 2), (2100, 200), (1001, 10), (2049, 10), (2048, 10), (3, 10)):
-        src = (tgt[:ns] @ rot.T + np.array([700, -400, 90], np.float32)).astype(np.float32)
-        T, it = ctx.icp(src, tgt, max_iter=it_cap)
-        Tr, itr = orc.icp(src, tgt, max_iter=it_cap)
-        assert it == itr, (ns, it_cap)
-        np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+    for dev in (0, 1):
+        ctx.set_option("icp_device", dev)
+        try:
+            for ns, it_cap in ((2100, 0), (2100, 1), (2100, 2), (2100, 200), (1001, 10), (2049, 10), (2048, 10), (3, 10)):
+                src = (tgt[:ns] @ rot.T + np.array([700, -400, 90], np.float32)).astype(np.float32)
+                T, it = ctx.icp(src, tgt, max_iter=it_cap)
+                Tr, itr = orc.icp(src, tgt, max_iter=it_cap)
+                assert it == itr, (dev, ns, it_cap)
+                np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+        finally:
+            ctx.set_option("icp_device", 0)
 
 
 @pytest.mark.parametrize("big", [False, True])
@@ -288,6 +321,29 @@ def test_ransac_scores_kernel(ctx, nidx, nhyp):
     h = bshot_py.ransac_scores(cs, ct, hyp)
     assert np.array_equal(g, h)
     assert g.min() >= 0 and g.max() <= nidx
+
+
+@pytest.mark.parametrize("rank_wg", [0, 1])
+def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg):
+    """The two SHOT rank kernels (a wave per 64-rank chunk; a workgroup per keypoint staging
+    whole-bucket spans in LDS) give the host-planned describe's bits and histograms exactly, on
+    the device plan and on the host plan."""
+    ridx, rrat = sr_ref
+    kidx, _ = orc.select_topk(ridx, rrat, 2048)
+    kps = cloud[kidx]
+    ctx.set_cloud(cloud)
+    ctx.set_option("rank_wg", 0)
+    ctx.set_option("dev_plan_hint", 0)
+    ref_bits, ref_shot, _ = ctx.describe(kps)
+    ctx.set_option("rank_wg", rank_wg)
+    try:
+        for hint in (0, 1 << 30):
+            ctx.set_option("dev_plan_hint", hint)
+            bits, shot, _ = ctx.describe(kps)
+            np.testing.assert_array_equal(bits, ref_bits)
+            np.testing.assert_array_equal(shot.view(np.uint32), ref_shot.view(np.uint32))
+    finally:
+        ctx.set_option("rank_wg", 2)
 
 
 def test_config5_dense_large_radius_describe():
