@@ -160,12 +160,13 @@ __device__ __forceinline__ void rank_in_place(KnnLds* L, int tot, float sc0) {
     __builtin_amdgcn_wave_barrier();
 }
 
-// level-0 d2 histogram of list[0, total): every in-radius key of the delivering ladder step. Built
-// after the step instead of per streamed chunk, so steps that fall short cost no LDS atomics.
-__device__ __forceinline__ void hist_of_list(KnnLds* L, int total, float sc0) {
+// level-0 d2 histogram of the delivering ladder step: the keys of list[0, nl) (its first KNN_CAP
+// in-radius keys) added to the histogram of the keys past the list, which the step counted as it
+// streamed (zero when it did not overflow). Built after the step instead of per streamed chunk, so
+// steps that fall short cost no LDS atomics.
+__device__ __forceinline__ void hist_of_list(KnnLds* L, int nl, float sc0) {
     const int lane = lane_id();
-    hist_clear(L);
-    for (int i = lane; i < total; i += 64)
+    for (int i = lane; i < nl; i += 64)
         atomicAdd(&L->hist[bucket_of(__uint_as_float((unsigned)(L->list[i] >> 32)), 0.f, sc0)], 1u);
     __builtin_amdgcn_wave_barrier();
 }
@@ -203,7 +204,11 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
     for (; step <= last; ++step) {
         rs = step == last ? r : r * lg.frac[step];
         rs2 = step == last ? r2 : (float)((double)rs * (double)rs);
+        const float sc = (float)KNN_NB / rs2;
         int cnt = 0;
+        // keys past the LDS list are counted into the level-0 histogram as they stream (the list's
+        // own keys join it afterwards, knn_finish): a step that overflows needs no extra pass for it
+        hist_clear(L);
         // a step whose cube holds fewer than max_nn candidates cannot deliver: skipped unstreamed
         const bool went = for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             if constexpr (DIAG) ++chunks;
@@ -212,6 +217,7 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
                 const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
                 if (slot < KNN_CAP) L->list[slot] = knn_key(d2, idx);
+                else atomicAdd(&L->hist[bucket_of(d2, 0.f, sc)], 1u);
             }
             cnt += __popcll(m);
         }, step == last ? 0 : max_nn);
@@ -263,12 +269,11 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
     *need_out = need;
     if (need == 0) return true;
     const float sc0 = (float)KNN_NB / rs2;
-    bool hist0 = false;  // L->hist holds the level-0 histogram of the whole ball
+    // L->hist: the level-0 histogram of the whole ball (the streamed overflow + the list's keys)
+    hist_of_list(L, total < KNN_CAP ? total : KNN_CAP, sc0);
 
     // ---- fast path: every in-radius key is in L->list
     if (total <= KNN_CAP) {
-        hist_of_list(L, total, sc0);
-        hist0 = true;
         int Bmax = KNN_NB - 1;
         if (total > need) {
             int below;
@@ -317,7 +322,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
         float w = rs2;
 #pragma unroll
         for (int lev = 0; lev < 3; ++lev) {
-            if (lev > 0 || !hist0) {
+            if (lev > 0) {
                 hist_clear(L);
                 if constexpr (DIAG) {
                     if (lev > 0 && lane == 0) atomicAdd(&kst[7], 1ull);
@@ -326,7 +331,6 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
                     if constexpr (DIAG) ++chunks;
                     if (!v) return;
                     int b = bucket_of(d2, lo[0], sc[0]);
-                    if (lev == 0) { atomicAdd(&L->hist[b], 1u); return; }
                     if (b != B[0]) return;
                     b = bucket_of(d2, lo[1], sc[1]);
                     if (lev == 1) { atomicAdd(&L->hist[b], 1u); return; }

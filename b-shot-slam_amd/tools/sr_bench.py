@@ -21,5 +21,7 @@ c.set_timing(False)
 s = [int(x) for x in c.knn_stats()]
 q = max(1, s[0])
 print(json.dumps({"lib": os.environ.get("BSHOT_LIB", "tree"), "ms_per_launch": round(st["seg_ratio"][0] / 10, 4),
-                  "chunks_per_q": round(s[5] / q, 3), "failed_chunks_per_q": round(s[26] / q, 3)}))
+                  "chunks_per_q": round(s[5] / q, 3), "failed_chunks_per_q": round(s[26] / q, 3),
+                  "streaming_path_frac": round(s[11] / q, 4), "in_radius_per_q": round(s[10] / q, 1),
+                  "refine_passes_per_q": round(s[7] / q, 4)}))
 c.close()
