@@ -167,7 +167,9 @@ __device__ __forceinline__ void icp_put_flag(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+#ifndef ICP_WAVES
 #define ICP_WAVES 4
+#endif
 // per-source Umeyama record of an iteration, SoA rows of ns floats in rec: source xyz (the source's
 // current position), its NN target xyz, the NN's d2
 __device__ __forceinline__ void icp_put_rec(float* rec, int ns, int i, float qx, float qy, float qz, float4 t,
