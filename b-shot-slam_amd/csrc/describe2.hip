@@ -490,6 +490,9 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 #ifndef HF_WPE
 #define HF_WPE 0
 #endif
+#ifndef HF_DIAG
+#define HF_DIAG 0  // diagnostic builds only: 1 = no apply, 2 = no record computation
+#endif
 #ifndef HF_APQ
 #define HF_APQ 4  // the applying wave reads a chunk's records in HF_APQ parts
 #endif
@@ -585,7 +588,15 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
         const int i = t * 64 + lane;
         int bins[5] = {-1, -1, -1, -1, -1};
         float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#if HF_DIAG == 2
+        // diagnostic: no records computed (apply cost alone)
+        if (i < n) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) { bins[j] = (64 * j + lane) % 352; vals[j] = 1.0f; }
+        }
+#else
         if (i < n) shot_records(pts4, normals, kx, ky, kz, R, rf, seg[o + i], bins, vals);
+#endif
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             sS[buf][bi][64 * j + lane] = bins[j] < 0 ? (unsigned short)360 : (unsigned short)bins[j];
@@ -612,7 +623,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
             // LDS atomic unit's time is per active lane
             int use = 0;
             for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use |= suse[buf][bi];
-            if (lane < 5 && ((use >> lane) & 1)) {
+            if (HF_DIAG != 1 && lane < 5 && ((use >> lane) & 1)) {
                 for (int part = 0; part < HF_APQ * HF_B && b * HF_B + part / HF_APQ < nch; ++part) {
                     // 64 / HF_APQ ranks of chunk part / HF_APQ at a time (keeps the applying path's
                     // registers low: the producers' FP64 code sets the kernel's VGPR budget)

@@ -148,6 +148,27 @@ __global__ void k_gmap_prep_rec(const float* __restrict__ rec, int kmax, int slo
     keys[i] = block_id_of(r[0], r[1], r[2]);
 }
 
+// the block of id: found, or created (um::initial(): one bucket, nothing allocated); -1 past capacity
+__device__ int find_or_create_block(const GMapDev& m, unsigned long long id) {
+    int b = find_block(m, id);
+    if (b >= 0) return b;
+    b = atomicAdd(&m.ctr[GM_NBLOCKS], 1);
+    if (b >= m.blk_cap) {
+        atomicOr(&m.ctr[GM_ERR], 1);
+        return -1;
+    }
+    GBlock B;
+    B.id = id;
+    B.n = 0; B.bkt = 1; B.next_resize = 0; B.cap = 0;
+    B.mslot = B.ord = B.pos = B.code = -1;
+    B.bk = -1; B.bk_cap = 0;
+    m.blk[b] = B;
+    unsigned int h = hash_key(id) & m.tmask;
+    while (atomicCAS(&m.tkey[h], BS_EMPTY_KEY, id) != BS_EMPTY_KEY) h = (h + 1) & m.tmask;
+    m.tval[h] = b;
+    return b;
+}
+
 // one thread per run of equal block ids in the sorted keys: find or create the block, record the run
 __global__ void k_gmap_segments(const unsigned long long* __restrict__ keys, int k, GMapDev m, int* __restrict__ seg) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -161,27 +182,95 @@ __global__ void k_gmap_segments(const unsigned long long* __restrict__ keys, int
         if (keys[mid] == id) lo = mid + 1;
         else hi = mid;
     }
-    int b = find_block(m, id);
-    if (b < 0) {
-        b = atomicAdd(&m.ctr[GM_NBLOCKS], 1);
-        if (b >= m.blk_cap) {
-            atomicOr(&m.ctr[GM_ERR], 1);
-            return;
-        }
-        GBlock B;
-        B.id = id;
-        B.n = 0; B.bkt = 1; B.next_resize = 0; B.cap = 0;  // um::initial(): one bucket, nothing allocated
-        B.mslot = B.ord = B.pos = B.code = -1;
-        B.bk = -1; B.bk_cap = 0;
-        m.blk[b] = B;
-        unsigned int h = hash_key(id) & m.tmask;
-        while (atomicCAS(&m.tkey[h], BS_EMPTY_KEY, id) != BS_EMPTY_KEY) h = (h + 1) & m.tmask;
-        m.tval[h] = b;
-    }
+    const int b = find_or_create_block(m, id);
+    if (b < 0) return;
     const int s = atomicAdd(&m.ctr[GM_NSEG], 1);
     seg[3 * s] = j;
     seg[3 * s + 1] = lo - j;
     seg[3 * s + 2] = b;
+}
+
+// Batches of <= GM_SORT_MAX keypoints (every own-map insert: K <= 4096): the sort, the runs and the
+// segment count in one workgroup. Bitonic sort of (block id, index) pairs in LDS: the indices are
+// the batch's sweep order and unique, so the order equals the stable radix sort's. Segments are
+// numbered by an exclusive scan of the run starts (deterministic, no counter to clear). Writes the
+// sorted indices to vals_out and m.ctr[GM_NSEG].
+#define GM_SORT_MAX 4096
+#define GM_SORT_T 1024
+__global__ void __launch_bounds__(GM_SORT_T) k_gmap_sort_segments(const unsigned long long* __restrict__ keys,
+                                                                 const unsigned int* __restrict__ vals, int k,
+                                                                 GMapDev m, unsigned int* __restrict__ vals_out,
+                                                                 int* __restrict__ seg) {
+    __shared__ unsigned long long sk[GM_SORT_MAX];
+    __shared__ unsigned int sv[GM_SORT_MAX];
+    __shared__ int wsum[GM_SORT_T / 64];
+    const int t = threadIdx.x;
+    int P = 64;
+    while (P < k) P <<= 1;
+    for (int i = t; i < P; i += GM_SORT_T) {
+        sk[i] = i < k ? keys[i] : BS_EMPTY_KEY;
+        sv[i] = i < k ? vals[i] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < P / 2; i += GM_SORT_T) {
+                const int a = 2 * i - (i & (stride - 1));  // lower index of the pair
+                const int b = a + stride;
+                const bool up = (a & size) == 0;
+                const unsigned long long ka = sk[a], kb = sk[b];
+                const unsigned int va = sv[a], vb = sv[b];
+                const bool gt = ka > kb || (ka == kb && va > vb);
+                if (gt == up) {
+                    sk[a] = kb; sk[b] = ka;
+                    sv[a] = vb; sv[b] = va;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = t; i < k; i += GM_SORT_T) vals_out[i] = sv[i];
+    // runs: each thread owns GM_SORT_MAX / GM_SORT_T consecutive positions
+    constexpr int PER = GM_SORT_MAX / GM_SORT_T;
+    const int j0 = PER * t;
+    int starts = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int j = j0 + u;
+        starts += (j < k && sk[j] != BS_EMPTY_KEY && (j == 0 || sk[j - 1] != sk[j])) ? 1 : 0;
+    }
+    // exclusive scan of the per-thread counts (wave scan, then the waves' totals)
+    const int lane = t & 63, wv = t >> 6;
+    int incl = starts;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wv; ++w) base += wsum[w];
+    int s = base + incl - starts;
+    if (t == GM_SORT_T - 1) m.ctr[GM_NSEG] = base + incl;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int j = j0 + u;
+        if (!(j < k && sk[j] != BS_EMPTY_KEY && (j == 0 || sk[j - 1] != sk[j]))) continue;
+        const unsigned long long id = sk[j];
+        int e = j + 1, hi = k;
+        while (e < hi) {
+            const int mid = (e + hi) >> 1;
+            if (sk[mid] == id) e = mid + 1;
+            else hi = mid;
+        }
+        // a block past capacity (error bit set) leaves an empty run: the insert skips it
+        const int b = find_or_create_block(m, id);
+        seg[3 * s] = j;
+        seg[3 * s + 1] = b < 0 ? 0 : e - j;
+        seg[3 * s + 2] = b < 0 ? 0 : b;
+        ++s;
+    }
 }
 
 // bump allocation from a pool (lane 0); false when the pool is exhausted (error bit 2)
@@ -220,6 +309,7 @@ __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsig
     const int nseg = m.ctr[GM_NSEG];
     for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
         const int j0 = seg[3 * sg], cnt = seg[3 * sg + 1], b = seg[3 * sg + 2];
+        if (cnt == 0) continue;  // a run whose block could not be created (GM_ERR is set)
         GBlock B = m.blk[b];
         if (B.n + cnt > GM_LDS_N) {
             if (tid == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
@@ -599,14 +689,18 @@ static int gmap_reserve(bshot_ctx* c, GMap& g, int k, hipStream_t st = nullptr) 
 static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync, hipStream_t st = nullptr) {
     if (!st) st = c->stream;
     const int B = 256;
-    size_t tb = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
-                                     st), "gmap sort size");
-    HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
-    HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
-                                     st), "gmap sort");
-    HIPCHK(kfill(g.ctr.p + GM_NSEG, 0, sizeof(int), st), "gmap seg count");
-    bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, st>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
+    if (k <= GM_SORT_MAX) {
+        bsk::k_gmap_sort_segments<<<1, GM_SORT_T, 0, st>>>(g.keys.p, g.vals.p, k, dev_view(g), g.vals.p + k, g.seg.p);
+    } else {
+        size_t tb = 0;
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
+                                         st), "gmap sort size");
+        HIPCHK(g.tmp.ensure(tb + 16), "gmap sort tmp");
+        HIPCHK(rocprim::radix_sort_pairs(g.tmp.p, tb, g.keys.p, g.keys.p + k, g.vals.p, g.vals.p + k, (unsigned)k, 0, 64,
+                                         st), "gmap sort");
+        HIPCHK(kfill(g.ctr.p + GM_NSEG, 0, sizeof(int), st), "gmap seg count");
+        bsk::k_gmap_segments<<<(k + B - 1) / B, B, 0, st>>>(g.keys.p + k, k, dev_view(g), g.seg.p);
+    }
     // a workgroup holds a whole CU's LDS (the block image), and a batch touches a few hundred blocks
     // at most: more workgroups than that only occupy CUs to exit. Replica inserts (another stream,
     // off the critical chain) take fewer, leaving the CUs to the lookahead.
