@@ -588,7 +588,7 @@ template <bool DIAG>
 __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
                                                               float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
-                                                              unsigned long long* __restrict__ kst) {
+                                                              unsigned long long* __restrict__ kst, int zc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // the wave index in an SGPR: the wave's LDS base is then rematerialised, not held in a VGPR
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -597,7 +597,18 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
     const int nw = gridDim.x * KNN_WAVES;
     const float4* __restrict__ order = lg.g[0].spts;
     float* fl = reinterpret_cast<float*>(L->list);
-    for (int j = blockIdx.x * KNN_WAVES + wave; j < n; j += nw) {
+    int j0 = blockIdx.x * KNN_WAVES + wave;
+    if (zc > 0) {
+        // XCD-local chunks of cell order: workgroups b, b + 8, ... share an XCD (the dispatcher deals
+        // workgroups round-robin over the 8 XCDs), so the workgroups of label g = b % 8 take chunks
+        // g, g + 8, g + 16, ... of zc workgroups each: the 8 XCDs work on 8 adjacent chunks at a time
+        // (similar density, so the in-order dealing stays balanced) and each XCD's L2 holds its own
+        // chunk's neighbourhood instead of all eight holding the same one
+        const int g = blockIdx.x & 7, i = blockIdx.x >> 3;
+        const int m = i / zc, o = i - m * zc;
+        j0 = ((m * 8 + g) * zc + o) * KNN_WAVES + wave;
+    }
+    for (int j = j0; j < n; j += nw) {
         const float4 sp = order[j];
         const int q = (int)__float_as_uint(sp.w);
         float out = __builtin_nanf("");
@@ -718,18 +729,24 @@ static LadderGrids ladder(const DevGrid* const* g4, int mode) {
 
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst, int max_blocks) {
+                            unsigned long long* kst, int max_blocks, int xcd_chunk) {
     const size_t lds = bsk::knn_lds_bytes();
     int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
     // fewer, longer-lived waves cost less dispatch; more, short-lived ones let high-priority
     // kernels of other streams in sooner
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+    int zc = 0;  // workgroups per XCD-local chunk (one query per wave only)
+    if (xcd_chunk > 0 && (max_blocks <= 0 || blocks < max_blocks)) {
+        zc = (xcd_chunk + KNN_WAVES - 1) / KNN_WAVES;
+        const int rounds = (blocks + 8 * zc - 1) / (8 * zc);
+        blocks = rounds * 8 * zc;  // whole rounds of 8 chunks; the workgroups past n exit at once
+    }
     if (kst)
         bsk::k_seg_ratio<true><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
-                                                                   hint, ratio, err, kst);
+                                                                   hint, ratio, err, kst, zc);
     else
         bsk::k_seg_ratio<false><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
-                                                                    hint, ratio, err, nullptr);
+                                                                    hint, ratio, err, nullptr, zc);
     return hipGetLastError();
 }
 
