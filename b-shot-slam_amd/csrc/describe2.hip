@@ -490,6 +490,9 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 #ifndef HF_WPE
 #define HF_WPE 0
 #endif
+#ifndef HF_PACK
+#define HF_PACK 0  // > 0: ranks per ds_add_f32 in the apply (5 lanes each)
+#endif
 #ifndef HF_DIAG
 #define HF_DIAG 0  // diagnostic builds only: 1 = no apply, 2 = no record computation
 #endif
@@ -623,7 +626,35 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
             // LDS atomic unit's time is per active lane
             int use = 0;
             for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use |= suse[buf][bi];
+#if HF_PACK > 0
+            // HF_PACK ranks per ds_add_f32: lane 5 g + j applies slot j of rank r0 + g. Lanes that share a
+            // bin within one instruction must be applied in ascending lane order (rank, then slot) --
+            // what the LDS atomic unit does (experiments/microbench/lds_lane_order.hip)
+            {
+                constexpr int G = HF_PACK;
+                const int g = lane / 5, j = lane - 5 * (lane / 5);
+                if (HF_DIAG != 1 && lane < 5 * G && ((use >> j) & 1)) {
+                    for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) {
+                        const unsigned short* sb = &sS[buf][bi][64 * j];
+                        const float* sv = &sV[buf][bi][64 * j];
+                        unsigned int bn[(64 + G - 1) / G];
+                        float vv[(64 + G - 1) / G];
+#pragma unroll
+                        for (int u = 0; u < (64 + G - 1) / G; ++u) {
+                            const int r = G * u + g;
+                            bn[u] = r < 64 ? (unsigned int)sb[r] : 360u;
+                            vv[u] = r < 64 ? sv[r] : 0.f;
+                        }
+#pragma unroll
+                        for (int u = 0; u < (64 + G - 1) / G; ++u)
+                            if (vv[u] != 0.f) atomicAdd(&hist[bn[u]], vv[u]);
+                    }
+                }
+            }
+            if (false) {
+#else
             if (HF_DIAG != 1 && lane < 5 && ((use >> lane) & 1)) {
+#endif
                 for (int part = 0; part < HF_APQ * HF_B && b * HF_B + part / HF_APQ < nch; ++part) {
                     // 64 / HF_APQ ranks of chunk part / HF_APQ at a time (keeps the applying path's
                     // registers low: the producers' FP64 code sets the kernel's VGPR budget)
