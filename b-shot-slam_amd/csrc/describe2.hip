@@ -491,7 +491,7 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 #define HF_WPE 0
 #endif
 #ifndef HF_PACK
-#define HF_PACK 0  // > 0: ranks per ds_add_f32 in the apply (5 lanes each)
+#define HF_PACK 12  // ranks per ds_add_f32 in the apply (5 lanes each); 0: one rank per instruction
 #endif
 #ifndef HF_DIAG
 #define HF_DIAG 0  // diagnostic builds only: 1 = no apply, 2 = no record computation
