@@ -60,6 +60,7 @@ ABI_SYMBOLS = [
     "bshot_odom_get_inliers", "bshot_odom_get_iss", "bshot_odom_ctx", "bshot_odom_map_delta",
     "bshot_odom_replica_insert", "bshot_odom_replica_size", "bshot_stage_times", "bshot_stage_reset",
     "bshot_set_timing", "bshot_work_counters", "bshot_radius_pairs", "bshot_debug_knn_stats",
+    "bshot_debug_lds_lane_order",
     "bshot_map_create", "bshot_map_destroy", "bshot_map_add", "bshot_map_query", "bshot_map_size",
     "bshot_map_set_query_mode",
     "bshot_map_block_id", "bshot_set_option", "bshot_prefetch_cloud_device", "bshot_odom_set_next_device",
@@ -338,6 +339,12 @@ class Context:
         w = (ctypes.c_int64 * 32)()
         self._chk(self.L.bshot_debug_knn_stats(self.h, w, 32), "knn_stats")
         return list(w)
+
+    def lds_lane_order(self):
+        m, s, a = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._chk(self.L.bshot_debug_lds_lane_order(self.h, ctypes.byref(m), ctypes.byref(s), ctypes.byref(a)),
+                  "lds_lane_order")
+        return m.value, s.value, bool(a.value)
 
     def radius_pairs(self, R):
         t = ctypes.c_int64()

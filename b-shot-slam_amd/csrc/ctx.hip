@@ -472,6 +472,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.bstart = c->sbst.p;
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
         A.rank_wg = rank_wg_for(c, k, c->seg_hint);
+        A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
@@ -539,6 +540,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
     A.rank_wg = rank_wg_for(c, k, total);
+    A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -879,7 +881,34 @@ int bshot_create(bshot_ctx** out, int device, const bshot_params* p) {
         delete c;
         return BSHOT_EHIP;
     }
+    // the packed SHOT apply relies on same-address ds_add_f32 lanes applying in ascending lane
+    // order: checked once per device and process (a few ms); a device that fails runs the
+    // one-rank-per-instruction apply (same results, slower)
+    {
+        static std::mutex m;
+        static int checked[64];
+        static int result[64];
+        std::lock_guard<std::mutex> lk(m);
+        if (device < 64 && !checked[device]) {
+            result[device] = bsh::lds_lane_order_check(nullptr);
+            checked[device] = 1;
+        }
+        c->hf_pack_ok = device < 64 && result[device] == 0;
+    }
     *out = c;
+    return BSHOT_OK;
+}
+
+int bshot_debug_lds_lane_order(bshot_ctx* c, int* mismatches, int* sensitive, int* active) {
+    TraceScope trace_scope_("bshot_debug_lds_lane_order");
+    if (!c || !mismatches) return BSHOT_EINVAL;
+    (void)hipSetDevice(c->device);
+    int sens = 0;
+    const int r = bsh::lds_lane_order_check(&sens);
+    if (r < 0) return c->fail("lds lane-order check: HIP error", BSHOT_EHIP);
+    *mismatches = r;
+    if (sensitive) *sensitive = sens;
+    if (active) *active = c->opt_hist_pack && c->hf_pack_ok;
     return BSHOT_OK;
 }
 
@@ -1187,6 +1216,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "icp_device") c->opt_icp_device = value ? 1 : 0;
     else if (k == "icp_host_delay_ms") c->opt_icp_host_delay_ms = value < 0 ? 0 : value;
     else if (k == "diag_skip_icp") c->opt_diag_skip_icp = value ? 1 : 0;  // diagnostic: the period without ICP
+    else if (k == "hist_pack") c->opt_hist_pack = value ? 1 : 0;
     else if (k == "rank_wg") c->opt_rank_wg = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;

@@ -491,7 +491,7 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 #define HF_WPE 0
 #endif
 #ifndef HF_PACK
-#define HF_PACK 12  // ranks per ds_add_f32 in the apply (5 lanes each); 0: one rank per instruction
+#define HF_PACK 12  // ranks per ds_add_f32 in the packed apply (5 lanes each)
 #endif
 #ifndef HF_DIAG
 #define HF_DIAG 0  // diagnostic builds only: 1 = no apply, 2 = no record computation
@@ -504,7 +504,7 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 #else
 #define HF_ATTR
 #endif
-template <int HF_WAVES>
+template <int HF_WAVES, int PACK>
 __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const float4* __restrict__ pts4,
                                                               const float4* __restrict__ normals,
                                                               const float* __restrict__ kps, int k, float R,
@@ -626,12 +626,13 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
             // LDS atomic unit's time is per active lane
             int use = 0;
             for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) use |= suse[buf][bi];
-#if HF_PACK > 0
-            // HF_PACK ranks per ds_add_f32: lane 5 g + j applies slot j of rank r0 + g. Lanes that share a
+            if constexpr (PACK > 0) {
+            // PACK ranks per ds_add_f32: lane 5 g + j applies slot j of rank r0 + g. Lanes that share a
             // bin within one instruction must be applied in ascending lane order (rank, then slot) --
-            // what the LDS atomic unit does (experiments/microbench/lds_lane_order.hip)
+            // what the LDS atomic unit does (experiments/microbench/lds_lane_order.hip; checked on the
+            // device at context creation, lds_lane_order_mismatches, else PACK = 0 runs)
             {
-                constexpr int G = HF_PACK;
+                constexpr int G = PACK;
                 const int g = lane / 5, j = lane - 5 * (lane / 5);
                 if (HF_DIAG != 1 && lane < 5 * G && ((use >> j) & 1)) {
                     for (int bi = 0; bi < HF_B && b * HF_B + bi < nch; ++bi) {
@@ -651,10 +652,7 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
                     }
                 }
             }
-            if (false) {
-#else
-            if (HF_DIAG != 1 && lane < 5 && ((use >> lane) & 1)) {
-#endif
+            } else if (HF_DIAG != 1 && lane < 5 && ((use >> lane) & 1)) {
                 for (int part = 0; part < HF_APQ * HF_B && b * HF_B + part / HF_APQ < nch; ++part) {
                     // 64 / HF_APQ ranks of chunk part / HF_APQ at a time (keeps the applying path's
                     // registers low: the producers' FP64 code sets the kernel's VGPR budget)
@@ -692,9 +690,93 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
     if (wave == 0) hist_finish(hist, gcode, q, good, lane, shot_out, bits_out);
 }
 
+// The packed SHOT apply needs one ds_add_f32 to apply lanes that share an address in ascending lane
+// order. 8 waves, each on its own 64 bins: LC_TRIALS trials of LC_OPS atomic adds with hashed
+// addresses (1, 4, 16 or 64 distinct), exec masks and values of mixed magnitude (order-sensitive
+// float sums); lane 0 of each wave replays every trial sequentially in ascending lane order and the
+// wave counts the bins whose bits differ. out[0] += mismatches, out[1] += order-sensitive bins (where
+// the descending order differs: the check's power).
+#define LC_TRIALS 16
+#define LC_OPS 16
+__device__ __forceinline__ unsigned int lc_hash(unsigned int a, unsigned int b, unsigned int c) {
+    unsigned int h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+__device__ __forceinline__ float lc_val(unsigned int h) {
+    const float m = (float)(h & 0xFFFFFu) / 1048576.0f - 0.5f;
+    return ldexpf(m, (int)((h >> 20) % 40u) - 20);
+}
+__device__ __forceinline__ unsigned long long lc_mask(unsigned int t, unsigned int op) {
+    const unsigned int k = op % 3u;
+    if (k == 0) return ~0ull;
+    if (k == 1) return 0x0FFFFFFFFFFFFFFFull;  // the packed apply's 60 lanes
+    return ((unsigned long long)lc_hash(t, op, 1000u) << 32) | lc_hash(t, op, 2000u);
+}
+__global__ void __launch_bounds__(512) k_lds_lane_order(unsigned int seed, int* __restrict__ out) {
+    __shared__ float bins[8][64];
+    __shared__ float ref[8][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int mism = 0, sens = 0;
+    for (int t0 = 0; t0 < LC_TRIALS; ++t0) {
+        const unsigned int t = seed + (unsigned int)(blockIdx.x * 8 + wave) * LC_TRIALS + (unsigned int)t0;
+        const float init = lc_val(lc_hash(t, 77u, (unsigned int)lane)) * 1000.f;
+        bins[wave][lane] = init;
+        ref[wave][lane] = init;
+        __builtin_amdgcn_wave_barrier();
+        for (unsigned int op = 0; op < LC_OPS; ++op) {
+            const unsigned int span = 1u << (2u * (op & 3u));  // 1, 4, 16, 64
+            const unsigned int h = lc_hash(t, op, (unsigned int)lane);
+            if ((lc_mask(t, op) >> lane) & 1ull) atomicAdd(&bins[wave][h % span], lc_val(h >> 6));
+        }
+        __builtin_amdgcn_wave_barrier();
+        float dn = init;  // descending replay of this lane's bin (the check's power)
+        if (lane == 0) {
+            for (unsigned int op = 0; op < LC_OPS; ++op) {
+                const unsigned int span = 1u << (2u * (op & 3u));
+                const unsigned long long m = lc_mask(t, op);
+                for (int l = 0; l < 64; ++l) {
+                    const unsigned int h = lc_hash(t, op, (unsigned int)l);
+                    if ((m >> l) & 1ull) ref[wave][h % span] = ref[wave][h % span] + lc_val(h >> 6);
+                }
+            }
+        }
+        for (unsigned int op = 0; op < LC_OPS; ++op) {
+            const unsigned int span = 1u << (2u * (op & 3u));
+            const unsigned long long m = lc_mask(t, op);
+            for (int l = 63; l >= 0; --l) {
+                const unsigned int h = lc_hash(t, op, (unsigned int)l);
+                if (((m >> l) & 1ull) && (int)(h % span) == lane) dn = dn + lc_val(h >> 6);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        mism += __float_as_uint(bins[wave][lane]) != __float_as_uint(ref[wave][lane]) ? 1 : 0;
+        sens += __float_as_uint(dn) != __float_as_uint(ref[wave][lane]) ? 1 : 0;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (mism) atomicAdd(&out[0], mism);
+    if (sens) atomicAdd(&out[1], sens);
+}
+
 }  // namespace bsk
 
 namespace bsh {
+
+int lds_lane_order_check(int* sensitive) {
+    int* d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(int)) != hipSuccess) return -1;
+    int h[2] = {0, 0};
+    bool ok = hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) {
+        bsk::k_lds_lane_order<<<64, 512>>>(12345u, d);
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+             hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(d);
+    if (!ok) return -1;
+    if (sensitive) *sensitive = h[1];
+    return h[0];
+}
 
 // part 0: in-bucket rank (sorted segments); 1: LRF; 2: histogram records + ordered apply
 hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
@@ -727,8 +809,12 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
         return hipGetLastError();
     }
     // HF_NW waves per workgroup: 1 applies, HF_NW - 1 produce records
-    bsk::k_hist_fused<HF_NW><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb, A.sorted,
-                                                 A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
+    if (A.hf_pack)
+        bsk::k_hist_fused<HF_NW, HF_PACK><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
+                                                               A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
+    else
+        bsk::k_hist_fused<HF_NW, 0><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
+                                                         A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
     return hipGetLastError();
 }
 

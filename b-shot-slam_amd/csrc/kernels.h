@@ -126,8 +126,12 @@ struct Describe2Args {
     const unsigned int* bstart = nullptr;  // per-keypoint bucket starts of the bucket-grouped segment
     int max_blocks = 0;  // grid cap of the chunk kernels (0: one block per 4 chunks)
     int rank_wg = 0;     // 1: k_shot_rank_wg (workgroup per keypoint, large neighbourhoods); 0: k_shot_rank
+    int hf_pack = 1;     // 1: the SHOT apply packs several ranks per ds_add_f32 (needs lds_lane_order_check() == 0)
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
+// mismatches of same-address ds_add_f32 lanes against ascending lane order on the current device
+// (0 expected; *sensitive = bins where the order mattered), -1 on a HIP error
+int lds_lane_order_check(int* sensitive);
 
 // A10 RANSAC: score (inlier count) of every hypothesis (csrc/ransac.hip)
 hipError_t launch_ransac_score(const float* cs, const float* ct, int nidx, const int* hyp, int nhyp, double thr2,

@@ -294,7 +294,11 @@ int bshot_map_set_query_mode(bshot_map* m, int mode);
  *      lists when normal_radius == shot_radius (the same (d2, idx)-sorted radius search);
  *      "ransac_dev" 1 (default): RANSAC hypotheses scored on the GPU; "topk_thread" 1 (default);
  *      "pre_fast" 1 (default): the preprocessor's one-sort path when it applies; "side_prio";
- *      "timing_mask" stage-event mask. Behaviour: "gpu_map" 1 (default, libstdc++ order) / 2
+ *      "timing_mask" stage-event mask; "rank_wg" 2 (default: by neighbourhood size) / 1 / 0: SHOT
+ *      neighbour ranking with a workgroup per keypoint or a wave per 64-rank chunk; "hist_pack" 1
+ *      (default): the SHOT apply packs 12 ranks per LDS float atomic when the device passed the
+ *      lane-order check (bshot_debug_lds_lane_order); "icp_device" 0 (default) / 1: ICP iterations
+ *      handed to the host's Umeyama, or the whole loop on the device. Behaviour: "gpu_map" 1 (default, libstdc++ order) / 2
  *      (canonical order) / 0 (host Map); "xseq_targets" 0 (default): other sequences' replicas join
  *      the matching targets; "host_map_log" 1 (default; 0 under bshot_odom): keep the GPU map's
  *      insert log so the host Map view (LidarOdometry::getKeypoints, getBlockKeypoints) can be
@@ -340,6 +344,11 @@ int bshot_radius_pairs(bshot_ctx* c, float R, int64_t* total);
  * ladder / fast selection / streaming selection / ratio math, [16 + s] queries whose ladder
  * stopped at step s. */
 int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n);
+/* the device check behind the packed SHOT apply (k_hist_fused): same-address ds_add_f32 lanes must
+ * apply in ascending lane order. mismatches = bins that differ from the ascending replay (0
+ * expected), sensitive = bins where the order mattered, active = the packed apply is in use
+ * (option "hist_pack" and a clean check at bshot_create). Extension (no reference counterpart). */
+int bshot_debug_lds_lane_order(bshot_ctx* c, int* mismatches, int* sensitive, int* active);
 
 #ifdef __cplusplus
 }

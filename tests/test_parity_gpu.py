@@ -346,6 +346,34 @@ def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg):
         ctx.set_option("rank_wg", 2)
 
 
+def test_lds_lane_order_check(ctx):
+    """The packed SHOT apply (12 ranks per LDS float atomic) relies on same-address lanes of one
+    ds_add_f32 being applied in ascending lane order; the device check behind it must find no
+    mismatch, have real power (bins where the descending order differs), and leave the packed
+    apply active on this device."""
+    mism, sens, active = ctx.lds_lane_order()
+    assert mism == 0
+    assert sens > 1000
+    assert active
+
+
+def test_hist_pack_matches_one_rank_apply(ctx, cloud, sr_ref):
+    """The packed apply and the one-rank-per-instruction apply give the same histograms and bits,
+    bit for bit, and both equal the oracle (test_describe_parity covers the default)."""
+    ridx, rrat = sr_ref
+    kidx, _ = orc.select_topk(ridx, rrat, 2048)
+    kps = cloud[kidx]
+    ctx.set_cloud(cloud)
+    bits1, shot1, _ = ctx.describe(kps)
+    ctx.set_option("hist_pack", 0)
+    try:
+        bits0, shot0, _ = ctx.describe(kps)
+    finally:
+        ctx.set_option("hist_pack", 1)
+    np.testing.assert_array_equal(bits1, bits0)
+    np.testing.assert_array_equal(shot1.view(np.uint32), shot0.view(np.uint32))
+
+
 def test_config5_dense_large_radius_describe():
     """BASELINE config 5: VLP-128-style 256k-point sweep, K=4096 keypoints, SHOT radius 5000 mm
     (the large-neighbourhood stress case). The GPU describes all 4096 keypoints and the oracle
