@@ -135,7 +135,7 @@ struct bshot_ctx {
     // tuning knobs (bshot_set_option): results never depend on them
     int opt_ladder4 = 1;  // 1: 4 nested grids + 7-step sqrt(2) radius ladder (default); 0: 2 grids, 4 steps
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
-    int opt_sr_xcd_chunk = 0;   // SR queries per XCD-local chunk of cell order (0: round-robin queries)
+    int opt_sr_xcd_chunk = 1024;  // SR queries per XCD-local chunk of cell order (0: round-robin queries)
     int opt_sr_blocks = 0;      // SR grid cap (0: one query per wave -- short waves let the main stream in)
     int opt_side_prio = 0;      // describe (side) stream priority: 0 low (as SR/ISS ahead), 1 middle, 2 the main stream's
     int opt_map_sync = 1;       // GPU map insert: wait for it and report the map size per sweep (0: stream-ordered, size -1)

@@ -576,9 +576,9 @@ __device__ float sr_of_neighbours(const unsigned long long* sorted, const float4
 // ------------------------------------------------------------------------------------------
 // A1: segmentation ratio of every point. max_nn <= 512 (host-checked).
 // Queries go in the ladder grids' cell order (g[0].spts, a permutation of the cloud whose .w holds
-// each point's index), dealt round-robin over the grid's waves (consecutive workgroups sit on
-// different XCDs; a contiguous stretch of cell order per XCD would hand one XCD the dense
-// near-sensor region). One query per wave pass: short waves let the other streams' kernels in
+// each point's index), in XCD-local chunks (zc > 0, below) or dealt round-robin over the grid's
+// waves (consecutive workgroups sit on different XCDs; one contiguous stretch of cell order per XCD
+// would hand one XCD the dense near-sensor region). One query per wave pass: short waves let the other streams' kernels in
 // (runs of several cell-order queries per wave, each starting its ladder at its predecessor's
 // step, streamed 11-18 % fewer candidates but were slower in the pipeline,
 // profiles/r03_ab_sr_order_runs.txt).
