@@ -41,7 +41,10 @@ def pmc_kernel(stage, path=None):
     scripts/pmc_summary.py): HBM bytes per launch (rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE,
     separate passes) and, where collected, the SQ / TCC / TCP derived metrics."""
     import glob
-    files = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    import re
+    # the default configuration's sets only (rNN<letter>_pmc.json; config sets carry a suffix: r04c_c5)
+    files = [path] if path else sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
+                                       if re.fullmatch(r"r\d\d[a-z]?_pmc\.json", os.path.basename(f)))
     if not files:
         return None, None
     try:
