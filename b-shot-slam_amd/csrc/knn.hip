@@ -34,6 +34,9 @@ namespace bsk {
 #endif
 #define KNN_PRE 512  // largest prefix the counting sort handles (8 keys per lane)
 #define KNN_WAVES 2
+#ifndef SR_DIAG_NOFIN
+#define SR_DIAG_NOFIN 0  // diagnostic: 1 = skip the ratio computation (timing of the selection alone)
+#endif
 #ifndef SR_WPE
 #define SR_WPE 5  // VGPRs <= 96: 5 waves per SIMD
 #endif
@@ -624,7 +627,11 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
             if (!ok) {
                 if (lane == 0) atomicOr(err, 1);
             } else if (need > 0) {
+#if SR_DIAG_NOFIN
+                out = (float)need;  // diagnostic builds only: the selection without the ratio
+#else
                 out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
+#endif
             }
             if constexpr (DIAG) {
                 const unsigned long long tm1 = cycle_stamp();
