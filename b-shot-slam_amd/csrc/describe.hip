@@ -249,9 +249,9 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
     }();
 }
 
-// Workgroup per keypoint (LPT order): the keypoint's bucket-grouped segment is ranked span by span,
-// a span being whole buckets holding <= RK_SPAN keys: staged in LDS with coalesced loads (with its
-// bucket starts), every key ranked inside its bucket from LDS, its index written to its sorted slot.
+// Workgroup per keypoint (LPT order): the keypoint's bucket-grouped segment is ordered span by span,
+// a span being whole buckets holding <= RK_SPAN keys: staged in LDS with coalesced loads, sorted
+// there (bitonic), its indices written back coalesced.
 // Two dependent global round trips per span instead of ~5 per 64-rank chunk (owner, offsets, keys,
 // bucket starts, bucket keys): the kernel streams a large neighbourhood (config 5: ~28k keys per
 // keypoint) instead of waiting on it. A bucket alone larger than RK_SPAN is ranked from HBM.
@@ -270,8 +270,7 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
     const long long o = offs[q];
     const int n = (int)(offs[q + 1] - o);
     if (n <= 0) return;
-    const float R2 = (float)((double)R * (double)R);
-    const float sc = (float)SG_BUCKETS / R2;
+    (void)R;
     const unsigned long long* sg = seg + o;
     unsigned int* op = out + o;
     // the bucket starts, and end(1024) = n
@@ -302,17 +301,30 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
             }
             e = b0 + 1;
         } else {
+            // the span holds whole buckets in bucket order, and the bucket is monotone in d2, so the
+            // span sorted by (d2 bits, idx) is its slice of the keypoint's order: an LDS bitonic sort
+            // (cost independent of the bucket sizes, unlike ranking each key against its bucket), then
+            // coalesced index writes
             const unsigned int hi = sbs[e], m = hi - lo;
-            for (unsigned int i = t; i < m; i += RK_T) st[i] = sg[lo + i];
+            int P = 64;
+            while (P < (int)m) P <<= 1;
+            for (int i = t; i < P; i += RK_T) st[i] = i < (int)m ? sg[lo + i] : ~0ull;
             __syncthreads();
-            for (unsigned int i = t; i < m; i += RK_T) {
-                const unsigned long long key = st[i];
-                const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
-                const unsigned int s0 = sbs[b] - lo, e0 = sbs[b + 1] - lo;
-                unsigned int rank = 0;
-                for (unsigned int j = s0; j < e0; ++j) rank += st[j] < key ? 1u : 0u;
-                op[lo + s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
+            for (int size = 2; size <= P; size <<= 1) {
+                for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                    for (int i = t; i < P / 2; i += RK_T) {
+                        const int a = 2 * i - (i & (stride - 1)), b = a + stride;
+                        const bool up = (a & size) == 0;
+                        const unsigned long long x = st[a], y = st[b];
+                        if ((x > y) == up) {
+                            st[a] = y;
+                            st[b] = x;
+                        }
+                    }
+                    __syncthreads();
+                }
             }
+            for (unsigned int i = t; i < m; i += RK_T) op[lo + i] = (unsigned int)(st[i] & 0xFFFFFFFFu);
         }
         __syncthreads();  // st and s_e are rewritten for the next span
         b0 = e;

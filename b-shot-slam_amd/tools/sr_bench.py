@@ -36,5 +36,9 @@ for arg in sys.argv[1:] or ["default"]:
                       "ms_per_launch": round(st["seg_ratio"][0] / 10, 4),
                       "chunks_per_q": round(s[5] / q, 3), "failed_chunks_per_q": round(s[26] / q, 3),
                       "streaming_path_frac": round(s[11] / q, 4), "in_radius_per_q": round(s[10] / q, 1),
-                      "refine_passes_per_q": round(s[7] / q, 4)}))
+                      "refine_passes_per_q": round(s[7] / q, 4),
+                      # per-query wave-clock shares (DIAG launch): ladder + streaming, selection from
+                      # the LDS list, selection on the streaming path, the ratio (centroid + signs)
+                      "cycle_share": {k: round(s[i] / max(1, s[12] + s[13] + s[14] + s[15]), 3)
+                                      for k, i in (("ladder", 12), ("select", 13), ("select_stream", 14), ("ratio", 15))}}))
 c.close()
