@@ -250,13 +250,17 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
 }
 
 // Workgroup per keypoint (LPT order): the keypoint's bucket-grouped segment is ordered span by span,
-// a span being whole buckets holding <= RK_SPAN keys: staged in LDS with coalesced loads, sorted
-// there (bitonic), its indices written back coalesced.
+// a span being whole buckets holding <= RK_SPAN keys: staged in LDS with coalesced loads, then every
+// key ranked inside its bucket (small buckets), or the span sorted there (bitonic; its cost does not
+// grow with the bucket sizes), indices written to their sorted slots.
 // Two dependent global round trips per span instead of ~5 per 64-rank chunk (owner, offsets, keys,
 // bucket starts, bucket keys): the kernel streams a large neighbourhood (config 5: ~28k keys per
 // keypoint) instead of waiting on it. A bucket alone larger than RK_SPAN is ranked from HBM.
 #define RK_T 256
 #define RK_SPAN 2048
+#ifndef RK_RANKMAX
+#define RK_RANKMAX 64  // spans whose buckets all hold <= this many keys rank in place; larger ones sort
+#endif
 __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int* __restrict__ perm,
                                                       const long long* __restrict__ offs,
                                                       const unsigned int* __restrict__ bstart,
@@ -265,12 +269,14 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
     __shared__ unsigned long long st[RK_SPAN];
     __shared__ unsigned int sbs[SG_BUCKETS + 1];
     __shared__ int s_e;
+    __shared__ unsigned int s_maxb;
     const int t = threadIdx.x;
     const int q = perm[blockIdx.x];
     const long long o = offs[q];
     const int n = (int)(offs[q + 1] - o);
     if (n <= 0) return;
-    (void)R;
+    const float R2 = (float)((double)R * (double)R);
+    const float sc = (float)SG_BUCKETS / R2;
     const unsigned long long* sg = seg + o;
     unsigned int* op = out + o;
     // the bucket starts, and end(1024) = n
@@ -282,7 +288,10 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
         const unsigned int lo = sbs[b0];
         if (lo >= (unsigned int)n) break;
         // the span: buckets [b0, e) with e the largest bucket end within RK_SPAN keys of lo
-        if (t == 0) s_e = b0;
+        if (t == 0) {
+            s_e = b0;
+            s_maxb = 0;
+        }
         __syncthreads();
         int best = b0;
         for (int e = b0 + 1 + t; e <= SG_BUCKETS; e += RK_T)
@@ -290,6 +299,12 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
         if (best > b0) atomicMax(&s_e, best);
         __syncthreads();
         int e = s_e;
+        // the span's largest bucket decides how it is ordered
+        unsigned int mb = 0;
+        for (int b = b0 + t; b < e; b += RK_T) mb = max(mb, sbs[b + 1] - sbs[b]);
+        if (mb) atomicMax(&s_maxb, mb);
+        __syncthreads();
+        const bool rank_path = s_maxb <= RK_RANKMAX;
         if (e == b0) {
             // bucket b0 alone exceeds the span: rank it from HBM
             const unsigned int s0 = lo, e0 = sbs[b0 + 1];
@@ -300,6 +315,19 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
                 op[s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
             }
             e = b0 + 1;
+        } else if (rank_path) {
+            // small buckets: every key ranked against its bucket in LDS
+            const unsigned int hi = sbs[e], m = hi - lo;
+            for (unsigned int i = t; i < m; i += RK_T) st[i] = sg[lo + i];
+            __syncthreads();
+            for (unsigned int i = t; i < m; i += RK_T) {
+                const unsigned long long key = st[i];
+                const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
+                const unsigned int s0 = sbs[b] - lo, e0 = sbs[b + 1] - lo;
+                unsigned int rank = 0;
+                for (unsigned int j = s0; j < e0; ++j) rank += st[j] < key ? 1u : 0u;
+                op[lo + s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
+            }
         } else {
             // the span holds whole buckets in bucket order, and the bucket is monotone in d2, so the
             // span sorted by (d2 bits, idx) is its slice of the keypoint's order: an LDS bitonic sort
