@@ -286,7 +286,7 @@ int bshot_map_set_query_mode(bshot_map* m, int mode);
 
 /* ---- options. Tuning knobs (results never depend on them): "ladder_grids" 4 (default) / 2 grids for
  *      the exact-kNN radius ladder; "ladder_front" 1 (default): two more small radii in front;
- *      "sr_start" percent scale of the ladder-start prediction (0: step 0); "sr_blocks" SR grid cap;
+ *      "sr_start" 80 (default): percent scale of the ladder-start prediction (0: step 0); "sr_blocks" SR grid cap;
  *      "sr_xcd_chunk" 1024 (default): SR queries per XCD-local chunk of cell order (0: queries dealt round-robin);
  *      "iss_cell" 2 (default) / 1: ISS grid cell in salient radii (grid options take effect at the
  *      next set_cloud); "iss_ovf_blocks", "iss_nms_blocks", "chunk_blocks" grid caps; "normals_seg"
