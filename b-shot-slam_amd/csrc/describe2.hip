@@ -321,21 +321,19 @@ __device__ __forceinline__ float dot4f_2(float a0, float a1, float a2, float b0,
 
 // the <= 5 (bin, value) interpolation records of neighbour idx, in PCL's add order (cos
 // neighbour, radius, inclination, azimuth, main bin); unused slots: bin -1
-__device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, const float4* __restrict__ normals,
-                                             float kx, float ky, float kz, float R, const float* rf,
-                                             unsigned int idx, int* bins, float* vals) {
+// (from the neighbour's normal nv and point p, both already loaded)
+__device__ __forceinline__ void shot_records_of(float4 nv, float4 p, float kx, float ky, float kz, float R,
+                                                const float* rf, int* bins, float* vals) {
         const double Rd = (double)R;
         const double r12 = Rd / 2, r34 = (Rd * 3) / 4, r14 = Rd / 4;
         const int nr_bins = 10;
     #pragma unroll
         for (int j = 0; j < 5; ++j) { bins[j] = -1; vals[j] = 0.f; }
-        const float4 nv = normals[idx];
         if (__builtin_isfinite(nv.x) && __builtin_isfinite(nv.y) && __builtin_isfinite(nv.z)) {
             double cosd = (double)dot4f_2(nv.x, nv.y, nv.z, rf[6], rf[7], rf[8]);
             if (cosd > 1.0) cosd = 1.0;
             if (cosd < -1.0) cosd = -1.0;
             double bd = ((1.0 + cosd) * nr_bins) / 2;
-            const float4 p = pts4[idx];
             const float dx = p.x - kx, dy = p.y - ky, dz = p.z - kz;
             // the gather's d2 (same expression and operands as the ranked key's)
             const double distance = sqrt((double)d2_flann(kx, ky, kz, p.x, p.y, p.z));
@@ -399,6 +397,12 @@ __device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, co
                 vals[4] = (float)w;
             }
         }
+}
+
+__device__ __forceinline__ void shot_records(const float4* __restrict__ pts4, const float4* __restrict__ normals,
+                                             float kx, float ky, float kz, float R, const float* rf,
+                                             unsigned int idx, int* bins, float* vals) {
+    shot_records_of(normals[idx], pts4[idx], kx, ky, kz, R, rf, bins, vals);
 }
 
 // normalizeHistogram + B-SHOT of one keypoint's histogram h (wave-uniform q, good)
@@ -489,6 +493,9 @@ __device__ __forceinline__ void hist_finish(float* h, unsigned int* gcode, int q
 #endif
 #ifndef HF_WPE
 #define HF_WPE 0
+#endif
+#ifndef HF_PREF
+#define HF_PREF 1  // producers load a chunk's normals and points one chunk ahead
 #endif
 #ifndef HF_PACK
 #define HF_PACK 12  // ranks per ds_add_f32 in the packed apply (5 lanes each)
@@ -587,11 +594,34 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
     float rf[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j) rf[j] = good ? rfs[j] : 0.f;
+#if HF_PREF
+    // producer pipeline: wave w's chunks are m HF_B + w - 1, m = 0, 1, ...; a chunk's normals and
+    // points are loaded while the previous chunk's records are computed, its indices one chunk
+    // earlier still (the FP64 record code then waits on no gather)
+    auto chunk_idx = [&](int t) -> unsigned int {
+        const int i = t * 64 + lane;
+        return (t < nch && i < n) ? seg[o + i] : 0u;
+    };
+    float4 cur_nv = make_float4(0.f, 0.f, 0.f, 0.f), cur_p = cur_nv;
+    unsigned int nxt_idx = 0u;
+    if (wave >= 1) {
+        const unsigned int i0 = chunk_idx(wave - 1);
+        nxt_idx = chunk_idx(HF_B + wave - 1);
+        cur_nv = normals[i0];
+        cur_p = pts4[i0];
+    }
+#endif
     auto produce = [&](int t, int buf, int bi) {
         const int i = t * 64 + lane;
         int bins[5] = {-1, -1, -1, -1, -1};
         float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#if HF_DIAG == 2
+#if HF_PREF && HF_DIAG != 2
+        const float4 nx_nv = normals[nxt_idx], nx_p = pts4[nxt_idx];
+        nxt_idx = chunk_idx(t + 2 * HF_B);
+        if (i < n) shot_records_of(cur_nv, cur_p, kx, ky, kz, R, rf, bins, vals);
+        cur_nv = nx_nv;
+        cur_p = nx_p;
+#elif HF_DIAG == 2
         // diagnostic: no records computed (apply cost alone)
         if (i < n) {
 #pragma unroll
