@@ -105,6 +105,9 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
 // as it holds more than ISS_LCAP neighbours and hands the point to the overflow list (wave kernel
 // above). The kept keys are then sorted by (d2, idx) in registers with a bitonic network sized to
 // the wave's longest list, and the double scatter matrix is summed in that rank order.
+#ifndef ISS_CELL_ORDER
+#define ISS_CELL_ORDER 1
+#endif
 #define ISS_LCAP 32
 #define ISS_LBLOCK 64
 
@@ -170,9 +173,19 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
                                                         unsigned int* __restrict__ nml, int* __restrict__ nmc) {
     __shared__ unsigned long long keys[ISS_LCAP][ISS_LBLOCK];  // [slot][thread]: conflict-free columns
     const int t = threadIdx.x;
+#if ISS_CELL_ORDER
+    // points in the grid's cell order (spts .w = index): a wave's lanes scan the same or adjacent
+    // cells, so their loops and loads stay together
+    const int j = blockIdx.x * ISS_LBLOCK + t;
+    const bool live = j < n;
+    const float4 sp = live ? g.spts[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int q = live ? (int)__float_as_uint(sp.w) : n;
+    const float4 c = sp;
+#else
     const int q = blockIdx.x * ISS_LBLOCK + t;
     const bool live = q < n;
     const float4 c = live ? pts4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     const bool fin = live && __builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z);
     int cnt = 0;
     if (fin) {
