@@ -16,6 +16,9 @@ namespace bsk {
 
 #define ISS_CAP 512
 #define ISS_WAVES 2
+#ifndef ISS_OVF_GROUP
+#define ISS_OVF_GROUP 4  // candidate chunks in flight in the overflow kernel
+#endif
 
 struct IssLds {
     unsigned long long list[ISS_CAP];
@@ -45,13 +48,23 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
     cand_init(&L->cand);
     const float r2 = (float)((double)salient * (double)salient);
     const int n_ovf = ovf[0];
+    // the eigen test of up to 64 points at once: lane k keeps the k-th pending point's scatter
+    // matrix, and the Jacobi solves run on all lanes together (one lane per point)
+    double psm[6] = {0, 0, 0, 0, 0, 0};
+    int pq = -1, npend = 0;
+    auto flush = [&]() {
+        if (pq >= 0) third[pq] = iss_third(psm, g21, g32);
+        pq = -1;
+        npend = 0;
+    };
     for (int oi = blockIdx.x * ISS_WAVES + wave; oi < n_ovf; oi += gridDim.x * ISS_WAVES) {
         const int q = ovf[1 + oi];
         const float4 c = pts4[q];
         double out = 0.0;
+        bool pend = false;
         if (__builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z)) {
             int cnt = 0;
-            for_candidates<1>(g, &L->cand, c.x, c.y, c.z, salient, r2, [&](bool v, float d2, unsigned int idx) {
+            for_candidates<ISS_OVF_GROUP>(g, &L->cand, c.x, c.y, c.z, salient, r2, [&](bool v, float d2, unsigned int idx) {
                 const unsigned long long m = __ballot(v);
                 if (v) {
                     const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
@@ -92,12 +105,22 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
                 }
                 const double sm[6] = {__shfl(cov[0], 0, 64), __shfl(cov[0], 1, 64), __shfl(cov[0], 2, 64),
                                       __shfl(cov[0], 3, 64), __shfl(cov[0], 4, 64), __shfl(cov[0], 5, 64)};
-                if (lane == 0) out = iss_third(sm, g21, g32);
+                if (lane == npend) {
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) psm[u] = sm[u];
+                    pq = q;
+                }
+                pend = true;
             }
         }
-        if (lane == 0) third[q] = out;
+        if (pend) {
+            if (++npend == 64) flush();
+        } else if (lane == 0) {
+            third[q] = out;
+        }
         __builtin_amdgcn_wave_barrier();
     }
+    flush();
 }
 
 // lane/point: every lane owns one point. Neighbours within the salient radius are appended to a
