@@ -222,10 +222,16 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(kfill(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
-        HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient * (float)c->opt_iss_cell, s.pts4.p, st, false),
-               "grid build (ISS)");
+        // the SR ladder's finest grid serves ISS when its cell holds the salient ball's cube in
+        // 2 x 2 x 2 cells (r/16 = 187.5 mm >= 2 x 60 mm at the reference's settings): no sort of
+        // its own (the ISS kernels visit the same points, in cells that hold more of them)
+        const bool reuse = c->opt_iss_grid && c->opt_ladder4 && s.fine_ladder &&
+                           s.grid_l16.n == n && s.grid_l16.cell >= 2.f * c->prm.iss_salient;
+        if (!reuse)
+            HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient * (float)c->opt_iss_cell, s.pts4.p, st, false),
+                   "grid build (ISS)");
         c->hmark("Q_iss_grid");
-        HIPCHK(launch_iss(s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
+        HIPCHK(launch_iss(reuse ? s.grid_l16 : s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
                           s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks),
                "iss launch");
@@ -1221,6 +1227,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
+    else if (k == "iss_grid") c->opt_iss_grid = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
     else if (k == "pre_fast") c->opt_pre_fast = value ? 1 : 0;
     else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;

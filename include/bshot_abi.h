@@ -288,6 +288,7 @@ int bshot_map_set_query_mode(bshot_map* m, int mode);
  *      the exact-kNN radius ladder; "ladder_front" 1 (default): two more small radii in front;
  *      "sr_start" 80 (default): percent scale of the ladder-start prediction (0: step 0); "sr_blocks" SR grid cap;
  *      "sr_xcd_chunk" 1024 (default): SR queries per XCD-local chunk of cell order (0: queries dealt round-robin);
+ *      "iss_grid" 1 (default): ISS on the SR ladder's finest grid when its cell >= 2 salient radii;
  *      "iss_cell" 2 (default) / 1: ISS grid cell in salient radii (grid options take effect at the
  *      next set_cloud); "iss_ovf_blocks", "iss_nms_blocks", "chunk_blocks" grid caps; "normals_seg"
  *      1 (default): keypoint normals from the first normal_max_nn entries of the SHOT neighbour
