@@ -117,6 +117,30 @@ def test_gmap_crafted_inserts_vs_host_map():
         od.close()
 
 
+def test_gmap_large_batches_both_sort_paths():
+    """A batch's block ids are ordered by a one-workgroup LDS sort up to 4096 keypoints and by the
+    rocprim radix sort past that; both must leave the replica equal to the host Map (sizes, and the
+    reference's block loop around several positions)."""
+    rng = np.random.default_rng(5)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=64))
+    hm = bshot_py.KeypointMap()
+    try:
+        for k in (4096, 6000, 1):
+            pts = np.round(rng.uniform(-6000, 6000, (k, 3))) * 10.0  # on the map's 10 mm grid
+            pts[:, 2] = np.round(rng.uniform(-300, 300, k)) * 10.0
+            pts = pts.astype(np.float32)
+            rec = _rec(pts, rng.uniform(0, 1, k).astype(np.float32), rng)
+            od.gpu_replica_insert(0, rec)
+            _host_add(hm, rec)
+            assert od.gpu_replica_size(0) == hm.size()
+            for pos in ([0.0, 0.0, 0.0], [40000.0, -30000.0, 0.0], [-55000.0, 52000.0, 1000.0]):
+                gx, gb = od.gpu_replica_query(0, np.array(pos, np.float32))
+                hx, hb = hm.query(np.array(pos, np.float32))
+                assert np.array_equal(_u(gx), _u(hx)) and np.array_equal(gb, hb)
+    finally:
+        od.close()
+
+
 def test_gmap_block_capacity_error_surfaces():
     """A 10 m block holds at most 4096 members in the GPU map (the insert workgroup's LDS image;
     DESIGN.md §3). Going past it is reported (BSHOT_ECAP), never silently dropped."""
