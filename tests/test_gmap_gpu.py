@@ -128,7 +128,7 @@ def test_gmap_large_batches_both_sort_paths():
         for k in (4096, 6000, 1):
             pts = np.round(rng.uniform(-6000, 6000, (k, 3))) * 10.0  # on the map's 10 mm grid
             pts[:, 2] = np.round(rng.uniform(-300, 300, k)) * 10.0
-            pts = pts.astype(np.float32)
+            pts = (pts + 0.0).astype(np.float32)  # +0, as the 10 mm quantisation writes it (never -0)
             rec = _rec(pts, rng.uniform(0, 1, k).astype(np.float32), rng)
             od.gpu_replica_insert(0, rec)
             _host_add(hm, rec)
