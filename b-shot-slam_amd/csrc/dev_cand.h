@@ -43,6 +43,7 @@ template <int GROUP, class F>
 __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs, int& epoch, float qx, float qy,
                                                   float qz, float rs2, unsigned int st, unsigned int cnt, int off,
                                                   int total, F& f, int part = 0, int nparts = 1) {
+    static_assert(GROUP >= 1 && GROUP <= CAND_GROUP, "CandLds::mark holds CAND_GROUP chunks of marks");
     const int lane = lane_id();
     const int cbase = (int)st - off;  // spts index of flattened candidate t is cbase(cell) + t
     const unsigned long long nonempty = __ballot(cnt > 0);
