@@ -297,7 +297,21 @@ def main():
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(bshot_py.Exchange.unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
-        xchg = bshot_py.Exchange(bytes(uid.cpu().numpy().tobytes()), world, rank, local, a.keypoints)
+        ok = 1
+        try:
+            xchg = bshot_py.Exchange(bytes(uid.cpu().numpy().tobytes()), world, rank, local, a.keypoints)
+        except bshot_py.BshotError as e:
+            print(f"rank {rank}: RCCL exchange unavailable ({e}); map offers go over torch.distributed", file=sys.stderr)
+            ok, xchg = 0, None
+        # every rank takes the same transport (a rank whose communicator failed would otherwise leave
+        # the others waiting in the all-gather)
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            if xchg is not None:
+                xchg.close()
+                xchg = None
+            a.map_bcast_py = True
     elif a.sim_peers > 0 and world == 1:
         xchg = bshot_py.Exchange(bshot_py.Exchange.unique_id(), 1, 0, local, a.keypoints)
 
@@ -577,7 +591,8 @@ def main():
                        "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
                        "map_size_readback": bool(a.map_sync),
                        "icp_iters": icp_it, "mutual_corr": round(corr, 1), "parallelism": f"frame-shard x{world}" +
-                       (" + RCCL map exchange" if a.map_bcast else "") +
+                       ((" + map exchange over torch.distributed" if a.map_bcast_py else " + RCCL map exchange")
+                        if a.map_bcast else "") +
                        (f" + RCCL map exchange (1 rank) with {a.sim_peers} simulated peers' replica inserts"
                         if a.sim_peers > 0 else "")},
             "roofline": roof,
