@@ -10,11 +10,13 @@ import numpy as np  # noqa: E402
 
 import bshot_py  # noqa: E402
 
-pc, _ = bshot_py.synth_sweep(3)
-c = bshot_py.Context(0)
+# DESCRIBE_CFG=5: BASELINE config 5 (VLP-128 style sweep, K = 4096, SHOT radius 5000 mm)
+cfg5 = os.environ.get("DESCRIBE_CFG") == "5"
+pc, _ = bshot_py.synth_sweep(3, sensor=1 if cfg5 else 0)
+c = bshot_py.Context(0, bshot_py.default_params(shot_radius=5000.0) if cfg5 else None)
 c.set_cloud(pc)
 idx, rat = c.seg_ratio()
-kp, _ = bshot_py.select_topk(idx, rat, 2048)
+kp, _ = bshot_py.select_topk(idx, rat, 4096 if cfg5 else 2048)
 kps = pc[kp]
 ref = None
 # arguments: name=value option sets ("chunk_blocks=2048,dev_plan=0"); none: the defaults
