@@ -144,6 +144,7 @@ struct bshot_ctx {
     int opt_diag_skip_icp = 0;  // diagnostic only: ICP returns the identity without running (never in a bench line)
     int opt_hist_pack = 1;      // SHOT apply: 1 several ranks per ds_add_f32 when the device passed the lane-order check
     int hf_pack_ok = 0;         // that check's result for this context's device (bshot_create)
+    int opt_rank_max = -1;      // k_shot_rank_wg's in-place threshold (-1: RK_RANKMAX; 0: every span sorted)
     int opt_rank_wg = 2;        // SHOT rank kernel: 0 wave per 64-rank chunk, 1 workgroup per keypoint, 2 by neighbourhood size
     int opt_sr_start = 80;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_grid = 1;       // ISS on the SR ladder's finest grid when its cell >= 2 x salient radius (0: own grid)

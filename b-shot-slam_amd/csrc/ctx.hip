@@ -479,6 +479,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
         A.rank_wg = rank_wg_for(c, k, c->seg_hint);
         A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
+        A.rank_max = c->opt_rank_max;
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
         c->stage_end(sg10, st);
@@ -547,6 +548,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.max_blocks = c->opt_chunk_blocks;
     A.rank_wg = rank_wg_for(c, k, total);
     A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
+    A.rank_max = c->opt_rank_max;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);
@@ -1222,6 +1224,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "icp_device") c->opt_icp_device = value ? 1 : 0;
     else if (k == "icp_host_delay_ms") c->opt_icp_host_delay_ms = value < 0 ? 0 : value;
     else if (k == "diag_skip_icp") c->opt_diag_skip_icp = value ? 1 : 0;  // diagnostic: the period without ICP
+    else if (k == "rank_max") c->opt_rank_max = value;
     else if (k == "hist_pack") c->opt_hist_pack = value ? 1 : 0;
     else if (k == "rank_wg") c->opt_rank_wg = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);

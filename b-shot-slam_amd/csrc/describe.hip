@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
                                                       const long long* __restrict__ offs,
                                                       const unsigned int* __restrict__ bstart,
                                                       const unsigned long long* __restrict__ seg,
-                                                      unsigned int* __restrict__ out) {
+                                                      unsigned int* __restrict__ out, unsigned int rank_max) {
     __shared__ unsigned long long st[RK_SPAN];
     __shared__ unsigned int sbs[SG_BUCKETS + 1];
     __shared__ int s_e;
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
         for (int b = b0 + t; b < e; b += RK_T) mb = max(mb, sbs[b + 1] - sbs[b]);
         if (mb) atomicMax(&s_maxb, mb);
         __syncthreads();
-        const bool rank_path = s_maxb <= RK_RANKMAX;
+        const bool rank_path = s_maxb <= rank_max;
         if (e == b0) {
             // bucket b0 alone exceeds the span: rank it from HBM
             const unsigned int s0 = lo, e0 = sbs[b0 + 1];
@@ -391,9 +391,10 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
 }
 
 hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long* offs, const unsigned int* bstart,
-                               const unsigned long long* seg, unsigned int* out, hipStream_t s) {
+                               const unsigned long long* seg, unsigned int* out, hipStream_t s, int rank_max) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_rank_wg<<<k, RK_T, 0, s>>>(k, R, perm, offs, bstart, seg, out);
+    bsk::k_shot_rank_wg<<<k, RK_T, 0, s>>>(k, R, perm, offs, bstart, seg, out,
+                                             rank_max < 0 ? (unsigned int)RK_RANKMAX : (unsigned int)rank_max);
     return hipGetLastError();
 }
 

@@ -818,7 +818,7 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
         if (A.n_chunks > 0) {
             bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
             if (A.rank_wg) {
-                if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s))) return e;
+                if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s, A.rank_max))) return e;
             } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
                                              A.max_blocks))) {
                 return e;

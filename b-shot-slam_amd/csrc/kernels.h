@@ -39,7 +39,7 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
 // d2 from the points with the gather's expression, bit-identical)
 // the same, a workgroup per keypoint in perm's order (spans of whole buckets staged in LDS)
 hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long* offs, const unsigned int* bstart,
-                               const unsigned long long* seg, unsigned int* out, hipStream_t s);
+                               const unsigned long long* seg, unsigned int* out, hipStream_t s, int rank_max = -1);
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
                             hipStream_t s, int max_blocks = 0);
@@ -126,6 +126,7 @@ struct Describe2Args {
     const unsigned int* bstart = nullptr;  // per-keypoint bucket starts of the bucket-grouped segment
     int max_blocks = 0;  // grid cap of the chunk kernels (0: one block per 4 chunks)
     int rank_wg = 0;     // 1: k_shot_rank_wg (workgroup per keypoint, large neighbourhoods); 0: k_shot_rank
+    int rank_max = -1;   // k_shot_rank_wg: spans whose buckets all hold <= this many keys rank in place (-1: default)
     int hf_pack = 1;     // 1: the SHOT apply packs several ranks per ds_add_f32 (needs lds_lane_order_check() == 0)
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);

@@ -44,6 +44,25 @@ def test_seg_ratio_bit_exact(ctx, cloud, sr_ref, ladder):
     ctx.set_option("ladder_grids", 4)
 
 
+@pytest.mark.parametrize("opts", [{"sr_xcd_chunk": 0}, {"sr_xcd_chunk": 4096}, {"sr_start": 0}, {"sr_start": 300},
+                                  {"sr_blocks": 1024}])
+def test_seg_ratio_schedules_agree(ctx, cloud, sr_ref, opts):
+    """The SR launch's query schedule (XCD-local chunks or round-robin, a persistent grid), and the
+    ladder's start step only change the work done, never a ratio."""
+    defaults = {"sr_xcd_chunk": 1024, "sr_start": 80, "sr_blocks": 0}
+    try:
+        for k, v in opts.items():
+            ctx.set_option(k, v)
+        ctx.set_cloud(cloud)
+        idx, rat = ctx.seg_ratio()
+    finally:
+        for k in opts:
+            ctx.set_option(k, defaults[k])
+    ridx, rrat = sr_ref
+    np.testing.assert_array_equal(idx, ridx)
+    np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32))
+
+
 def _edge_cloud():
     """Sparse far points, a dense clump whose neighbourhoods overflow the kNN list (> KNN_CAP keys:
     the streaming selection), exact duplicates, origin points, NaN/inf rows and points beyond the
@@ -80,9 +99,15 @@ def test_topk_keypoints_exact(sr_ref):
         np.testing.assert_array_equal(a[0], b[0])
 
 
-def test_iss_exact(ctx, cloud):
-    ctx.set_cloud(cloud)
-    got = ctx.iss()
+@pytest.mark.parametrize("iss_grid", [1, 0])
+def test_iss_exact(ctx, cloud, iss_grid):
+    """ISS on the SR ladder's finest grid (default) and on a grid of its own."""
+    ctx.set_option("iss_grid", iss_grid)
+    try:
+        ctx.set_cloud(cloud)
+        got = ctx.iss()
+    finally:
+        ctx.set_option("iss_grid", 1)
     ref, _ = orc.iss(cloud)
     np.testing.assert_array_equal(got, ref)
 
@@ -323,11 +348,12 @@ def test_ransac_scores_kernel(ctx, nidx, nhyp):
     assert g.min() >= 0 and g.max() <= nidx
 
 
-@pytest.mark.parametrize("rank_wg", [0, 1])
-def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg):
+@pytest.mark.parametrize("rank_wg,rank_max", [(0, -1), (1, -1), (1, 0), (1, 1 << 30)])
+def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg, rank_max):
     """The two SHOT rank kernels (a wave per 64-rank chunk; a workgroup per keypoint staging
-    whole-bucket spans in LDS) give the host-planned describe's bits and histograms exactly, on
-    the device plan and on the host plan."""
+    whole-bucket spans in LDS, each span ranked in place or bitonic-sorted: rank_max 0 sorts every
+    span, 2^30 ranks every span in place) give the host-planned describe's bits and histograms
+    exactly, on the device plan and on the host plan."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 2048)
     kps = cloud[kidx]
@@ -336,6 +362,7 @@ def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg):
     ctx.set_option("dev_plan_hint", 0)
     ref_bits, ref_shot, _ = ctx.describe(kps)
     ctx.set_option("rank_wg", rank_wg)
+    ctx.set_option("rank_max", rank_max)
     try:
         for hint in (0, 1 << 30):
             ctx.set_option("dev_plan_hint", hint)
@@ -344,6 +371,7 @@ def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg):
             np.testing.assert_array_equal(shot.view(np.uint32), ref_shot.view(np.uint32))
     finally:
         ctx.set_option("rank_wg", 2)
+        ctx.set_option("rank_max", -1)
 
 
 def test_lds_lane_order_check(ctx):
