@@ -33,7 +33,9 @@ namespace bsk {
 #define KNN_CAP 704
 #endif
 #define KNN_PRE 512  // largest prefix the counting sort handles (8 keys per lane)
+#ifndef KNN_WAVES
 #define KNN_WAVES 2
+#endif
 #ifndef SR_DIAG_NOFIN
 #define SR_DIAG_NOFIN 0  // diagnostic: 1 = skip the ratio computation (timing of the selection alone)
 #endif
