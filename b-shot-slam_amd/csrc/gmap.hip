@@ -292,17 +292,20 @@ __device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long lon
 // are tested, the insert position is found (lane 0, um::) and the bucket-order list is shifted by
 // the whole workgroup. After a replacement the remaining candidates are tested against every member.
 #define GM_INS_T 512
+#define GM_SMALL_N 1024   // members: buckets stay <= 1109 (the libstdc++ prime after 541)
+#define GM_SMALL_BK 1152
+template <int LN, int LBK>
 __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
                                                           const int* __restrict__ seg, int slot_base) {
     // the block's LDS image (142 KiB, one workgroup per CU; a sweep touches ~100 blocks): list
     // indices as ushort, hash codes as u32 (10 mm-grid keys), each member's current position + ratio,
     // and the batch's per-candidate results against the staged members
-    __shared__ unsigned short s_ord[GM_LDS_N], s_pos[GM_LDS_N], s_nxt[GM_LDS_N], s_bk[GM_LDS_BK];
-    __shared__ int s_slot[GM_LDS_N];
-    __shared__ unsigned int s_code[GM_LDS_N];
-    __shared__ float4 s_mem[GM_LDS_N];
-    __shared__ unsigned short s_hit0[GM_LDS_N];  // staged member at the candidate's position (0xFFFF: none)
-    __shared__ unsigned char s_rej0[GM_LDS_N];   // rejected by a staged member
+    __shared__ unsigned short s_ord[LN], s_pos[LN], s_nxt[LN], s_bk[LBK];
+    __shared__ int s_slot[LN];
+    __shared__ unsigned int s_code[LN];
+    __shared__ float4 s_mem[LN];
+    __shared__ unsigned short s_hit0[LN];  // staged member at the candidate's position (0xFFFF: none)
+    __shared__ unsigned char s_rej0[LN];   // rejected by a staged member
     __shared__ int s_rej, s_hit, s_at, s_nb, s_nr;
     __shared__ GBlock s_B;
     const int tid = threadIdx.x;
@@ -311,10 +314,13 @@ __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsig
         const int j0 = seg[3 * sg], cnt = seg[3 * sg + 1], b = seg[3 * sg + 2];
         if (cnt == 0) continue;  // a run whose block could not be created (GM_ERR is set)
         GBlock B = m.blk[b];
-        if (B.n + cnt > GM_LDS_N) {
-            if (tid == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
+        // two instantiations split the blocks: the small LDS image (<= GM_SMALL_N members after the
+        // batch) leaves the CU room for other kernels' workgroups; the full one takes the rest
+        if (B.n + cnt > LN) {
+            if (LN == GM_LDS_N && tid == 0) atomicOr(&m.ctr[GM_ERR], 4);  // block larger than the LDS image
             continue;
         }
+        if (LN == GM_LDS_N && B.n + cnt <= GM_SMALL_N) continue;
         // stage the block
         for (int i = tid; i < B.n; i += GM_INS_T) {
             s_ord[i] = (unsigned short)m.ipool[B.ord + i];
@@ -705,7 +711,10 @@ static int gmap_run_insert(bshot_ctx* c, GMap& g, int k, bool sync, hipStream_t 
     // at most: more workgroups than that only occupy CUs to exit. Replica inserts (another stream,
     // off the critical chain) take fewer, leaving the CUs to the lookahead.
     const int wgs = std::min(k, st == c->stream ? 256 : 64);
-    bsk::k_gmap_insert<<<wgs, GM_INS_T, 0, st>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
+    bsk::k_gmap_insert<GM_SMALL_N, GM_SMALL_BK><<<wgs, GM_INS_T, 0, st>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
+    // blocks past GM_SMALL_N members are few: a handful of full-image workgroups (each needs a whole
+    // CU's LDS to start) grid-stride over the segments
+    bsk::k_gmap_insert<GM_LDS_N, GM_LDS_BK><<<std::min(k, 16), GM_INS_T, 0, st>>>(dev_view(g), g.vals.p + k, g.seg.p, g.slots);
     HIPCHK(hipGetLastError(), "gmap insert launch");
     g.slots += k;
     HIPCHK(kcopy(g.p_ctr.p, g.ctr.p, sizeof(int) * GM_QTOT, st), "D2H map counters");
