@@ -550,11 +550,19 @@ __global__ void __launch_bounds__(64 * HF_WAVES) HF_ATTR k_hist_fused(const floa
     for (int j = 0; j < 6; ++j) ev[j] = ok0 ? eig[8 * (size_t)q + j] : 0.0;
     if (ok0) {
         int pt = 0, pn = 0;
-        for (int i0 = 0; i0 < n; i0 += 64 * HF_WAVES) {
+        // pipelined like the record producers: the next pass's point and the index after it are
+        // loaded while this pass's dot products run
+        constexpr int SP = 64 * HF_WAVES;
+        auto sidx = [&](int i) -> unsigned int { return i < n ? seg[o + i] : 0u; };
+        float4 pnext = pts4[sidx((int)threadIdx.x)];
+        unsigned int inext = sidx((int)threadIdx.x + SP);
+        for (int i0 = 0; i0 < n; i0 += SP) {
             const int i = i0 + (int)threadIdx.x;
             bool a = false, c = false;
+            const float4 p = pnext;
+            pnext = pts4[inext];
+            inext = sidx(i + 2 * SP);
             if (i < n) {
-                const float4 p = pts4[seg[o + i]];
                 if (!(p.x == kx && p.y == ky && p.z == kz)) {
                     const double vx = (double)(p.x - kx), vy = (double)(p.y - ky), vz = (double)(p.z - kz);
                     a = ((vx * ev[0] + vy * ev[1]) + vz * ev[2]) >= 0;
