@@ -173,6 +173,7 @@ struct bshot_ctx {
     // load-balanced SHOT (describe2.hip)
     DBuf<int4> plan;
     DBuf<int> cb, owner, okf, perm;
+    DBuf<int4> cinfo;  // per-chunk records for the chunk kernels (k_chunk_owner)
     DBuf<double> csum, eig;
     PinBuf<long long> p_offs;
     PinBuf<int> p_plan;  // plan (4 ints per item) then cb (k + 1)

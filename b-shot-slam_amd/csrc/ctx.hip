@@ -455,6 +455,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         HIPCHK(c->cb.ensure((size_t)k + 1), "alloc cb");
         HIPCHK(c->perm.ensure(k), "alloc perm");
         HIPCHK(c->owner.ensure((size_t)chunk_cap), "alloc owner");
+        HIPCHK(c->cinfo.ensure((size_t)chunk_cap), "alloc chunk records");
         HIPCHK(c->csum.ensure(8 * (size_t)chunk_cap), "alloc csum");
         HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
         HIPCHK(c->okf.ensure(k), "alloc okf");
@@ -479,6 +480,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
         A.rank_wg = rank_wg_for(c, k, c->seg_hint);
         A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
+        A.cinfo = seg_cap < 0x7FFFFFFFll ? c->cinfo.p : nullptr;
         A.rank_max = c->opt_rank_max;
         const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
         HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
@@ -531,6 +533,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     hcb[k] = cbr;
     HIPCHK(c->cb.ensure((size_t)k + 1), "alloc cb");
     HIPCHK(c->owner.ensure(cbr > 0 ? (size_t)cbr : 1), "alloc owner");
+    HIPCHK(c->cinfo.ensure(cbr > 0 ? (size_t)cbr : 1), "alloc chunk records");
     HIPCHK(c->csum.ensure(8 * (size_t)(cbr > 0 ? cbr : 1)), "alloc csum");
     HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
     HIPCHK(c->okf.ensure(k), "alloc okf");
@@ -549,6 +552,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.rank_wg = rank_wg_for(c, k, total);
     A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
     A.rank_max = c->opt_rank_max;
+    A.cinfo = total < 0x7FFFFFFFll ? c->cinfo.p : nullptr;
     const int sg10 = c->stage_begin(BSHOT_STAGE_SHOT_SORT, st);
     HIPCHK(launch_describe2(A, 0, st), "describe2 sort");
     c->stage_end(sg10, st);

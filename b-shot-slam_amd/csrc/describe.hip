@@ -210,15 +210,26 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
                                                    const int* __restrict__ cb, const int* __restrict__ owner,
                                                    const unsigned int* __restrict__ bstart,
                                                    const unsigned long long* __restrict__ seg,
-                                                   unsigned int* __restrict__ out) {
+                                                   unsigned int* __restrict__ out, const int4* __restrict__ cinfo) {
     __shared__ unsigned long long stage[4][SR_STAGE];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
     for (int c = blockIdx.x * 4 + wave; c < cb[k]; c += gridDim.x * 4) [&]() {
-        const int q = owner[c];
-        const long long o = offs[q];
-        const int n = (int)(offs[q + 1] - o);
-        const int c0 = (c - cb[q]) * 64;
+        int q, n, c0;
+        long long o;
+        if (cinfo) {
+            // one load: keypoint, chunk index, segment length and offset (k_chunk_owner)
+            const int4 ci = cinfo[c];
+            q = ci.x;
+            c0 = ci.y * 64;
+            n = ci.z;
+            o = (long long)(unsigned int)ci.w;
+        } else {
+            q = owner[c];
+            o = offs[q];
+            n = (int)(offs[q + 1] - o);
+            c0 = (c - cb[q]) * 64;
+        }
         const int i = c0 + lane;
         const int last = min(n, c0 + 64) - 1;  // last valid rank of the chunk (wave-uniform)
         const float R2 = (float)((double)R * (double)R);
@@ -400,11 +411,11 @@ hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long*
 
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
-                            hipStream_t s, int max_blocks) {
+                            hipStream_t s, const int4* cinfo, int max_blocks) {
     if (k <= 0 || n_chunks <= 0) return hipSuccess;
     int blocks = (n_chunks + 3) / 4;
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    bsk::k_shot_rank<<<blocks, 256, 0, s>>>(k, R, offs, cb, owner, bstart, seg, out);
+    bsk::k_shot_rank<<<blocks, 256, 0, s>>>(k, R, offs, cb, owner, bstart, seg, out, cinfo);
     return hipGetLastError();
 }
 

@@ -24,11 +24,20 @@
 
 namespace bsk {
 
-// owner[c] = keypoint of chunk c (block per keypoint)
-__global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restrict__ cb, int* __restrict__ owner) {
+// owner[c] = keypoint of chunk c (block per keypoint); with cinfo, also the chunk's record
+// {keypoint, chunk index in the keypoint, segment length, segment offset} in one 16-B load, so the
+// chunk kernels skip the owner -> offsets/chunk-base round trip (segments below 2^31 keys)
+__global__ void __launch_bounds__(256) k_chunk_owner(int k, const int* __restrict__ cb, int* __restrict__ owner,
+                                                     const long long* __restrict__ offs, int4* __restrict__ cinfo) {
     const int q = blockIdx.x;
     if (q >= k) return;
-    for (int c = cb[q] + threadIdx.x; c < cb[q + 1]; c += 256) owner[c] = q;
+    const int c0 = cb[q], c1 = cb[q + 1];
+    const long long o = cinfo ? offs[q] : 0;
+    const int n = cinfo ? (int)(offs[q + 1] - o) : 0;
+    for (int c = c0 + threadIdx.x; c < c1; c += 256) {
+        owner[c] = q;
+        if (cinfo) cinfo[c] = make_int4(q, c - c0, n, (int)o);
+    }
 }
 
 // The 7 butterfly sums of wave_tree_sum_d (partners lane ^ 32, ^ 16, ..., ^ 1 in that order), all at
@@ -86,13 +95,19 @@ __global__ void __launch_bounds__(256) k_lrf_chunks(const float4* __restrict__ p
                                                     int k, float R, const long long* __restrict__ offs,
                                                     const int* __restrict__ cb, const int* __restrict__ owner,
                                                     const unsigned int* __restrict__ seg,
-                                                    double* __restrict__ csum) {
+                                                    double* __restrict__ csum, const int4* __restrict__ cinfo) {
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
     for (int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cb[k]; c += gridDim.x * 4) {
-        const int q = owner[c];
-        const long long o = offs[q];
-        lrf_chunk_terms(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], R, seg + o, (int)(offs[q + 1] - o), c - cb[q],
-                        csum + 8 * (size_t)c);
+        if (cinfo) {
+            const int4 ci = cinfo[c];
+            lrf_chunk_terms(pts4, kps[3 * ci.x], kps[3 * ci.x + 1], kps[3 * ci.x + 2], R, seg + (unsigned int)ci.w, ci.z,
+                            ci.y, csum + 8 * (size_t)c);
+        } else {
+            const int q = owner[c];
+            const long long o = offs[q];
+            lrf_chunk_terms(pts4, kps[3 * q], kps[3 * q + 1], kps[3 * q + 2], R, seg + o, (int)(offs[q + 1] - o),
+                            c - cb[q], csum + 8 * (size_t)c);
+        }
     }
 }
 
@@ -824,10 +839,10 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (A.max_blocks > 0 && cblocks > A.max_blocks) cblocks = A.max_blocks;
     if (part == 0) {
         if (A.n_chunks > 0) {
-            bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner);
+            bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner, A.offs, A.cinfo);
             if (A.rank_wg) {
                 if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s, A.rank_max))) return e;
-            } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s,
+            } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s, A.cinfo,
                                              A.max_blocks))) {
                 return e;
             }
@@ -837,7 +852,7 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
     if (part == 1) {
         if (A.n_chunks > 0) {
             bsk::k_lrf_chunks<<<cblocks, 256, 0, s>>>(A.pts4, A.kps, A.k, A.R, A.offs, A.cb, A.owner, A.sorted,
-                                                       A.csum);
+                                                       A.csum, A.cinfo);
         }
         // nmax > 0: the keypoint normals from the sorted segments in the same launch
         bsk::k_lrf_eig<<<(A.k + LE_WAVES / 2 - 1) / (LE_WAVES / 2), 64 * LE_WAVES, 0, s>>>(

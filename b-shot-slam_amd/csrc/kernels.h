@@ -42,7 +42,7 @@ hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long*
                                const unsigned long long* seg, unsigned int* out, hipStream_t s, int rank_max = -1);
 hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
                             const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
-                            hipStream_t s, int max_blocks = 0);
+                            hipStream_t s, const int4* cinfo = nullptr, int max_blocks = 0);
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
@@ -106,6 +106,7 @@ struct Describe2Args {
     float R = 0.f;
     const int* cb = nullptr;               // k + 1 chunk offsets
     int* owner = nullptr;                  // keypoint of every chunk
+    int4* cinfo = nullptr;                 // per chunk {keypoint, chunk index, length, offset} (offsets < 2^31), or null
     const int* perm = nullptr;             // keypoints by descending neighbourhood size
     const long long* offs = nullptr;       // k + 1 segment offsets
     const float4* pts4 = nullptr;
