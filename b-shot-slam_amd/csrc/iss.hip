@@ -131,7 +131,9 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
 #ifndef ISS_CELL_ORDER
 #define ISS_CELL_ORDER 1
 #endif
+#ifndef ISS_LCAP
 #define ISS_LCAP 32
+#endif
 #define ISS_LBLOCK 64
 
 template <int N>
@@ -194,6 +196,7 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
                                                         float salient, float nonmax, int min_nn, double g21,
                                                         double g32, double* __restrict__ third, int* __restrict__ ovf,
                                                         unsigned int* __restrict__ nml, int* __restrict__ nmc) {
+    static_assert(ISS_LCAP == 16 || ISS_LCAP == 32, "the sort networks cover 8, 16 and 32 keys");
     __shared__ unsigned long long keys[ISS_LCAP][ISS_LBLOCK];  // [slot][thread]: conflict-free columns
     const int t = threadIdx.x;
 #if ISS_CELL_ORDER
@@ -282,7 +285,9 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
         int cnm;
         if (wmax <= 8) cnm = iss_sum_sorted<8>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
         else if (wmax <= 16) cnm = iss_sum_sorted<16>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+#if ISS_LCAP > 16
         else cnm = iss_sum_sorted<32>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+#endif
         out = iss_third(sm, g21, g32);
         nmc[q] = cnm;
     }
