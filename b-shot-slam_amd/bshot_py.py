@@ -147,7 +147,12 @@ def _ptr(a):
 
 
 class BshotError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
+
+
+ESTALE = -5  # BSHOT_ESTALE: a frame-sharded record described over other normals than the sequence's
 
 
 class Context:
@@ -163,7 +168,7 @@ class Context:
 
     def _chk(self, rc, what):
         if rc < 0:
-            raise BshotError(f"{what}: {self.L.bshot_last_error(self.h).decode()} ({rc})")
+            raise BshotError(f"{what}: {self.L.bshot_last_error(self.h).decode()} ({rc})", rc)
         return rc
 
     def close(self):
@@ -419,7 +424,7 @@ class Odometry:
 
     def _chk(self, rc, what):
         if rc < 0:
-            raise BshotError(f"{what}: {self.L.bshot_odom_last_error(self.h).decode()} ({rc})")
+            raise BshotError(f"{what}: {self.L.bshot_odom_last_error(self.h).decode()} ({rc})", rc)
         return rc
 
     def process(self, xyz):
@@ -448,13 +453,16 @@ class Odometry:
     def extract_device(self, dptr, n):
         """Frame-sharded mode: the extraction half of a device sweep as a float32 record
         (bshot_odom_extract_device); the set_next lookahead applies."""
-        cap = 8 + 15 * max(1, self.params.num_keypoints) + 3 * (n + 1)  # k <= K, ISS points <= n
+        K = max(1, self.params.num_keypoints)
+        cap = 8 + 15 * K + 3 * (n + 1) + 4 * min(n, K)  # k <= K, ISS points <= n, normals slots min(n, K)
         rec = np.zeros(cap, np.float32)
         ln = self._chk(self.L.bshot_odom_extract_device(self.h, P(dptr), n, _ptr(rec), cap), "odom_extract_device")
         return rec[:ln].copy()
 
     def process_record(self, rec):
-        """Frame-sharded mode: the chain half of the next sweep from an extraction record."""
+        """Frame-sharded mode: the chain half of the next sweep from an extraction record. Raises
+        BshotError with code ESTALE (and changes nothing) when the record was described over other
+        stale normals than the sequence's: process that sweep with process[_device] instead."""
         rec = np.ascontiguousarray(rec, np.float32)
         st = FrameStats()
         self._chk(self.L.bshot_odom_process_record(self.h, _ptr(rec), len(rec), ctypes.byref(st)), "odom_process_record")

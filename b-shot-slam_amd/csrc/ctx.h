@@ -263,6 +263,7 @@ struct bshot_ctx {
     PinBuf<uint32_t> p_a, p_bits;
     PinBuf<int> p_left, p_gidx, p_err;
     PinBuf<float> p_g3, p_src, p_tgt, p_xyz;
+    PinBuf<float> p_nrm;  // persistent-normals slots read / written by the frame-sharded mode
     hipEvent_t ev_xyz = nullptr;  // the staged host cloud (p_xyz) has been copied
     PinBuf<unsigned long long> p_best;
     PinBuf<long long> p_i64;
@@ -309,6 +310,11 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k);
 int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k);
 int ctx_normals_restore(bshot_ctx* c);
 void ctx_normals_discard(bshot_ctx* c);
+// frame-sharded mode: slots [0, m) of the persistent normals array to the host (m <= its logical
+// size; synchronous on the main stream), and a whole state put in place: logical size `size`, slots
+// [0, m) from the host, [m, size) zero (synchronous)
+int ctx_normals_read(bshot_ctx* c, int m, float* out);
+int ctx_normals_write(bshot_ctx* c, int size, int m, const float* slots);
 // after a describe's error word reached the host (err[0..3] as copied from c->errw): true when the
 // describe must be run again -- errw bit 16, a device plan over capacity (the re-run plans on the
 // host; the capacity hint grows to the total the device counted)

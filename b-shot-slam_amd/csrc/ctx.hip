@@ -397,6 +397,31 @@ int ctx_normals_restore(bshot_ctx* c) {
 
 void ctx_normals_discard(bshot_ctx* c) { c->normals_snap_size = -1; }
 
+int ctx_normals_read(bshot_ctx* c, int m, float* out) {
+    if (m < 0 || m > c->normals_size) return c->fail("normals read past the logical size", BSHOT_EINVAL);
+    if (m == 0) return BSHOT_OK;
+    HIPCHK(c->p_nrm.ensure(4 * (size_t)m), "alloc pinned normals");
+    HIPCHK(kcopy(c->p_nrm.p, c->normals.p, sizeof(float4) * m, c->stream), "D2H normals");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync normals");
+    std::memcpy(out, c->p_nrm.p, sizeof(float4) * m);
+    return BSHOT_OK;
+}
+
+int ctx_normals_write(bshot_ctx* c, int size, int m, const float* slots) {
+    if (size < 0 || m < 0 || m > size) return c->fail("normals state: bad sizes", BSHOT_EINVAL);
+    HIPCHK(c->normals.ensure(std::max(size, 1)), "alloc normals");
+    if (m > 0) {
+        HIPCHK(c->p_nrm.ensure(4 * (size_t)m), "alloc pinned normals");
+        std::memcpy(c->p_nrm.p, slots, sizeof(float4) * m);
+        HIPCHK(kcopy(c->normals.p, c->p_nrm.p, sizeof(float4) * m, c->stream), "H2D normals");
+    }
+    if (size > m) HIPCHK(kfill(c->normals.p + m, 0, sizeof(float4) * (size - m), c->stream), "zero normals");
+    HIPCHK(hipStreamSynchronize(c->stream), "sync normals");
+    c->normals_size = size;
+    c->normals_snap_size = -1;
+    return BSHOT_OK;
+}
+
 // keypoints already in c->kps (device, k x 3)
 // the SHOT rank kernel for k keypoints with about `total` neighbours: the workgroup-per-keypoint
 // kernel streams large neighbourhoods (config 5: ~28k per keypoint, 2.0 -> ? ms), the wave-per-chunk
@@ -960,6 +985,7 @@ void bshot_destroy(bshot_ctx* c) {
     c->ma.release(); c->lbest.release(); c->left.release();
     c->p_a.release(); c->p_bits.release(); c->p_left.release(); c->p_gidx.release(); c->p_err.release();
     c->p_g3.release(); c->p_src.release(); c->p_tgt.release(); c->p_best.release(); c->p_i64.release(); c->p_xyz.release();
+    c->p_nrm.release(); c->normals_snap.release();
     if (c->ev_xyz) (void)hipEventDestroy(c->ev_xyz);
     c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
     c->sbh.release(); c->sbst.release(); c->kidx.release(); c->p_kidx.release(); c->p_kps3.release();

@@ -296,7 +296,7 @@ __device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long lon
 #define GM_SMALL_BK 1152
 template <int LN, int LBK>
 __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
-                                                          const int* __restrict__ seg, int slot_base) {
+                                                          int* __restrict__ seg, int slot_base) {
     // the block's LDS image (142 KiB, one workgroup per CU; a sweep touches ~100 blocks): list
     // indices as ushort, hash codes as u32 (10 mm-grid keys), each member's current position + ratio,
     // and the batch's per-candidate results against the staged members
@@ -469,6 +469,9 @@ __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsig
                 m.ipool[Bw.bk + i] = v == (unsigned short)um::UM_EMPTY ? um::UM_EMPTY : (v == (unsigned short)um::UM_BB ? um::UM_BB : (int)v);
             }
         }
+        // the segment is done: the small-image launch owns it (it decided from B.n before its own
+        // insert), so the full-image launch that follows must not take it again after B.n has grown
+        if (LN != GM_LDS_N && tid == 0) seg[3 * sg + 1] = 0;
         __syncthreads();
     }
 }

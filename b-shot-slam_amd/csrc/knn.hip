@@ -4,13 +4,15 @@
 //
 // Selection semantics (FLANN KNNRadiusResultSet, sorted): the max_nn smallest (d2, idx) with
 // d2 < r2, in ascending (d2, idx) order. One wavefront per query:
-//   1. radius ladder rs in {r/8, r/4 (fine grid, cell r/8), r/2, r (coarse grid, cell r/2)}: LDS
-//      histogram of d2 over [0, rs^2); stop at the first rs with >= max_nn hits (then every one of
-//      the max_nn nearest lies strictly inside rs) -- exact;
-//   2. the histogram's crossing bucket bounds the prefix; refine (<= 3 levels x 512 buckets) only
-//      if prefix + boundary bucket exceed the 1024-entry LDS list;
-//   3. collect the prefix into LDS as u64 keys (d2 bits << 32 | idx), bitonic sort;
-//   4. ordered float reductions in rank order exactly as PCL (computeCentroid, covariance).
+//   1. radius ladder rs = r * 2^(-k/2) for k = 8 .. 0 (9 steps, r/16 .. r; ladder mode 2, the
+//      default), each step streamed from the nested hashed grid whose cell is rs/2 or rs/sqrt(2)
+//      (r/16 for the two front steps); the first step is predicted from the query's own-cell counts
+//      (ladder_start). Stop at the first rs with >= max_nn points inside (then every one of the
+//      max_nn nearest lies strictly inside rs) -- exact whatever the start;
+//   2. that step also stored its first KNN_CAP in-radius keys (d2 bits << 32 | idx) in LDS: a
+//      KNN_NB-bucket d2 histogram of them bounds the prefix, and a counting sort + in-bucket rank
+//      orders it in place (the rare crowded cases re-stream with <= 3 refinement levels);
+//   3. ordered float reductions in rank order exactly as PCL (computeCentroid, covariance).
 #include <hip/hip_runtime.h>
 
 #include "bshot_math.h"

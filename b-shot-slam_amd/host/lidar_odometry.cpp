@@ -157,6 +157,7 @@ void LidarOdometry::setSrcFrame(Frame::Ptr src) {
     src_ = src;
     src_pc_ = *src_->getPointCloud();
     src_dev_ = nullptr;
+    src_ext_ = nullptr;
     src_n_ = (int)src_pc_.size();
     check(bshot_set_cloud(ctx_, src_n_ ? &src_pc_[0][0] : nullptr, src_n_), "setSrcFrame");
 }
@@ -169,6 +170,7 @@ void LidarOdometry::setSrcFrameDevice(Frame::Ptr src, const float* d_xyz, int n)
     src_ = src;
     src_pc_.clear();
     src_dev_ = d_xyz;
+    src_ext_ = nullptr;
     src_n_ = n;
     check(bshot_set_cloud_device(ctx_, d_xyz, n), "setSrcFrameDevice");
 }
@@ -192,7 +194,10 @@ void LidarOdometry::setSrcFrameExtracted(Frame::Ptr src, std::shared_ptr<const E
     ready_ = la;
     src_ = src;
     src_pc_.clear();
-    src_dev_ = la->d_xyz;
+    // the record's address is an identity token only: it is no device cloud (issKpDetection must not
+    // restore it) and it dangles once the caller's record is gone
+    src_dev_ = nullptr;
+    src_ext_ = la->d_xyz;
     src_n_ = la->n;
 }
 
@@ -205,6 +210,14 @@ LidarOdometry::Extracted LidarOdometry::extracted() const {
     e.ratios = seg_ratios_;
     e.words.resize(11 * cloud1_bshot_.size());
     for (size_t i = 0; i < cloud1_bshot_.size(); ++i) bits_to_words(cloud1_bshot_[i].bits, &e.words[11 * i]);
+    return e;
+}
+
+LidarOdometry::Extracted LidarOdometry::extractedWithNormals() {
+    Extracted e = extracted();
+    const int m = std::min(e.n_points, prm_.num_keypoints);
+    e.normals.assign(4 * (size_t)std::max(m, 0), 0.f);
+    if (m > 0) check(bsh::ctx_normals_read(ctx_, m, e.normals.data()), "read normals");
     return e;
 }
 
@@ -369,7 +382,7 @@ void LidarOdometry::extractKeypoints() {
     TicToc t_ex;
     const int n = src_n_;
     stats_.n_points = n;
-    if (ready_ && ready_->d_xyz == src_dev_ && ready_->n == n) {
+    if (ready_ && static_cast<const void*>(ready_->d_xyz) == srcId() && ready_->n == n) {
         // computed ahead by the worker thread (prefetchFrameDevice)
         const Lookahead& la = *ready_;
         stats_.n_valid_ratios = la.nv;
@@ -388,6 +401,7 @@ void LidarOdometry::extractKeypoints() {
         stats_.host_ms[0] = (float)t_ex.toc();
         return;
     }
+    if (src_ext_) throw std::runtime_error("extractKeypoints: the external frame's record is gone");
     // A1 + A2 (src/lidar_odometry.cpp:51-153)
     std::vector<int32_t> idx(n > 0 ? n : 1), kidx(prm_.num_keypoints > 0 ? prm_.num_keypoints : 1);
     std::vector<float> ratio(n > 0 ? n : 1), kr(kidx.size());
@@ -427,7 +441,7 @@ void LidarOdometry::computeDescriptors() {
     // A4-A7 (src/lidar_odometry.cpp:173-184); keypoints are already on the device (ctx->kps)
     TicToc t_d;
     const int k = (int)cloud1_kps_.size();
-    if (ready_ && ready_->d_xyz == src_dev_ && ready_->n == src_n_) {
+    if (ready_ && static_cast<const void*>(ready_->d_xyz) == srcId() && ready_->n == src_n_) {
         const std::vector<uint32_t>& w = ready_->words;
         cloud1_bshot_.resize(k);
         auto desc = std::make_shared<std::vector<std::bitset<352>>>();
@@ -443,6 +457,7 @@ void LidarOdometry::computeDescriptors() {
         stats_.host_ms[2] = (float)t_d.toc();
         return;
     }
+    if (src_ext_) throw std::runtime_error("computeDescriptors: the external frame's record is gone");
     check(bsh::ctx_describe_dev(ctx_, k), "describe");
     check(ctx_->p_bits.ensure(11 * (size_t)(k > 0 ? k : 1)) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned bits");
     check(ctx_->p_err.ensure(4) == hipSuccess ? BSHOT_OK : BSHOT_EHIP, "alloc pinned err");
@@ -736,9 +751,10 @@ PointCloudXYZ LidarOdometry::issKpDetection(const PointCloudXYZ& kps) {
     PointCloudXYZ out;
     for (int i = 0; i < ni; ++i) out.push_back(kps[iss[i]]);
     // restore the source cloud
+    // (an external frame has no cloud on this context: nothing to restore)
     if (src_n_ > 0) {
         if (src_dev_) check(bshot_set_cloud_device(ctx_, src_dev_, src_n_), "restore cloud");
-        else check(bshot_set_cloud(ctx_, &src_pc_[0][0], src_n_), "restore cloud");
+        else if (!src_pc_.empty()) check(bshot_set_cloud(ctx_, &src_pc_[0][0], src_n_), "restore cloud");
     }
     return out;
 }

@@ -1,6 +1,7 @@
 // odom_abi.cpp -- C ABI over myslam::LidarOdometry: the headless odometry_test frame loop
 // (test/odometry_test.cpp:159-194, test/kp_test.cpp:159-181) plus the map-delta records used by
 // the multi-GPU throughput mode (BASELINE config 4). No exception crosses the ABI.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -35,6 +36,12 @@ struct bshot_odom {
     int next2_n = 0;
     std::FILE* metrics = nullptr;  // per-sweep JSON lines (bshot_odom_set_metrics_file / BSHOT_METRICS)
     long long sweep = 0;
+    // frame-sharded chain owner (bshot_odom_process_record): the sequence's own persistent normals
+    // array (include/bshot_bits.h:58-87) -- logical size and slots [0, min(size, K)) (the slots past
+    // K are never written, so they stay zero) -- against which every record's stale slots are checked
+    bool shard_owner = false;
+    int seq_size = 0;
+    std::vector<float> seq_nrm;
     ~bshot_odom() {
         if (metrics) std::fclose(metrics);
     }
@@ -90,6 +97,13 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
               std::shared_ptr<const myslam::LidarOdometry::Extracted> ex = nullptr) {
     const auto t0 = std::chrono::steady_clock::now();
     myslam::LidarOdometry& lo = *o->lo;
+    const int K = lo.params().num_keypoints;
+    if (o->shard_owner && !ex) {
+        // a sweep the chain owner extracts itself (a record was refused): its describe must start from
+        // the sequence's normals state, not from whatever this context last described
+        if (bsh::ctx_normals_write(lo.context(), o->seq_size, (int)(o->seq_nrm.size() / 4), o->seq_nrm.data()) < 0)
+            throw std::runtime_error(std::string("normals state: ") + bshot_last_error(lo.context()));
+    }
     myslam::Frame::Ptr f = myslam::Frame::createFrame();
     if (xyz) {
         auto pc = std::make_shared<std::vector<myslam::Vector3f>>(n);
@@ -102,6 +116,13 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     else lo.setSrcFrameDevice(f, d_xyz, n);
     lo.extractKeypoints();
     lo.computeDescriptors();
+    if (o->shard_owner && !ex) {
+        const int m = std::max(0, std::min(n, K));
+        o->seq_nrm.assign(4 * (size_t)m, 0.f);
+        if (m > 0 && bsh::ctx_normals_read(lo.context(), m, o->seq_nrm.data()) < 0)
+            throw std::runtime_error(std::string("normals state: ") + bshot_last_error(lo.context()));
+        o->seq_size = n;
+    }
     start_lookahead(o);
     lo.featureMatching();
     lo.evaluateEstimation();
@@ -266,9 +287,10 @@ int bshot_odom_gpu_replica_query(bshot_odom* o, int replica, const float pos[3],
 }
 
 // frame-sharded single sequence: record layout (floats): [0] magic, [1] n_points, [2] n_valid,
-// [3] k, [4] n_iss (int bits), [5..7] 0; k x 3 keypoints, k ratios, k x 11 descriptor words (bit
-// patterns), n_iss x 3 ISS points
-static constexpr int kRecMagic = 0x42534852;  // "RHSB"
+// [3] k, [4] n_iss, [5] K (num_keypoints), [6] m = min(n_points, K) (int bits), [7] 0; k x 3
+// keypoints, k ratios, k x 11 descriptor words (bit patterns), n_iss x 3 ISS points, m x 4 normals
+// slots (the persistent array as the sweep's SHOT read it: [0, k) its own, [k, m) stale)
+static constexpr int kRecMagic = 0x32534852;  // "RHS2"
 static constexpr int kRecHdr = 8;
 
 int bshot_odom_extract_device(bshot_odom* o, const float* d_xyz, int n, float* rec, int cap) {
@@ -280,12 +302,13 @@ int bshot_odom_extract_device(bshot_odom* o, const float* d_xyz, int n, float* r
         lo.setSrcFrameDevice(f, d_xyz, n);
         lo.extractKeypoints();
         lo.computeDescriptors();
+        // the normals slots are read before the next sweep's lookahead describe can touch them
+        const myslam::LidarOdometry::Extracted e = lo.extractedWithNormals();
         start_lookahead(o);
-        const myslam::LidarOdometry::Extracted e = lo.extracted();
-        const int k = (int)e.kps.size(), ni = (int)e.iss.size();
-        len = kRecHdr + 15 * k + 3 * ni;
+        const int k = (int)e.kps.size(), ni = (int)e.iss.size(), m = (int)(e.normals.size() / 4);
+        len = kRecHdr + 15 * k + 3 * ni + 4 * m;
         if (len > cap) return;
-        const int hdr[kRecHdr] = {kRecMagic, e.n_points, e.n_valid, k, ni, 0, 0, 0};
+        const int hdr[kRecHdr] = {kRecMagic, e.n_points, e.n_valid, k, ni, lo.params().num_keypoints, m, 0};
         std::memcpy(rec, hdr, sizeof(hdr));
         float* p = rec + kRecHdr;
         if (k) std::memcpy(p, e.kps[0].v, sizeof(float) * 3 * k);
@@ -295,6 +318,8 @@ int bshot_odom_extract_device(bshot_odom* o, const float* d_xyz, int n, float* r
         if (k) std::memcpy(p, e.words.data(), sizeof(uint32_t) * 11 * k);
         p += 11 * k;
         if (ni) std::memcpy(p, e.iss[0].v, sizeof(float) * 3 * ni);
+        p += 3 * ni;
+        if (m) std::memcpy(p, e.normals.data(), sizeof(float) * 4 * m);
     });
     if (rc < 0) return rc;
     return len > cap ? -len : len;
@@ -304,13 +329,49 @@ int bshot_odom_process_record(bshot_odom* o, const float* rec, int len, bshot_fr
     if (!o || !rec || len < kRecHdr) return BSHOT_EINVAL;
     int hdr[kRecHdr];
     std::memcpy(hdr, rec, sizeof(hdr));
-    const int k = hdr[3], ni = hdr[4];
-    if (hdr[0] != kRecMagic || k < 0 || ni < 0 || len != kRecHdr + 15 * k + 3 * ni) {
+    const int n = hdr[1], k = hdr[3], ni = hdr[4], K = hdr[5], m = hdr[6];
+    const int myK = o->lo->params().num_keypoints;
+    if (hdr[0] != kRecMagic || n < 0 || k < 0 || ni < 0 || k > n || m != std::min(n, std::max(K, 0)) ||
+        (long long)len != kRecHdr + 15ll * k + 3ll * ni + 4ll * m) {
         o->err = "bshot_odom_process_record: not an extraction record";
         return BSHOT_EINVAL;
     }
+    if (K != myK || k > K) {
+        o->err = "bshot_odom_process_record: record extracted with K = " + std::to_string(K) + ", this context has K = " +
+                 std::to_string(myK);
+        return BSHOT_EINVAL;
+    }
+    const float* nrm = rec + kRecHdr + 15 * (size_t)k + 3 * (size_t)ni;
+    if (!o->shard_owner) {
+        // the sequence's normals state so far: this context's own (empty for a fresh context)
+        const int rc0 = guard(o, [&]() {
+            o->lo->drainLookahead();
+            bshot_ctx* c = o->lo->context();
+            const int m0 = std::min(c->normals_size, myK);
+            o->seq_nrm.assign(4 * (size_t)std::max(m0, 0), 0.f);
+            if (m0 > 0 && bsh::ctx_normals_read(c, m0, o->seq_nrm.data()) < 0)
+                throw std::runtime_error(std::string("normals state: ") + bshot_last_error(c));
+            o->seq_size = c->normals_size;
+        });
+        if (rc0 < 0) return rc0;
+        o->shard_owner = true;
+    }
+    // the sequence's state after resize(n) (include/bshot_bits.h:59: slots [0, min(size, n)) kept, new
+    // ones zero), against which the record's stale slots [k, m) must match bit for bit: the record's
+    // SHOT read them, the sequential reference would have read these
+    std::vector<float> next(4 * (size_t)m, 0.f);
+    const int keep = std::min(std::min(o->seq_size, n), (int)(o->seq_nrm.size() / 4));
+    if (std::min(keep, m) > 0) std::memcpy(next.data(), o->seq_nrm.data(), sizeof(float) * 4 * std::min(keep, m));
+    if (m > k && std::memcmp(next.data() + 4 * (size_t)k, nrm + 4 * (size_t)k, sizeof(float) * 4 * (m - k)) != 0) {
+        o->err = "bshot_odom_process_record: the record was described over stale normals slots [" + std::to_string(k) +
+                 ", " + std::to_string(m) + ") that differ from this sequence's (a sweep with fewer than K keypoints "
+                 "after a sweep another context extracted); extract this sweep on the chain owner instead "
+                 "(bshot_odom_process_device)";
+        return BSHOT_ESTALE;
+    }
+    if (k) std::memcpy(next.data(), nrm, sizeof(float) * 4 * k);
     auto e = std::make_shared<myslam::LidarOdometry::Extracted>();
-    e->n_points = hdr[1];
+    e->n_points = n;
     e->n_valid = hdr[2];
     const float* p = rec + kRecHdr;
     e->kps.resize(k);
@@ -323,7 +384,12 @@ int bshot_odom_process_record(bshot_odom* o, const float* rec, int len, bshot_fr
     p += 11 * k;
     e->iss.resize(ni);
     if (ni) std::memcpy(&e->iss[0][0], p, sizeof(float) * 3 * ni);
-    return guard(o, [&]() { run_frame(o, nullptr, nullptr, e->n_points, st, e); });
+    const int rc = guard(o, [&]() { run_frame(o, nullptr, nullptr, e->n_points, st, e); });
+    if (rc == BSHOT_OK) {
+        o->seq_nrm.swap(next);
+        o->seq_size = n;
+    }
+    return rc;
 }
 
 int bshot_odom_drain(bshot_odom* o) {

@@ -80,9 +80,17 @@ class LidarOdometry {
         PointCloudXYZ kps, iss;
         std::vector<float> ratios;
         std::vector<uint32_t> words;  // 11 per keypoint (bits_to_words)
+        // the persistent normals array (include/bshot_bits.h:58-87) as this sweep's SHOT read it:
+        // slots [0, min(n_points, K)) x (nx, ny, nz, curvature). Slots [0, k) are the sweep's own;
+        // [k, min(n_points, K)) are stale ones left by earlier describes of the extracting context,
+        // which the chain owner checks against the sequence's own (bshot_odom_process_record).
+        // Filled by extractedWithNormals(); empty from extracted().
+        std::vector<float> normals;
     };
     // the current sweep's extraction half (after computeDescriptors)
     Extracted extracted() const;
+    // the same plus the persistent normals slots [0, min(n_points, K)) (one device read, synchronous)
+    Extracted extractedWithNormals();
     // adopt another context's extraction of this sweep: the next extractKeypoints/computeDescriptors
     // take it as computed here (matching, RANSAC, ICP and the map update then run as usual)
     void setSrcFrameExtracted(Frame::Ptr src, std::shared_ptr<const Extracted> ex);
@@ -118,8 +126,11 @@ class LidarOdometry {
     bshot_ctx* ctx_ = nullptr;
     Frame::Ptr ref_, src_;
     PointCloudXYZ src_pc_, ref_pc_;  // src_pcl_ / ref_pcl_ (src/lidar_odometry.cpp:29-41)
-    const float* src_dev_ = nullptr;
+    const float* src_dev_ = nullptr;  // device cloud of the current sweep (null for host or external frames)
+    const void* src_ext_ = nullptr;   // identity of an external frame's record (setSrcFrameExtracted); never read
     int src_n_ = 0;
+    // identity the adopted lookahead / record must match for the current sweep
+    const void* srcId() const { return src_ext_ ? src_ext_ : static_cast<const void*>(src_dev_); }
     STATUS status_;
     std::vector<float> seg_ratios_;
     Map globalMap_;

@@ -25,6 +25,7 @@ extern "C" {
 #define BSHOT_EHIP (-2)
 #define BSHOT_ECAP (-3)
 #define BSHOT_ESTATE (-4)
+#define BSHOT_ESTALE (-5) /* frame-sharded record described over other normals than the sequence's */
 
 typedef struct bshot_ctx bshot_ctx;
 
@@ -242,13 +243,20 @@ int bshot_odom_gpu_replica_query(bshot_odom* o, int replica, const float pos[3],
 /* frame-sharded single sequence (extension; BASELINE config 3 over several GPUs):
  * a sweep's extraction half (A0-A7 + ISS: extractKeypoints + computeDescriptors,
  * src/lidar_odometry.cpp:51-184) on one context, packed as a record of floats -- [0] magic, [1]
- * n_points, [2] n_valid, [3] k, [4] n_iss (int bits), [5..7] 0, then k x 3 keypoints, k ratios, k x 11
- * descriptor words (bit patterns), n_iss x 3 ISS points -- and the chain half (A8-A13,
+ * n_points, [2] n_valid, [3] k, [4] n_iss, [5] K, [6] m = min(n_points, K) (int bits), [7] 0, then
+ * k x 3 keypoints, k ratios, k x 11 descriptor words (bit patterns), n_iss x 3 ISS points and m x 4
+ * floats of the persistent normals array as the sweep's SHOT read it -- and the chain half (A8-A13,
  * :186-376) of the sequence on another, in sweep order. The set_next[2]_device lookahead applies to
- * the extracting context. Returns the record length in floats, or -length when cap is too small.
+ * the extracting context. extract returns the record length in floats, or -length when cap is too
+ * small.
  * The reference's persistent normals array (include/bshot_bits.h:58-87) carries state from one
- * describe to the next only through a sweep with fewer keypoints than the one after it; across
- * sweeps with K keypoints each, records from independent contexts equal the sequential ones. */
+ * describe to the next through a sweep with fewer than K keypoints: its SHOT reads slots [k, K) as
+ * the sweeps before it left them. The chain owner keeps the sequence's own array state and checks
+ * each record's stale slots [k, m) against it bit for bit; a record that read other values (its
+ * extracting context last described a different sweep) is refused with BSHOT_ESTALE and changes
+ * nothing -- the caller then runs that sweep on the owner with bshot_odom_process[_device], which
+ * starts from the sequence's state, so the chain stays identical to the sequential run. Across
+ * sweeps with K keypoints each no record is ever refused. */
 int bshot_odom_extract_device(bshot_odom* o, const float* d_xyz, int n, float* rec, int cap);
 int bshot_odom_process_record(bshot_odom* o, const float* rec, int len, bshot_frame_stats* st);
 /* wait for the lookahead work started by the last process call (the prefetched sweep's describe on

@@ -117,6 +117,36 @@ def test_gmap_crafted_inserts_vs_host_map():
         od.close()
 
 
+def test_gmap_block_crossing_small_image_limit():
+    """a block whose members plus the batch fit the small LDS image before the insert
+    (<= 1024) belongs to the small-image launch alone, even when the insert takes it past 1024; a
+    block already past 1024 goes to the full-image launch. Both against the host Map."""
+    rng = np.random.default_rng(11)
+    od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=64))
+    hm = bshot_py.KeypointMap()
+    try:
+        g = np.stack(np.meshgrid(np.arange(-4800, 4800, 300), np.arange(-4800, 4800, 300), np.arange(-900, 900, 600)),
+                     -1).reshape(-1, 3).astype(np.float32) + [-30000.0, 10000.0, 0.0]
+        g = g[rng.permutation(len(g))]
+        assert len(g) >= 1300
+        r = np.linspace(0.01, 0.99, 1300).astype(np.float32)  # rising: every candidate is admitted
+        parts = [(g[:600], r[:600]), (g[600:1000], r[600:1000]),  # 600 + 400 <= 1024 before the insert
+                 (g[1000:1100], r[1000:1100]),                     # 1000 + 100 > 1024: the full image
+                 (np.concatenate([g[:40], g[1100:1300]]), np.concatenate([r[:40] + 0.5, r[1100:1300]]))]
+        for pts, rat in parts:
+            rec = _rec(pts, rat, rng)
+            od.gpu_replica_insert(0, rec)
+            _host_add(hm, rec)
+            assert od.gpu_replica_size(0) == hm.size()
+            for pos in ([-30000.0, 10000.0, 0.0], [-25000.0, 5000.0, 0.0]):
+                gx, gb = od.gpu_replica_query(0, np.array(pos, np.float32))
+                hx, hb = hm.query(np.array(pos, np.float32))
+                assert np.array_equal(_u(gx), _u(hx)) and np.array_equal(gb, hb)
+        assert hm.size() > 1100
+    finally:
+        od.close()
+
+
 def test_gmap_large_batches_both_sort_paths():
     """A batch's block ids are ordered by a one-workgroup LDS sort up to 4096 keypoints and by the
     rocprim radix sort past that; both must leave the replica equal to the host Map (sizes, and the

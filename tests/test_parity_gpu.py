@@ -5,6 +5,8 @@ expected bit-exact because device and oracle share one documented operation orde
 (-ffp-contract=off, IEEE +-*/ sqrt, identical transcendental algorithms); the stated tolerance
 below (SHOT |d| <= 1e-5, normals <= 1e-5) is the contract floor, bit-equality is asserted where
 the convention guarantees it."""
+import os
+
 import numpy as np
 import pytest
 
@@ -419,6 +421,15 @@ def test_config5_dense_large_radius_describe():
     finally:
         c.close()
     assert len(pc) > 200000 and len(kps) == 4096
+    # the CV SR of the whole 245k-point sweep against the oracle's (the keypoints
+    # above come from the GPU's own SR), on all host cores
+    orc.set_point_threads(min(16, os.cpu_count() or 1))
+    try:
+        ridx, rrat = orc.seg_ratio(pc)
+    finally:
+        orc.set_point_threads(1)
+    np.testing.assert_array_equal(idx, ridx)
+    np.testing.assert_array_equal(rat.view(np.uint32), rrat.view(np.uint32))
     rn = orc.normals(pc, kps)
     rs, rrf = orc.shot(pc, rn, kps, radius=5000.0)
     np.testing.assert_array_equal(shot.view(np.uint32), rs.view(np.uint32))
