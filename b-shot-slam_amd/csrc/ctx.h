@@ -288,6 +288,9 @@ struct bshot_ctx {
 
 namespace bsh {
 // internal entry points shared by the C ABI and the odometry driver
+// A2 from a sweep's SR ratio array (NaN = skipped): the std::sort tail of the valid (index, ratio)
+// pairs (host/topk.cpp)
+int topk_from_ratios(const float* ratio, int n, int k, int32_t* kp_idx, float* kp_ratio, int* k_out, int* nv_out);
 int ctx_make_side_stream(bshot_ctx* c);
 int ctx_set_cloud_dev(bshot_ctx* c, const float* d_xyz, int n);  // adopts a matching prefetch
 int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n);   // grids + SR + ISS on the side stream

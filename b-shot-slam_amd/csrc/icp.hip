@@ -252,7 +252,15 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
 // iterations from the current positions (ctx_icp).
 #define ICPH_THREADS 64
 #define ICP_WAIT_TICKS 100000000ll  // 1 s at the 100 MHz wall clock: a launch that cannot finish exits
-__global__ void __launch_bounds__(ICPH_THREADS) k_icp_iterations(const float* __restrict__ src0, int ns, int j0,
+#ifndef ICPH_WPE
+#define ICPH_WPE 0
+#endif
+#if ICPH_WPE > 0
+#define ICPH_ATTR __attribute__((amdgpu_waves_per_eu(ICPH_WPE)))
+#else
+#define ICPH_ATTR
+#endif
+__global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const float* __restrict__ src0, int ns, int j0,
                                                                  const float4* lst, const float* lsd,
                                                                  const int* __restrict__ lcnt,
                                                                  const float4* __restrict__ lcen, int cap, IcpGrids G,

@@ -60,7 +60,9 @@ struct KnnLds {
 };
 // the finishing math's 3 coordinate arrays sit FL_STRIDE floats apart: 512 + 4, so lanes reading
 // x[r], y[r], z[r] together hit 3 different LDS banks (a 512 stride put all three in one bank)
+#ifndef FL_STRIDE
 #define FL_STRIDE 516
+#endif
 static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 2 * (KNN_NB + 4) >= 3 * FL_STRIDE * 4,
               "list + hist + boff must hold 3 x FL_STRIDE floats");
 static_assert(KNN_CAP >= KNN_PRE, "the prefix must fit the list (and the bitonic sort's 512 keys)");

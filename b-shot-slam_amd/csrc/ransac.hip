@@ -26,7 +26,15 @@ namespace bsk {
 // cs/ct: correspondence source/target points (3 floats each, correspondence order); hyp: 3
 // correspondence positions per hypothesis
 #define RS_HYP 64
-__global__ void __launch_bounds__(64 * RS_WAVES) k_ransac_score(const float* __restrict__ cs,
+#ifndef RS_WPE
+#define RS_WPE 0
+#endif
+#if RS_WPE > 0
+#define RS_ATTR __attribute__((amdgpu_waves_per_eu(RS_WPE)))
+#else
+#define RS_ATTR
+#endif
+__global__ void __launch_bounds__(64 * RS_WAVES) RS_ATTR k_ransac_score(const float* __restrict__ cs,
                                                                 const float* __restrict__ ct, int nidx,
                                                                 const int* __restrict__ hyp, int nhyp, double thr2,
                                                                 int* __restrict__ cnt) {

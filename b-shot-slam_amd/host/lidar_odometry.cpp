@@ -37,21 +37,10 @@ struct LidarOdometry::TopkAhead {
 // SR ratios of a cloud (pinned host copy) -> valid (index, ratio) pairs -> top-K (libstdc++ order)
 static int select_from_ratios(const float* h_ratio, int n, int k_want, std::vector<int32_t>& kidx,
                               std::vector<float>& kr, int* nv_out) {
-    std::vector<int32_t> idx(n > 0 ? n : 1);
-    std::vector<float> ratio(n > 0 ? n : 1);
-    int nv = 0;
-    for (int i = 0; i < n; ++i) {
-        const float r = h_ratio[i];
-        if (r != r) continue;
-        idx[nv] = i;
-        ratio[nv] = r;
-        ++nv;
-    }
-    *nv_out = nv;
     kidx.resize(k_want > 0 ? k_want : 1);
     kr.resize(kidx.size());
     int k = 0;
-    const int rc = bshot_select_topk(idx.data(), ratio.data(), nv, k_want, kidx.data(), kr.data(), &k);
+    const int rc = bsh::topk_from_ratios(h_ratio, n, k_want, kidx.data(), kr.data(), &k, nv_out);
     if (rc < 0) return rc;
     kidx.resize(k);
     kr.resize(k);
@@ -266,17 +255,19 @@ void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
         const float* h_ratio = c->pf2.h_ratio.p;
         const int* h_err = c->pf2.h_err.p;
         const int dev = c->device;
-        p->th = std::thread([p, ev, h_ratio, h_err, dev, kwant, n]() {
+        p->th = std::thread([p, c, ev, h_ratio, h_err, dev, kwant, n]() {
             (void)hipSetDevice(dev);
             if (hipEventSynchronize(ev) != hipSuccess) {
                 p->err = "lookahead sr";
                 return;
             }
+            c->hmark("T_sr_ready");
             if (h_err[0]) {
                 p->err = "seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)";
                 return;
             }
             if (select_from_ratios(h_ratio, n, kwant, p->kidx, p->kr, &p->nv) < 0) p->err = "topk";
+            c->hmark("T_done");
         });
         return tk;
     };

@@ -27,6 +27,40 @@ def test_select_topk_matches_std_sort(n, k, levels):
     assert np.array_equal(gi, ei) and np.array_equal(gr, er)
 
 
+def _pattern(kind, n, rng):
+    i = np.arange(n)
+    x = rng.random(n)
+    if kind == "equal":
+        return np.ones(n, np.float32)
+    if kind == "two":
+        return np.where(x < 0.5, 1.0, 0.5).astype(np.float32)
+    if kind == "sorted":
+        return i.astype(np.float32)
+    if kind == "reversed":
+        return (n - i).astype(np.float32)
+    if kind == "saw":
+        return (i % 7).astype(np.float32)
+    if kind == "organ":
+        return np.minimum(i, n - i).astype(np.float32)
+    # CV-like: 1 - min(a, b) / max(a, b) of small counts, many exact 1.0
+    a, b = rng.integers(0, 150, n), rng.integers(1, 150, n)
+    return (1.0 - np.minimum(a, b) / np.maximum(a, b)).astype(np.float32)
+
+
+@pytest.mark.parametrize("kind", ["equal", "two", "sorted", "reversed", "saw", "organ", "cv"])
+@pytest.mark.parametrize("n,k", [(17, 600), (40, 30), (600, 600), (601, 600), (5000, 2048), (131000, 2048)])
+def test_select_topk_patterns_match_std_sort(kind, n, k):
+    """The block partition (host/topk.cpp) pairs left and right stoppers as libstdc++'s
+    __unguarded_partition does; adversarial value patterns and sizes around k and 16 (the final
+    insertion pass's guarded head) against std::sort itself."""
+    rng = np.random.default_rng(n * 7 + k)
+    r = _pattern(kind, n, rng)
+    idx = np.arange(n, dtype=np.int32)
+    gi, gr = bshot_py.select_topk(idx, r, k)
+    ei, er = orc.select_topk(idx, r, k)
+    assert np.array_equal(gi, ei) and np.array_equal(gr.view(np.uint32), er.view(np.uint32))
+
+
 # ----------------------------------------------------------------------------- RANSAC
 def _corr_set(seed, n_src=800, n_corr=400, inlier_frac=0.6, noise=30.0):
     rng = np.random.default_rng(seed)
