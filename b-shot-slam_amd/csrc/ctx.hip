@@ -189,7 +189,8 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
 
 // SR of cloud s on stream st; ratios and error word land in pinned host memory at s.ev_sr
 static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
-    if (c->prm.seg_max_nn < 1 || c->prm.seg_max_nn > 512) return c->fail("seg_max_nn must be in [1, 512]", BSHOT_EINVAL);
+    if (c->prm.seg_max_nn < 1 || c->prm.seg_max_nn > knn_max_nn())
+        return c->fail("seg_max_nn must be in [1, " + std::to_string(knn_max_nn()) + "]", BSHOT_EINVAL);
     const int n = s.n;
     HIPCHK(s.ratio.ensure(n > 0 ? n : 1), "alloc ratio");
     HIPCHK(s.h_ratio.ensure(n > 0 ? n : 1), "alloc pinned ratio");
@@ -432,8 +433,10 @@ static int rank_wg_for(const bshot_ctx* c, int k, long long total) {
 }
 
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
-    if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > 512)
-        return c->fail("normal_max_nn must be in [1, 512]", BSHOT_EINVAL);
+    // the SHOT-segment normals take up to 512 neighbours, the kNN engine's (k_normals) up to knn_max_nn()
+    const int nmax = c->opt_normals_seg && c->prm.normal_radius == c->prm.shot_radius ? 512 : knn_max_nn();
+    if (c->prm.normal_max_nn < 1 || c->prm.normal_max_nn > nmax)
+        return c->fail("normal_max_nn must be in [1, " + std::to_string(nmax) + "]", BSHOT_EINVAL);
     const int n = S.n;
     // persistent normals array: resize(n) keeps [0, min) and value-initialises new slots
     HIPCHK(c->normals.ensure(std::max(n, std::max(k, 1))), "alloc normals");

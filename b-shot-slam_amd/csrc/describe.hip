@@ -388,6 +388,10 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
                                   hipStream_t s) {
     if (k <= 0) return hipSuccess;
     if (k > DP_MAXK) return hipErrorInvalidValue;
+#ifdef DIAG_COUNT_TWICE
+    // diagnostic builds only: the count kernel twice (it overwrites its outputs) -- its marginal cost
+    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
+#endif
     bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
     bsk::k_desc_plan<<<1, 1024, 0, s>>>(counts, k, seg_cap, chunk_cap, offs, cb, perm, err);
     return hipGetLastError();

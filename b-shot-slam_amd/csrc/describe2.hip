@@ -862,6 +862,12 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
         return hipGetLastError();
     }
     // HF_NW waves per workgroup: 1 applies, HF_NW - 1 produce records
+#ifdef DIAG_HF_TWICE
+    // diagnostic builds only: the histogram kernel twice (idempotent) -- its marginal cost
+    if (A.hf_pack)
+        bsk::k_hist_fused<HF_NW, HF_PACK><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
+                                                               A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
+#endif
     if (A.hf_pack)
         bsk::k_hist_fused<HF_NW, HF_PACK><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
                                                                A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);

@@ -20,18 +20,26 @@ namespace bsk {
 #define CAND_GROUP 4
 #endif
 
+// marks are 16-bit: (epoch << 6) | lane with a 10-bit epoch in 1 .. 1023; 0 is never a tag, so the
+// marks are cleared to 0 when the epoch wraps (every 1023 candidate groups)
+#define CAND_EPOCHS 1024
 struct CandLds {
-    int mark[64 * CAND_GROUP];
+    unsigned short mark[64 * CAND_GROUP];
     int epoch;
     int pad_[3];
 };
 
-// once per wave before the first for_candidates on this CandLds
-__device__ __forceinline__ void cand_init(CandLds* cs) {
+__device__ __forceinline__ void cand_clear_marks(CandLds* cs) {
     const int lane = lane_id();
 #pragma unroll
-    for (int j = 0; j < CAND_GROUP; ++j) cs->mark[lane + 64 * j] = -1;
-    if (lane == 0) cs->epoch = 0;
+    for (int j = 0; j < CAND_GROUP; ++j) cs->mark[lane + 64 * j] = 0;
+    __builtin_amdgcn_wave_barrier();
+}
+
+// once per wave before the first for_candidates on this CandLds
+__device__ __forceinline__ void cand_init(CandLds* cs) {
+    cand_clear_marks(cs);
+    if (lane_id() == 0) cs->epoch = 0;
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -54,14 +62,17 @@ __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs
             const unsigned long long started = __ballot(cnt > 0 && off <= t0);
             carry = 63 - __clzll((long long)started);
         }
-        ++epoch;
+        if (++epoch == CAND_EPOCHS) {
+            cand_clear_marks(cs);  // wave-uniform, once per 1023 groups
+            epoch = 1;
+        }
         const int tag = epoch << 6;
-        if (cnt > 0 && off >= t0 && off < t0 + 64 * GROUP) cs->mark[off - t0] = tag | lane;
+        if (cnt > 0 && off >= t0 && off < t0 + 64 * GROUP) cs->mark[off - t0] = (unsigned short)(tag | lane);
         __builtin_amdgcn_wave_barrier();
         int owner[GROUP];
 #pragma unroll
         for (int j = 0; j < GROUP; ++j) {
-            const int v = cs->mark[64 * j + lane];
+            const int v = (int)cs->mark[64 * j + lane];
             owner[j] = (v & ~63) == tag ? (v & 63) : -1;
         }
 #pragma unroll

@@ -15,6 +15,8 @@ hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s);
 
 // g4: the radius-ladder grids (cells r/16, r/8, r/4, r/2 for ladder modes 1, 2; r/8, r/8, r/2, r/2
 // for mode 0), see ladder() in knn.hip
+// largest max_nn the kNN engine's finishing arrays hold (csrc/knn.hip FL_STRIDE)
+int knn_max_nn();
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
                             unsigned long long* kst = nullptr, int max_blocks = 8192, int xcd_chunk = 0);

@@ -23,16 +23,17 @@
 namespace bsk {
 
 #ifndef KNN_NB
-#define KNN_NB 192
+#define KNN_NB 128
 #endif
 // k_seg_ratio's candidate streaming is bound by dependent L2 round trips, so waves per CU set its
-// speed (3 -> 4 waves per SIMD: 1.05 -> 0.86 ms, profiles/ab_sr_stream.txt). Per wave: the key
-// list (KNN_CAP keys), hist, offsets (u16) and candidate marks = 7.8 KB, so 20 waves fit the
-// CU's 160 KB LDS, matched by <= 96 VGPRs (waves_per_eu 5). The list holds every in-radius key of
-// the deciding ladder step when they fit; the counting sort of the selected prefix (<= KNN_PRE keys)
-// runs in place through registers.
+// speed (3 -> 4 waves per SIMD: 1.05 -> 0.86 ms, profiles/ab_sr_stream.txt; 5 -> 6: 0.621 -> 0.601
+// ms standalone, profiles/r05_ab_sr_w6.txt). Per wave: the key list (KNN_CAP keys), hist, offsets
+// (u16) and the 16-bit candidate marks = 6.3 KB, so 24 waves fit the CU's 160 KB LDS, matched by
+// <= 80 VGPRs (waves_per_eu 6). The list holds every in-radius key of the deciding ladder step when
+// they fit (a 640-key list sends 8 % of the queries down the streaming path, 704 keys 6 %); the
+// counting sort of the selected prefix (<= KNN_PRE keys) runs in place through registers.
 #ifndef KNN_CAP
-#define KNN_CAP 704
+#define KNN_CAP 640
 #endif
 #define KNN_PRE 512  // largest prefix the counting sort handles (8 keys per lane)
 #ifndef KNN_WAVES
@@ -42,7 +43,7 @@ namespace bsk {
 #define SR_DIAG_NOFIN 0  // diagnostic: 1 = skip the ratio computation (timing of the selection alone)
 #endif
 #ifndef SR_WPE
-#define SR_WPE 5  // VGPRs <= 96: 5 waves per SIMD
+#define SR_WPE 6  // VGPRs <= 80: 6 waves per SIMD
 #endif
 #if SR_WPE > 0
 #define SR_ATTR __attribute__((amdgpu_waves_per_eu(SR_WPE)))
@@ -51,17 +52,18 @@ namespace bsk {
 #endif
 
 // list, hist and boff are contiguous: after the selection they double as the rank-order float
-// arrays of the finishing math (3 x 512 coordinates; the CVS terms overwrite the x array)
+// arrays of the finishing math (3 x FL_STRIDE coordinates, so max_nn <= FL_STRIDE, host-checked; the
+// CVS terms overwrite the x array)
 struct KnnLds {
     unsigned long long list[KNN_CAP];  // in-radius keys of the last ladder step; then the sorted result
     unsigned int hist[KNN_NB];
     unsigned short boff[KNN_NB + 4];   // counting-sort bucket starts (<= KNN_PRE)
     CandLds cand;
 };
-// the finishing math's 3 coordinate arrays sit FL_STRIDE floats apart: 512 + 4, so lanes reading
-// x[r], y[r], z[r] together hit 3 different LDS banks (a 512 stride put all three in one bank)
+// the finishing math's 3 coordinate arrays sit FL_STRIDE floats apart: 480 + 4, so lanes reading
+// x[r], y[r], z[r] together hit 3 different LDS banks (a multiple of 32 put all three in one bank)
 #ifndef FL_STRIDE
-#define FL_STRIDE 516
+#define FL_STRIDE 484
 #endif
 static_assert(sizeof(unsigned long long) * KNN_CAP + 4 * KNN_NB + 2 * (KNN_NB + 4) >= 3 * FL_STRIDE * 4,
               "list + hist + boff must hold 3 x FL_STRIDE floats");
@@ -718,6 +720,8 @@ size_t knn_lds_bytes() { return sizeof(KnnLds) * KNN_WAVES + KNN_LDS_PAD; }
 
 namespace bsh {
 
+int knn_max_nn() { return FL_STRIDE; }
+
 // g4[0..3]: grids of cell r/16, r/8, r/4, r/2 when fine_ladder, else {r/8, r/8, r/2, r/2}
 // mode 0: grids r/8, r/8, r/2, r/2, radii r 2^-k (4 steps); 1: nested grids r/16 .. r/2, radii
 // r 2^(-k/2) from r/8 (7 steps); 2: as 1 with two more steps r/16, r/(8 sqrt 2) in front (9 steps),
@@ -754,6 +758,11 @@ hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const flo
         const int rounds = (blocks + 8 * zc - 1) / (8 * zc);
         blocks = rounds * 8 * zc;  // whole rounds of 8 chunks; the workgroups past n exit at once
     }
+#ifdef DIAG_SR_TWICE
+    // diagnostic builds only: SR twice (idempotent) -- its marginal cost
+    bsk::k_seg_ratio<false><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
+                                                                hint, ratio, err, nullptr, zc);
+#endif
     if (kst)
         bsk::k_seg_ratio<true><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
                                                                    hint, ratio, err, kst, zc);

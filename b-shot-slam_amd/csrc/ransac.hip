@@ -26,8 +26,11 @@ namespace bsk {
 // cs/ct: correspondence source/target points (3 floats each, correspondence order); hyp: 3
 // correspondence positions per hypothesis
 #define RS_HYP 64
+// <= 72 VGPRs (the double umeyama's registers spill): a workgroup then fits beside the SR launch's
+// 6 waves of 80 VGPRs per SIMD as soon as one of them retires, instead of waiting for two
+// (profiles/r05_ab_sr_w6.txt: the RANSAC phase 0.49 -> 0.19 ms under the 6-wave SR)
 #ifndef RS_WPE
-#define RS_WPE 0
+#define RS_WPE 7
 #endif
 #if RS_WPE > 0
 #define RS_ATTR __attribute__((amdgpu_waves_per_eu(RS_WPE)))
