@@ -144,6 +144,71 @@ BM_HD double acos_(double x) {
     return 2.0 * (df + w);
 }
 
+// Select forms of atan_ / atan2_ / acos_ for a wavefront whose lanes take different fdlibm ranges:
+// every range's operands are formed by selects and ONE division (one rational polynomial) serves all
+// lanes, where the branchy forms run every taken range's division and polynomial in turn. Each lane
+// evaluates exactly the expression its branch evaluates (same operands, same operation order), so
+// the results are bit-identical to atan_ / atan2_ / acos_ for the arguments they are used with:
+// atan_sel and atan2_sel for finite, not-both-zero (y, x), acos_sel for x in [-1, 1] (PCL's SHOT
+// clamps the inclination cosine; csrc/describe2.hip shot_records_of).
+BM_HD double atan_sel(double x) {
+    const bool neg = x < 0.0;
+    const double ax = neg ? -x : x;
+    const int id = ax < 0.4375 ? -1 : ax < 0.6875 ? 0 : ax < 1.1875 ? 1 : ax < 2.4375 ? 2 : 3;
+    // id -1: ax / 1.0 == ax exactly
+    const double num = id < 0 ? ax : id == 0 ? 2.0 * ax - 1.0 : id == 1 ? ax - 1.0 : id == 2 ? ax - 1.5 : -1.0;
+    const double den = id < 0 ? 1.0 : id == 0 ? 2.0 + ax : id == 1 ? ax + 1.0 : id == 2 ? 1.0 + 1.5 * ax : ax;
+    const double t = num / den;
+    const double z = t * t;
+    const double w = z * z;
+    const double s1 = z * (3.33333333333329318027e-01 +
+                      w * (1.42857142725034663711e-01 +
+                      w * (9.09088713343650656196e-02 +
+                      w * (6.66107313738753120669e-02 +
+                      w * (4.97687799461593236017e-02 +
+                      w * 1.62858201153657823623e-02)))));
+    const double s2 = w * (-1.99999999998764832476e-01 +
+                      w * (-1.11111104054623557880e-01 +
+                      w * (-7.69187620504482999495e-02 +
+                      w * (-5.83357013379057348645e-02 +
+                      w * -3.65315727442169155270e-02))));
+    const double hi = id == 0 ? 4.63647609000806093515e-01 : id == 1 ? 7.85398163397448278999e-01
+                    : id == 2 ? 9.82793723247329054082e-01 : 1.57079632679489655800e+00;
+    const double lo = id == 0 ? 2.26987774529616870924e-17 : id == 1 ? 3.06161699786838301793e-17
+                    : id == 2 ? 1.39033110312309984516e-17 : 6.12323399573676603587e-17;
+    double r = id < 0 ? t - t * (s1 + s2) : hi - ((t * (s1 + s2) - lo) - t);
+    if (id < 0 && ax < 1.862645149230957e-09) r = ax;
+    if (ax >= 3.6893488147419103e+19) r = 1.57079632679489655800e+00 + 6.12323399573676603587e-17;
+    return neg ? -r : r;
+}
+
+BM_HD double atan2_sel(double y, double x) {
+    const double pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
+    const double pio2 = 1.57079632679489655800e+00;
+    const double z = atan_sel(dabs(y / x));
+    double r = x > 0.0 ? z : pi - (z - pi_lo);
+    r = y < 0 ? -r : r;
+    if (x == 0.0) r = y < 0.0 ? -pio2 : pio2;
+    if (y == 0.0) r = __builtin_signbit(x) ? (__builtin_signbit(y) ? -pi : pi) : y;
+    return r;
+}
+
+BM_HD double acos_sel(double x) {
+    const double pi = 3.14159265358979311600e+00;
+    const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17;
+    const double ax = dabs(x);
+    const bool small = ax < 0.5, neg = x < 0.0;
+    const double z = small ? x * x : neg ? (1.0 + x) * 0.5 : (1.0 - x) * 0.5;
+    const double R = acos_R(z);
+    const double s = dsqrt(z);
+    const double df = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, s) & 0xFFFFFFFF00000000ull);
+    const double c = (z - df * df) / (s + df);
+    double r = small ? pio2_hi - (x - (pio2_lo - x * R)) : neg ? pi - 2.0 * (s + (R * s - pio2_lo)) : 2.0 * (df + (R * s + c));
+    if (ax <= 6.938893903907228e-18) r = pio2_hi + pio2_lo;
+    if (ax >= 1.0) r = ax == 1.0 ? (x > 0.0 ? 0.0 : pi + 2.0 * pio2_lo) : __builtin_nan("");
+    return r;
+}
+
 BM_HD double cos_s(double x) {
     const double z = x * x;
     double r = 1.0 / 620448401733239439360000.0;

@@ -373,40 +373,44 @@ __device__ __forceinline__ void shot_records_of(float4 nv, float4 p, float kx, f
                 double w = (1 - fabs(bd));
                 if (bd > 0) { bins[0] = vol + ((step + 1) % nr_bins); vals[0] = (float)bd; }
                 else { bins[0] = vol + ((step - 1 + nr_bins) % nr_bins); vals[0] = -(float)bd; }
-                if (distance > r12) {
-                    const double rd = (distance - r34) / r12;
-                    if (distance > r34) w += 1 - rd;
-                    else { w += 1 + rd; bins[1] = (desc - 2) * (nr_bins + 1) + step; vals[1] = (float)(-rd); }
-                } else {
-                    const double rd = (distance - r14) / r12;
-                    if (distance < r14) w += 1 + rd;
-                    else { w += 1 - rd; bins[1] = (desc + 2) * (nr_bins + 1) + step; vals[1] = (float)rd; }
+                // the radial, inclination and azimuth interpolations in select form: each lane
+                // evaluates exactly its branch's expressions, with one division per interpolation
+                // for the whole wavefront (the lanes of a chunk take every branch)
+                {
+                    const bool outer = distance > r12;
+                    const double rd = (distance - (outer ? r34 : r14)) / r12;
+                    const bool self = outer ? distance > r34 : distance < r14;  // votes only for itself
+                    const bool plus = outer ? !self : self;                      // w += 1 + rd
+                    w += plus ? 1 + rd : 1 - rd;
+                    if (!self) {
+                        bins[1] = (desc + (outer ? -2 : 2)) * (nr_bins + 1) + step;
+                        vals[1] = outer ? (float)(-rd) : (float)rd;
+                    }
                 }
                 double ic = zr / distance;
                 if (ic < -1.0) ic = -1.0;
                 if (ic > 1.0) ic = 1.0;
-                const double incl = bm::acos_(ic);
-                if (incl > PST2_RAD_90 || (fabs(incl - PST2_RAD_90) < 1e-30 && zr <= 0)) {
-                    const double id = (incl - PST2_RAD_135) / PST2_RAD_90;
-                    if (incl > PST2_RAD_135) w += 1 - id;
-                    else { w += 1 + id; bins[2] = (desc + 1) * (nr_bins + 1) + step; vals[2] = -(float)id; }
-                } else {
-                    const double id = (incl - PST2_RAD_45) / PST2_RAD_90;
-                    if (incl < PST2_RAD_45) w += 1 + id;
-                    else { w += 1 - id; bins[2] = (desc - 1) * (nr_bins + 1) + step; vals[2] = (float)id; }
+                const double incl = bm::acos_sel(ic);
+                {
+                    const bool lower = incl > PST2_RAD_90 || (fabs(incl - PST2_RAD_90) < 1e-30 && zr <= 0);
+                    const double id = (incl - (lower ? PST2_RAD_135 : PST2_RAD_45)) / PST2_RAD_90;
+                    const bool self = lower ? incl > PST2_RAD_135 : incl < PST2_RAD_45;
+                    const bool plus = lower ? !self : self;  // w += 1 + id
+                    w += plus ? 1 + id : 1 - id;
+                    if (!self) {
+                        bins[2] = (desc + (lower ? 1 : -1)) * (nr_bins + 1) + step;
+                        vals[2] = lower ? -(float)id : (float)id;
+                    }
                 }
                 if (yr != 0.0 || xr != 0.0) {
-                    const double az = bm::atan2_(yr, xr);
+                    const double az = bm::atan2_sel(yr, xr);
                     const int sel = desc >> 2;
                     double ad = (az - (-PST2_RAD_PI_7_8 + PST2_RAD_45 * sel)) / PST2_RAD_45;
                     ad = fmax(-0.5, fmin(ad, 0.5));
-                    if (ad > 0) {
-                        w += 1 - ad;
-                        bins[3] = ((desc + 4) % 32) * (nr_bins + 1) + step; vals[3] = (float)ad;
-                    } else {
-                        w += 1 + ad;
-                        bins[3] = ((desc - 4 + 32) % 32) * (nr_bins + 1) + step; vals[3] = -(float)ad;
-                    }
+                    const bool pos = ad > 0;
+                    w += pos ? 1 - ad : 1 + ad;
+                    bins[3] = ((desc + (pos ? 4 : 28)) % 32) * (nr_bins + 1) + step;
+                    vals[3] = pos ? (float)ad : -(float)ad;
                 }
                 bins[4] = vol + step;
                 vals[4] = (float)w;

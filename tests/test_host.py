@@ -219,6 +219,18 @@ def test_map_query_block_scan_order(seed):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
+def test_math_select_forms_match_fdlibm(tmp_path):
+    """The SHOT record producers' select forms of atan/atan2/acos (one division for a whole
+    wavefront, csrc/bshot_math.h) equal the branchy fdlibm forms bit for bit
+    (b-shot-slam_amd/tools/math_sel_check.cpp, 40 M random arguments plus every range boundary)."""
+    import subprocess
+    exe = tmp_path / "msc"
+    src = os.path.join(ROOT, "b-shot-slam_amd", "tools", "math_sel_check.cpp")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src])
+    out = subprocess.run([str(exe), "20"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
 def test_umap_order_restatement_matches_libstdcxx(tmp_path):
     """csrc/umap_order.h (the GPU map's per-block iteration order) against this image's libstdc++
     std::unordered_map<Vector3f, ., MapHasher>: bucket counts and iteration order after every insert
