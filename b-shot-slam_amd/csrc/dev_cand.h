@@ -82,12 +82,17 @@ __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs
             carry = readlane_i(m, 63);
             owner[j] = m;
         }
+        // the owners' run bases first, then all GROUP loads unconditionally (a lane past the total
+        // reads spts[0] and is masked by the validity flag): a load under a branch made the
+        // compiler wait for each one before issuing the next, serialising GROUP L2 round trips
+        int cb[GROUP];
+#pragma unroll
+        for (int j = 0; j < GROUP; ++j) cb[j] = __builtin_amdgcn_ds_bpermute(owner[j] << 2, cbase);
         float4 p[GROUP];
 #pragma unroll
         for (int j = 0; j < GROUP; ++j) {
-            const int cb = __builtin_amdgcn_ds_bpermute(owner[j] << 2, cbase);
             const int t = t0 + 64 * j + lane;
-            p[j] = t < total ? g.spts[cb + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+            p[j] = g.spts[t < total ? cb[j] + t : 0];
         }
 #pragma unroll
         for (int j = 0; j < GROUP; ++j) {
