@@ -112,25 +112,41 @@ __device__ __forceinline__ void cand_stream_round(const GridView& g, CandLds* cs
 // lim = rs + slack (cand_slack; a conservative cube: never a cell with an in-ball point left out).
 // rnz, rny: 1 / nz, 1 / ny (the cell index splits by float reciprocals: exact for these small
 // integers with the +0.5 bias, and no integer division sequence per lane)
+// lane's cell of round `base` of the query cube: its key, and whether it can hold an in-ball point
+// (in the cube and its box within lim of the query)
+__device__ __forceinline__ bool cand_cell(const GridView& g, int x0, int y0, int z0, int ny, int nz, float rny,
+                                          float rnz, int ncell, int cidx, float qx, float qy, float qz, float lim,
+                                          unsigned long long& key) {
+    key = BS_EMPTY_KEY;
+    if (cidx >= ncell) return false;
+    const int t = (int)(((float)cidx + 0.5f) * rnz), iz = cidx - t * nz;
+    const int ix = (int)(((float)t + 0.5f) * rny), iy = t - ix * ny;
+    const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
+    const float c = g.cell;
+    const float bx0 = (float)cx * c, by0 = (float)cy * c, bz0 = (float)cz * c;
+    float dx = 0.f, dy = 0.f, dz = 0.f;
+    if (qx < bx0) dx = bx0 - qx; else if (qx > bx0 + c) dx = qx - (bx0 + c);
+    if (qy < by0) dy = by0 - qy; else if (qy > by0 + c) dy = qy - (by0 + c);
+    if (qz < bz0) dz = bz0 - qz; else if (qz > bz0 + c) dz = qz - (bz0 + c);
+    if (!(dx * dx + dy * dy + dz * dz <= lim * lim)) return false;
+    key = cell_key(cx, cy, cz);
+    return true;
+}
+
+// lane's cell of round `base` of the query cube: its spts run (cnt = 0 when pruned or empty). The
+// cube and the pruning only decide which cells are visited, never which points count (every
+// candidate is tested d2 < rs^2), so they run in float with a slack that covers float rounding:
+// lim = rs + slack (cand_slack; a conservative cube: never a cell with an in-ball point left out).
+// rnz, rny: 1 / nz, 1 / ny (the cell index splits by float reciprocals: exact for these small
+// integers with the +0.5 bias, and no integer division sequence per lane)
 __device__ __forceinline__ void cand_lookup(const GridView& g, int x0, int y0, int z0, int ny, int nz, float rny,
                                             float rnz, int ncell, int cidx, float qx, float qy, float qz, float lim,
                                             unsigned int& st, unsigned int& cnt) {
     st = 0;
     cnt = 0;
-    if (cidx < ncell) {
-        const int t = (int)(((float)cidx + 0.5f) * rnz), iz = cidx - t * nz;
-        const int ix = (int)(((float)t + 0.5f) * rny), iy = t - ix * ny;
-        const int cx = x0 + ix, cy = y0 + iy, cz = z0 + iz;
-        const float c = g.cell;
-        const float bx0 = (float)cx * c, by0 = (float)cy * c, bz0 = (float)cz * c;
-        float dx = 0.f, dy = 0.f, dz = 0.f;
-        if (qx < bx0) dx = bx0 - qx; else if (qx > bx0 + c) dx = qx - (bx0 + c);
-        if (qy < by0) dy = by0 - qy; else if (qy > by0 + c) dy = qy - (by0 + c);
-        if (qz < bz0) dz = bz0 - qz; else if (qz > bz0 + c) dz = qz - (bz0 + c);
-        if (dx * dx + dy * dy + dz * dz <= lim * lim) {
-            if (!grid_lookup(g, cell_key(cx, cy, cz), st, cnt)) cnt = 0;
-        }
-    }
+    unsigned long long key;
+    if (cand_cell(g, x0, y0, z0, ny, nz, rny, rnz, ncell, cidx, qx, qy, qz, lim, key))
+        if (!grid_lookup(g, key, st, cnt)) cnt = 0;
 }
 
 // the float slack of a query's cube (see cand_lookup): 2^-20 of the query's magnitude (16 ulps of
@@ -158,9 +174,15 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
     int epoch = cs->epoch;
     bool streamed = true;
     if (ncell <= 128) {
-        unsigned int st0, cnt0, st1 = 0, cnt1 = 0;
-        cand_lookup(g, x0, y0, z0, ny, nz, rny, rnz, ncell, lane, qx, qy, qz, lim, st0, cnt0);
-        if (ncell > 64) cand_lookup(g, x0, y0, z0, ny, nz, rny, rnz, ncell, 64 + lane, qx, qy, qz, lim, st1, cnt1);
+        // both rounds' first probes in flight together, then their resolution
+        unsigned int st0 = 0, cnt0 = 0, st1 = 0, cnt1 = 0;
+        unsigned long long k0, k1;
+        const bool w0 = cand_cell(g, x0, y0, z0, ny, nz, rny, rnz, ncell, lane, qx, qy, qz, lim, k0);
+        const bool w1 = cand_cell(g, x0, y0, z0, ny, nz, rny, rnz, ncell, 64 + lane, qx, qy, qz, lim, k1);
+        const uint4 e0 = grid_probe0(g, w0 ? k0 : 0ull);
+        const uint4 e1 = grid_probe0(g, w1 ? k1 : 0ull);
+        if (w0 && !grid_resolve(g, k0, e0, st0, cnt0)) cnt0 = 0;
+        if (w1 && !grid_resolve(g, k1, e1, st1, cnt1)) cnt1 = 0;
         int tot0, tot1 = 0;
         const int off0 = wave_excl_scan((int)cnt0, tot0);
         const int off1 = ncell > 64 ? wave_excl_scan((int)cnt1, tot1) : 0;

@@ -13,7 +13,7 @@
 #define BS_WAVE 64
 #define BS_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
 
-struct CellEntry {
+struct __attribute__((aligned(16))) CellEntry {
     unsigned long long key;
     unsigned int start;
     unsigned int count;
@@ -55,13 +55,44 @@ __device__ __forceinline__ bool grid_lookup(const GridView& g, unsigned long lon
                                             unsigned int& count) {
     unsigned int h = hash_key(key) & g.mask;
     for (unsigned int probe = 0; probe <= g.mask; ++probe) {
-        const unsigned long long k = g.table[h].key;
+        // the whole 16-B entry in one load: key, start and count in one L2 round trip
+        const uint4 e = *reinterpret_cast<const uint4*>(&g.table[h]);
+        const unsigned long long k = ((unsigned long long)e.y << 32) | e.x;
         if (k == key) {
-            start = g.table[h].start;
-            count = g.table[h].count;
+            start = e.z;
+            count = e.w;
             return true;
         }
         if (k == BS_EMPTY_KEY) return false;
+        h = (h + 1) & g.mask;
+    }
+    return false;
+}
+
+// grid_lookup split in two, so several lookups' first probes can be in flight together: the first
+// probe's entry (issued by the caller), then its resolution (further probes only on a collision)
+__device__ __forceinline__ uint4 grid_probe0(const GridView& g, unsigned long long key) {
+    return *reinterpret_cast<const uint4*>(&g.table[hash_key(key) & g.mask]);
+}
+__device__ __forceinline__ bool grid_resolve(const GridView& g, unsigned long long key, uint4 e, unsigned int& start,
+                                             unsigned int& count) {
+    const unsigned long long k = ((unsigned long long)e.y << 32) | e.x;
+    if (k == key) {
+        start = e.z;
+        count = e.w;
+        return true;
+    }
+    if (k == BS_EMPTY_KEY) return false;
+    unsigned int h = ((hash_key(key) & g.mask) + 1) & g.mask;
+    for (unsigned int probe = 1; probe <= g.mask; ++probe) {
+        const uint4 f = *reinterpret_cast<const uint4*>(&g.table[h]);
+        const unsigned long long kf = ((unsigned long long)f.y << 32) | f.x;
+        if (kf == key) {
+            start = f.z;
+            count = f.w;
+            return true;
+        }
+        if (kf == BS_EMPTY_KEY) return false;
         h = (h + 1) & g.mask;
     }
     return false;

@@ -518,13 +518,15 @@ __device__ __forceinline__ void gather_xyz(const unsigned long long* sorted, con
         myidx[j] = r < need ? (unsigned int)(sorted[r] & 0xFFFFFFFFu) : 0u;
     }
     __builtin_amdgcn_wave_barrier();
+    // all loads issued before any store (unconditional: ranks past `need` read point 0), so the
+    // gathers' L2 round trips overlap instead of running one after another under a branch
+    float4 p[512 / 64];
+#pragma unroll
+    for (int j = 0; j < 512 / 64; ++j) p[j] = pts4[myidx[j]];
 #pragma unroll
     for (int j = 0; j < 512 / 64; ++j) {
         const int r = lane + 64 * j;
-        if (r < need) {
-            const float4 p = pts4[myidx[j]];
-            fl[r] = p.x; fl[FL_STRIDE + r] = p.y; fl[2 * FL_STRIDE + r] = p.z;
-        }
+        if (r < need) { fl[r] = p[j].x; fl[FL_STRIDE + r] = p[j].y; fl[2 * FL_STRIDE + r] = p[j].z; }
     }
     __builtin_amdgcn_wave_barrier();
 }
