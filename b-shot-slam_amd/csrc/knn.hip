@@ -182,6 +182,14 @@ __device__ __forceinline__ void hist_of_list(KnnLds* L, int nl, float sc0) {
     __builtin_amdgcn_wave_barrier();
 }
 
+// cube radius that holds every point of level-0 buckets [0, b] (bucket_of(d2, 0, KNN_NB / rs2) <= b
+// implies d2 < (b + 1) / KNN_NB * rs2 up to float rounding, covered by the 1e-4 margin): the
+// streaming path's later passes only keep such points, so their cube shrinks to this radius
+__device__ __forceinline__ float bucket_radius(float rs, int b) {
+    if (b >= KNN_NB - 1) return rs;
+    return fminf(rs, rs * sqrtf((float)(b + 1) / (float)KNN_NB) * 1.0001f + 0.01f);
+}
+
 template <bool DIAG>
 __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
                            int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
@@ -338,7 +346,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
                 if constexpr (DIAG) {
                     if (lev > 0 && lane == 0) atomicAdd(&kst[7], 1ull);
                 }
-                for_candidates<2>(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int) {
+                for_candidates<2>(g, &L->cand, qx, qy, qz, bucket_radius(rs, B[0]), rs2, [&](bool v, float d2, unsigned int) {
                     if constexpr (DIAG) ++chunks;
                     if (!v) return;
                     int b = bucket_of(d2, lo[0], sc[0]);
@@ -372,7 +380,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
         const int Bmax = lv >= 1 ? B[0] : KNN_NB - 1;
         const int tot = prefix_offsets(L, Bmax);
         if (tot <= KNN_PRE) {
-            for_candidates<2>(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+            for_candidates<2>(g, &L->cand, qx, qy, qz, bucket_radius(rs, Bmax), rs2, [&](bool v, float d2, unsigned int idx) {
                 if constexpr (DIAG) ++chunks;
                 if (v) {
                     const int b = bucket_of(d2, 0.f, sc0);
@@ -391,7 +399,7 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
     }
     // general path: collect the (refined) prefix and bitonic-sort it
     int cnt = 0;
-    for_candidates<2>(g, &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+    for_candidates<2>(g, &L->cand, qx, qy, qz, lv > 0 ? bucket_radius(rs, B[0]) : rs, rs2, [&](bool v, float d2, unsigned int idx) {
         if constexpr (DIAG) ++chunks;
         bool take = v;
         if (take && lv > 0) {
