@@ -742,6 +742,8 @@ static LadderGrids ladder(const DevGrid* const* g4, int mode) {
     if (mode >= 1) {
         // each step on the grid whose cell is rs/2 or rs/sqrt(2) (r/16 for the two front steps)
         const float f[9] = {0.0625f, 0.08838835f, 0.125f, 0.17677669f, 0.25f, 0.35355339f, 0.5f, 0.70710678f, 1.0f};
+        // (each step on the next finer grid instead: 0.54 -> 0.88 ms, 4.8 failed chunks per query,
+        // profiles/r05_ab_sr_w6.txt)
         const int gi[9] = {0, 0, 0, 1, 1, 2, 2, 3, 3};
         const int o = mode == 2 ? 0 : 2;
         lg.nsteps = 9 - o;
