@@ -194,9 +194,9 @@ struct bshot_ctx {
     int opt_gpu_map = 1;
     bsh::GMap* gmap = nullptr;
     std::vector<bsh::GMap*> gmap_replicas;  // other sequences' maps (multi-GPU exchange, bshot_odom_exchange)
-    // the exchange queues its replica inserts from a thread of its own (host/xchg.cpp): every host
-    // access to the replicas (and the context's teardown) first waits until that thread is idle
-    // (detach = 1 at the context's teardown: the exchange forgets it)
+    // the exchange (host/xchg.cpp) queues its replica inserts on the iss stream, or logs the offers
+    // for later (option xchg_index 0): every host access to the replicas first lets it index what it
+    // has logged (detach = 1 at the context's teardown: the exchange forgets it)
     int (*replica_quiesce)(void* arg, int detach) = nullptr;
     void* replica_quiesce_arg = nullptr;
     // before any access to the replicas: the exchange indexes the offers it has logged (its error code)
@@ -206,6 +206,7 @@ struct bshot_ctx {
         return rc;
     }
     int opt_xseq_targets = 0;  // 1: the replicas' entries join the matching targets (extension; 0 = reference)
+    int opt_xchg_index = 1;    // replica policy: 1 index every exchange at once (iss stream), 0 log and index on read
     DBuf<float> gtgt;  // matching targets assembled on the device (float3)
 
     // match: ma = a rows then b rows; lbest = left keys then right keys; left = left | right | flag

@@ -95,6 +95,10 @@ int gmap_pack_delta(bshot_ctx* c, int kmax, float* d_rec);
 // a record batch (device, count in the header) inserted into replica map `replica` on stream st
 // (nullptr: the context's main stream)
 int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax, bool sync, hipStream_t st = nullptr);
+// n record batches into n distinct replicas at once (the exchange's per-sweep insert): five launches
+// for all of them (kmax <= 4096, n <= 8; else the per-replica path), unsynchronised, on stream st
+int gmap_insert_records_multi(bshot_ctx* c, int n, const int* replicas, const float* const* d_recs, int kmax,
+                              hipStream_t st);
 // host records (bshot_odom_map_delta's 15-float layout) -> replica map (synchronous)
 int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n);
 int gmap_replica_size(bshot_ctx* c, int replica);

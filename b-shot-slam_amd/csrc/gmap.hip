@@ -130,9 +130,8 @@ __global__ void k_gmap_pack(GMapDev m, int slot_base, int k, int kmax, float* __
 
 // a record batch -> slots (positions are already on the grid: createKeypoint is idempotent on them),
 // block ids; records past the count get the empty key (sorted last, skipped by k_gmap_segments)
-__global__ void k_gmap_prep_rec(const float* __restrict__ rec, int kmax, int slot_base, GMapDev m,
-                                unsigned long long* __restrict__ keys, unsigned int* __restrict__ vals) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void prep_rec_at(const float* __restrict__ rec, int i, int kmax, int slot_base, const GMapDev& m,
+                                            unsigned long long* __restrict__ keys, unsigned int* __restrict__ vals) {
     if (i >= kmax) return;
     const int cnt = __float_as_int(rec[0]);
     vals[i] = (unsigned int)i;
@@ -146,6 +145,11 @@ __global__ void k_gmap_prep_rec(const float* __restrict__ rec, int kmax, int slo
 #pragma unroll
     for (int w = 0; w < 11; ++w) m.kdesc[11 * (size_t)s + w] = __float_as_uint(r[4 + w]);
     keys[i] = block_id_of(r[0], r[1], r[2]);
+}
+
+__global__ void k_gmap_prep_rec(const float* __restrict__ rec, int kmax, int slot_base, GMapDev m,
+                                unsigned long long* __restrict__ keys, unsigned int* __restrict__ vals) {
+    prep_rec_at(rec, blockIdx.x * blockDim.x + threadIdx.x, kmax, slot_base, m, keys, vals);
 }
 
 // the block of id: found, or created (um::initial(): one bucket, nothing allocated); -1 past capacity
@@ -197,10 +201,9 @@ __global__ void k_gmap_segments(const unsigned long long* __restrict__ keys, int
 // sorted indices to vals_out and m.ctr[GM_NSEG].
 #define GM_SORT_MAX 4096
 #define GM_SORT_T 1024
-__global__ void __launch_bounds__(GM_SORT_T) k_gmap_sort_segments(const unsigned long long* __restrict__ keys,
-                                                                 const unsigned int* __restrict__ vals, int k,
-                                                                 GMapDev m, unsigned int* __restrict__ vals_out,
-                                                                 int* __restrict__ seg) {
+__device__ __forceinline__ void sort_segments_wg(const unsigned long long* __restrict__ keys,
+                                                 const unsigned int* __restrict__ vals, int k, GMapDev m,
+                                                 unsigned int* __restrict__ vals_out, int* __restrict__ seg) {
     __shared__ unsigned long long sk[GM_SORT_MAX];
     __shared__ unsigned int sv[GM_SORT_MAX];
     __shared__ int wsum[GM_SORT_T / 64];
@@ -273,6 +276,46 @@ __global__ void __launch_bounds__(GM_SORT_T) k_gmap_sort_segments(const unsigned
     }
 }
 
+__global__ void __launch_bounds__(GM_SORT_T) k_gmap_sort_segments(const unsigned long long* __restrict__ keys,
+                                                                 const unsigned int* __restrict__ vals, int k,
+                                                                 GMapDev m, unsigned int* __restrict__ vals_out,
+                                                                 int* __restrict__ seg) {
+    sort_segments_wg(keys, vals, k, m, vals_out, seg);
+}
+
+// Batched replica inserts (the exchange: one sweep's offers into up to GM_XB replicas): one launch
+// per stage for all of them, the replica in blockIdx.y (insert, prep) or blockIdx.x (sort). The job
+// table travels as a kernel argument (blockIdx-uniform: scalar loads from the argument segment).
+#define GM_XB 8
+struct GMapJob {
+    GMapDev m;
+    const float* rec;          // record batch (count in the header)
+    unsigned long long* keys;  // scratch: kmax block ids
+    unsigned int* vals;        // scratch: 2 kmax (batch order, then the sorted order)
+    int* seg;                  // scratch: 3 kmax
+    int* p_ctr;                // pinned copy of the counters (host-coherent)
+    int slot_base;
+};
+struct GMapJobs {
+    GMapJob j[GM_XB];
+};
+
+__global__ void k_gmap_prep_rec_x(GMapJobs J, int kmax) {
+    const GMapJob& jb = J.j[blockIdx.y];
+    prep_rec_at(jb.rec, blockIdx.x * blockDim.x + threadIdx.x, kmax, jb.slot_base, jb.m, jb.keys, jb.vals);
+}
+
+__global__ void __launch_bounds__(GM_SORT_T) k_gmap_sort_segments_x(GMapJobs J, int k) {
+    const GMapJob& jb = J.j[blockIdx.x];
+    sort_segments_wg(jb.keys, jb.vals, k, jb.m, jb.vals + k, jb.seg);
+}
+
+// every replica's counters -> its pinned copy (one wave per replica)
+__global__ void k_gmap_ctr_x(GMapJobs J) {
+    const GMapJob& jb = J.j[blockIdx.x];
+    if (threadIdx.x < bsh::GM_QTOT) jb.p_ctr[threadIdx.x] = jb.m.ctr[threadIdx.x];
+}
+
 // bump allocation from a pool (lane 0); false when the pool is exhausted (error bit 2)
 __device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long long need, int* err, long long* off) {
     const long long o = (long long)atomicAdd(ctr_top, (int)need);
@@ -295,8 +338,8 @@ __device__ __forceinline__ bool pool_alloc(int* ctr_top, long long cap, long lon
 #define GM_SMALL_N 1024   // members: buckets stay <= 1109 (the libstdc++ prime after 541)
 #define GM_SMALL_BK 1152
 template <int LN, int LBK>
-__global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
-                                                          int* __restrict__ seg, int slot_base) {
+__device__ __forceinline__ void insert_wg(const GMapDev& m, const unsigned int* __restrict__ vals, int* __restrict__ seg,
+                                          int slot_base, int wg, int nwg) {
     // the block's LDS image (142 KiB, one workgroup per CU; a sweep touches ~100 blocks): list
     // indices as ushort, hash codes as u32 (10 mm-grid keys), each member's current position + ratio,
     // and the batch's per-candidate results against the staged members
@@ -310,7 +353,7 @@ __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsig
     __shared__ GBlock s_B;
     const int tid = threadIdx.x;
     const int nseg = m.ctr[GM_NSEG];
-    for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+    for (int sg = wg; sg < nseg; sg += nwg) {
         const int j0 = seg[3 * sg], cnt = seg[3 * sg + 1], b = seg[3 * sg + 2];
         if (cnt == 0) continue;  // a run whose block could not be created (GM_ERR is set)
         GBlock B = m.blk[b];
@@ -474,6 +517,18 @@ __global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsig
         if (LN != GM_LDS_N && tid == 0) seg[3 * sg + 1] = 0;
         __syncthreads();
     }
+}
+
+template <int LN, int LBK>
+__global__ void __launch_bounds__(GM_INS_T) k_gmap_insert(GMapDev m, const unsigned int* __restrict__ vals,
+                                                          int* __restrict__ seg, int slot_base) {
+    insert_wg<LN, LBK>(m, vals, seg, slot_base, blockIdx.x, gridDim.x);
+}
+
+template <int LN, int LBK>
+__global__ void __launch_bounds__(GM_INS_T) k_gmap_insert_x(GMapJobs J, int k) {
+    const GMapJob& jb = J.j[blockIdx.y];
+    insert_wg<LN, LBK>(jb.m, jb.vals + k, jb.seg, jb.slot_base, blockIdx.x, gridDim.x);
 }
 
 // Map::getKeypoints: one thread per position of the x/y/z loop -> its block's entry count
@@ -788,6 +843,54 @@ int gmap_insert_records(bshot_ctx* c, int replica, const float* d_rec, int kmax,
     if ((rc = gmap_reserve(c, g, kmax, st)) || (rc = gmap_scratch(c, g, kmax))) return rc;
     bsk::k_gmap_prep_rec<<<(kmax + 255) / 256, 256, 0, st>>>(d_rec, kmax, g.slots, dev_view(g), g.keys.p, g.vals.p);
     return gmap_run_insert(c, g, kmax, sync, st);
+}
+
+int gmap_insert_records_multi(bshot_ctx* c, int n, const int* replicas, const float* const* d_recs, int kmax,
+                              hipStream_t st) {
+    if (!st) st = c->stream;
+    if (n <= 0) return BSHOT_OK;
+    for (int a = 0; a < n; ++a)
+        for (int b = a + 1; b < n; ++b)
+            if (replicas[a] == replicas[b]) return c->fail("gmap_insert_records_multi: replica listed twice", BSHOT_EINVAL);
+    if (kmax > GM_SORT_MAX || n > GM_XB) {
+        // large batches: the per-replica path (radix sort), in order
+        for (int a = 0; a < n; ++a)
+            if (int rc = gmap_insert_records(c, replicas[a], d_recs[a], kmax, false, st)) return rc;
+        return BSHOT_OK;
+    }
+    bsk::GMapJobs J;
+    std::memset(&J, 0, sizeof(J));
+    for (int a = 0; a < n; ++a) {
+        GMap& g = replica_map(c, replicas[a]);
+        int rc = gmap_init(c, g, st);
+        if (rc) return rc;
+        if (kmax <= 0) continue;
+        if ((rc = gmap_reserve(c, g, kmax, st)) || (rc = gmap_scratch(c, g, kmax))) return rc;
+        bsk::GMapJob& jb = J.j[a];
+        jb.m = dev_view(g);
+        jb.rec = d_recs[a];
+        jb.keys = g.keys.p;
+        jb.vals = g.vals.p;
+        jb.seg = g.seg.p;
+        jb.p_ctr = g.p_ctr.p;
+        jb.slot_base = g.slots;
+    }
+    if (kmax <= 0) return BSHOT_OK;
+    bsk::k_gmap_prep_rec_x<<<dim3((kmax + 255) / 256, n), 256, 0, st>>>(J, kmax);
+    bsk::k_gmap_sort_segments_x<<<n, GM_SORT_T, 0, st>>>(J, kmax);
+    // as gmap_run_insert's replica launches, per replica
+    bsk::k_gmap_insert_x<GM_SMALL_N, GM_SMALL_BK><<<dim3(std::min(kmax, 64), n), GM_INS_T, 0, st>>>(J, kmax);
+    bsk::k_gmap_insert_x<GM_LDS_N, GM_LDS_BK><<<dim3(std::min(kmax, 16), n), GM_INS_T, 0, st>>>(J, kmax);
+    bsk::k_gmap_ctr_x<<<n, 64, 0, st>>>(J);
+    HIPCHK(hipGetLastError(), "gmap batched insert launch");
+    for (int a = 0; a < n; ++a) {
+        GMap& g = *c->gmap_replicas[replicas[a]];
+        g.slots += kmax;
+        if (!g.ev_ctr) HIPCHK(hipEventCreateWithFlags(&g.ev_ctr, hipEventDisableTiming), "map event");
+        HIPCHK(hipEventRecord(g.ev_ctr, st), "record map counters");
+        g.ctr_pending = true;
+    }
+    return BSHOT_OK;
 }
 
 int gmap_insert_host_records(bshot_ctx* c, int replica, const float* rec, int n) {

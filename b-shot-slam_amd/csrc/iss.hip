@@ -135,6 +135,9 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
 #define ISS_LCAP 32
 #endif
 #define ISS_LBLOCK 64
+#ifndef ISS_MERGE32
+#define ISS_MERGE32 1  // 0: the 32-key register network (A/B)
+#endif
 
 template <int N>
 __device__ __forceinline__ void sort_net(unsigned long long* k) {
@@ -179,8 +182,65 @@ __device__ __forceinline__ int iss_sum_sorted(const unsigned long long (*keys)[I
         if (r0 >= cnt) break;
         float4 pp[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (r0 + u < cnt) pp[u] = pts4[(unsigned)(k[r0 + u] & 0xFFFFFFFFu)];
+        for (int u = 0; u < 8; ++u) pp[u] = pts4[r0 + u < cnt ? (unsigned)(k[r0 + u] & 0xFFFFFFFFu) : 0u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (r0 + u >= cnt) break;
+            const double dx = (double)pp[u].x - cx, dy = (double)pp[u].y - cy, dz = (double)pp[u].z - cz;
+            sm[0] = sm[0] + dx * dx; sm[1] = sm[1] + dx * dy; sm[2] = sm[2] + dx * dz;
+            sm[3] = sm[3] + dy * dy; sm[4] = sm[4] + dy * dz; sm[5] = sm[5] + dz * dz;
+        }
+    }
+    return cnm;
+}
+
+// the same for lists of 17..32 keys without 32 keys in registers (the 32-key network alone took 64
+// VGPRs and held the kernel at 139, 1.8 waves/CU): each half of 16 is sorted in registers and put
+// back in its LDS slots, then the two runs are merged in rank order as the sum consumes them, 8
+// ranks at a time (the keys are unique: the index breaks d2 ties)
+__device__ __forceinline__ int iss_sum_merge32(unsigned long long (*keys)[ISS_LBLOCK], int t, int cnt,
+                                               const float4* __restrict__ pts4, double cx, double cy, double cz,
+                                               double* sm, unsigned int r2nm_bits, unsigned int* __restrict__ nml,
+                                               int n, int q) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        unsigned long long k[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) k[i] = 16 * h + i < cnt ? keys[16 * h + i][t] : ~0ull;
+        sort_net<16>(k);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) keys[16 * h + i][t] = k[i];
+    }
+    int ia = 0, ib = 16;
+    unsigned long long ha = keys[0][t], hb = keys[16][t];  // run heads (~0 past a run's valid keys)
+    int cnm = 0;
+#pragma unroll
+    for (int r0 = 0; r0 < 32; r0 += 8) {
+        if (r0 >= cnt) break;
+        unsigned long long kk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool ta = ha < hb;
+            kk[u] = ta ? ha : hb;
+            ia += ta ? 1 : 0;
+            ib += ta ? 0 : 1;
+            // both heads reloaded unconditionally (a load under the branch would serialise the steps)
+            const unsigned long long na = keys[ia < 16 ? ia : 15][t], nb = keys[ib < 32 ? ib : 31][t];
+            ha = ia < 16 ? na : ~0ull;
+            hb = ib < 32 ? nb : ~0ull;
+        }
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = r0 + u;
+            pp[u] = pts4[i < cnt ? (unsigned)(kk[u] & 0xFFFFFFFFu) : 0u];  // unconditional: loads in flight together
+            if (i < cnt) {
+                if ((unsigned int)(kk[u] >> 32) < r2nm_bits) {  // d2 >= 0: bit order = float order
+                    nml[(size_t)i * n + q] = (unsigned int)kk[u];
+                    cnm = i + 1;
+                }
+            }
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if (r0 + u >= cnt) break;
@@ -286,7 +346,11 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
         if (wmax <= 8) cnm = iss_sum_sorted<8>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
         else if (wmax <= 16) cnm = iss_sum_sorted<16>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
 #if ISS_LCAP > 16
+#if ISS_MERGE32
+        else cnm = iss_sum_merge32(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+#else
         else cnm = iss_sum_sorted<32>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+#endif
 #endif
         out = iss_third(sm, g21, g32);
         nmc[q] = cnm;

@@ -66,12 +66,23 @@ struct bshot_xchg {
     void* comm = nullptr;
     int nranks = 0, rank = 0, device = 0, kmax = 0;
     float* send = nullptr;  // GM_REC_HDR + GM_REC_W * kmax floats
-    float* recv = nullptr;  // nranks x that
-    // Received offers, append-only in HBM: one gathered recv image per exchange, copied off recv on
-    // the main stream right after the all-gather. The replicas index them only when something reads
-    // a replica (bshot_odom_gpu_replica_*, the Python transport's insert, or xseq_targets, which
-    // inserts every exchange at once): the per-sweep cost without a reader is the all-gather and one
-    // HBM copy. A full log is indexed (replayed in exchange order) before it takes more.
+    float* recv = nullptr;  // nranks x that: the buffer the current exchange gathers into (rbuf[par])
+    // Replica policy (context option xchg_index):
+    // 1 (default, eager): every exchange is indexed into the replicas right away, on the iss stream
+    //   behind the all-gather (one batched insert for all of them, gmap_insert_records_multi); the
+    //   main stream does not wait for it. The gathers alternate between two receive buffers, so the
+    //   next all-gather only waits for the inserts of the exchange before last.
+    // 0 (lazy): the offers are logged in HBM (below) and indexed only when something reads a replica.
+    float* rbuf[2] = {nullptr, nullptr};
+    hipEvent_t ev_rbuf[2] = {nullptr, nullptr};  // the eager inserts reading rbuf[i] are done (iss stream)
+    bool rbuf_busy[2] = {false, false};
+    int par = 0;
+    hipEvent_t ev_gathered = nullptr;  // main stream: the all-gather into recv has landed
+    // Received offers (lazy policy), append-only in HBM: one gathered recv image per exchange, copied
+    // off recv on the main stream right after the all-gather. The replicas index them only when
+    // something reads a replica (bshot_odom_gpu_replica_*, the Python transport's insert, or
+    // xseq_targets, which inserts every exchange at once): the per-sweep cost without a reader is the
+    // all-gather and one HBM copy. A full log is indexed (replayed in exchange order) before it takes more.
     float* log = nullptr;
     size_t log_cap = 0;                             // floats
     std::vector<std::pair<int, int>> log_entries;   // per logged exchange: include_self, sim_peers
@@ -84,15 +95,27 @@ namespace {
 
 size_t per_rank(const bshot_xchg* x) { return bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * x->kmax; }
 
-// insert one gathered image (nranks x per floats) into the replicas, in rank order, on stream xs
+// insert one gathered image (nranks x per floats) into the replicas on stream xs: replica r gets
+// rank r's batch, the simulated peers' replicas this rank's. Batched launches, up to 8 replicas each
+// (every replica's batches stay in exchange order: a replica appears once per image).
 int insert_image(bshot_ctx* c, bshot_xchg* x, const float* img, int include_self, int sim_peers, hipStream_t xs) {
     const size_t per = per_rank(x);
+    std::vector<int> reps;
+    std::vector<const float*> recs;
     for (int r = 0; r < x->nranks; ++r) {
         if (r == x->rank && !include_self) continue;
-        if (int rc = bsh::gmap_insert_records(c, r, img + per * r, x->kmax, false, xs)) return rc;
+        reps.push_back(r);
+        recs.push_back(img + per * r);
     }
-    for (int p = 0; p < sim_peers; ++p)
-        if (int rc = bsh::gmap_insert_records(c, x->nranks + p, img + per * x->rank, x->kmax, false, xs)) return rc;
+    for (int p = 0; p < sim_peers; ++p) {
+        reps.push_back(x->nranks + p);
+        recs.push_back(img + per * x->rank);
+    }
+    constexpr int kBatch = 8;
+    for (size_t a = 0; a < reps.size(); a += kBatch) {
+        const int n = (int)std::min<size_t>(kBatch, reps.size() - a);
+        if (int rc = bsh::gmap_insert_records_multi(c, n, reps.data() + a, recs.data() + a, x->kmax, xs)) return rc;
+    }
     return BSHOT_OK;
 }
 
@@ -153,11 +176,16 @@ int bshot_xchg_create(bshot_xchg** out, const void* id128, int nranks, int rank,
     x->kmax = kmax;
     const size_t per = bsh::GM_REC_HDR + (size_t)bsh::GM_REC_W * kmax;
     if (hipMalloc(&x->send, sizeof(float) * per) != hipSuccess ||
-        hipMalloc(&x->recv, sizeof(float) * per * nranks) != hipSuccess ||
-        hipEventCreateWithFlags(&x->ev_inserted, hipEventDisableTiming) != hipSuccess) {
+        hipMalloc(&x->rbuf[0], sizeof(float) * per * nranks) != hipSuccess ||
+        hipMalloc(&x->rbuf[1], sizeof(float) * per * nranks) != hipSuccess ||
+        hipEventCreateWithFlags(&x->ev_inserted, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->ev_gathered, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->ev_rbuf[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->ev_rbuf[1], hipEventDisableTiming) != hipSuccess) {
         bshot_xchg_destroy(x);
         return BSHOT_EHIP;
     }
+    x->recv = x->rbuf[0];
     UniqueId id;
     std::memcpy(id.internal, id128, 128);
     if (rccl().init_rank(&x->comm, nranks, id, rank) != 0) {
@@ -178,12 +206,14 @@ void bshot_xchg_destroy(bshot_xchg* x) {
         x->jc->replica_quiesce = nullptr;
     }
     if (x->comm) rccl().destroy(x->comm);
-    if (x->ev_inserted) {
-        (void)hipEventSynchronize(x->ev_inserted);
-        (void)hipEventDestroy(x->ev_inserted);
-    }
+    for (hipEvent_t* e : {&x->ev_inserted, &x->ev_rbuf[0], &x->ev_rbuf[1], &x->ev_gathered})
+        if (*e) {
+            (void)hipEventSynchronize(*e);
+            (void)hipEventDestroy(*e);
+        }
     if (x->send) (void)hipFree(x->send);
-    if (x->recv) (void)hipFree(x->recv);
+    for (float* b : x->rbuf)
+        if (b) (void)hipFree(b);
     if (x->log) (void)hipFree(x->log);
     delete x;
 }
@@ -201,12 +231,32 @@ int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self, int s
     c->hmark("M_x_begin");
     int rc = bsh::gmap_pack_delta(c, x->kmax, x->send);
     if (rc) return rc;
+    const bool eager = c->opt_xchg_index != 0 && !c->opt_xseq_targets;
+    if (eager) {
+        x->par ^= 1;
+        x->recv = x->rbuf[x->par];
+    }
+    // the eager inserts that read this buffer (the exchange before last) are done before it is refilled
+    if (x->rbuf_busy[x->par]) {
+        if (hipStreamWaitEvent(c->stream, x->ev_rbuf[x->par], 0) != hipSuccess)
+            return c->fail("exchange: stream wait", BSHOT_EHIP);
+        x->rbuf_busy[x->par] = false;
+    }
     const int e = rccl().all_gather(x->send, x->recv, per, kNcclFloat32, x->comm, c->stream);
     if (e != 0) return c->fail(std::string("ncclAllGather: ") + (rccl().err ? rccl().err(e) : "error"), BSHOT_EHIP);
     x->jc = c;
     c->replica_quiesce = quiesce;
     c->replica_quiesce_arg = x;
-    if (c->opt_xseq_targets) {
+    if (eager) {
+        // index this exchange now, on the iss stream behind the all-gather (after anything logged
+        // under the lazy policy); nothing on the main stream waits for it
+        if ((rc = replay_log(c, x))) return rc;
+        if (hipEventRecord(x->ev_gathered, c->stream) != hipSuccess || hipStreamWaitEvent(c->iss, x->ev_gathered, 0) != hipSuccess)
+            return c->fail("exchange: stream wait", BSHOT_EHIP);
+        if ((rc = insert_image(c, x, x->recv, include_self, sim_peers, c->iss))) return rc;
+        if (hipEventRecord(x->ev_rbuf[x->par], c->iss) != hipSuccess) return c->fail("exchange: event", BSHOT_EHIP);
+        x->rbuf_busy[x->par] = true;
+    } else if (c->opt_xseq_targets) {
         // the matching reads the replicas: index this exchange now (after anything logged), on the iss
         // stream, and let the main stream wait for it
         if ((rc = replay_log(c, x))) return rc;

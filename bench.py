@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--sim-peers", type=int, default=0,
                     help="N = 1: run the RCCL map exchange on a 1-rank communicator and insert this rank's batch "
                          "into P more replicas per sweep (bshot_odom_exchange_sim): the insert work of a job of 1 + P ranks")
+    ap.add_argument("--xchg-lazy", action="store_true",
+                    help="replica policy xchg_index 0: log the gathered offers in HBM, index replicas on read "
+                         "(default: every exchange indexed into the replicas inside the sweep, on the iss stream)")
     ap.add_argument("--map-bcast-py", action="store_true",
                     help="with --map-bcast: the Python all_gather of host records into host replicas instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -301,6 +304,8 @@ def main():
         odo.set_option("ladder_grids", a.ladder_grids)
     if a.metrics and rank == 0:
         odo.set_metrics_file(a.metrics)
+    if a.xchg_lazy:
+        odo.set_option("xchg_index", 0)
     for kv in a.opt:
         name, val = kv.split("=")
         odo.set_option(name, int(val))
@@ -605,11 +610,14 @@ def main():
                                    f"full extract+describe+match+RANSAC+ICP+map per sweep",
                        "keypoints": a.keypoints, "points_per_sweep": int(n_eff), "target_M": int(m_eff),
                        "map_size_readback": bool(a.map_sync),
-                       "icp_iters": icp_it, "mutual_corr": round(corr, 1), "parallelism": f"frame-shard x{world}" +
+                       "icp_iters": icp_it, "mutual_corr": round(corr, 1), "parallelism": f"sequence per rank x{world}" +
                        ((" + map exchange over torch.distributed" if a.map_bcast_py else " + RCCL map exchange")
                         if a.map_bcast else "") +
                        (f" + RCCL map exchange (1 rank) with {a.sim_peers} simulated peers' replica inserts"
-                        if a.sim_peers > 0 else "")},
+                        if a.sim_peers > 0 else "") +
+                       ((" (replicas logged in HBM, indexed on read)" if a.xchg_lazy else
+                         " (replicas indexed every sweep, inside the timed region)")
+                        if xchg is not None else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "upload_inclusive": upload_leg,

@@ -309,7 +309,8 @@ int bshot_map_set_query_mode(bshot_map* m, int mode);
  *      lane-order check (bshot_debug_lds_lane_order); "icp_device" 0 (default) / 1: ICP iterations
  *      handed to the host's Umeyama, or the whole loop on the device. Behaviour: "gpu_map" 1 (default, libstdc++ order) / 2
  *      (canonical order) / 0 (host Map); "xseq_targets" 0 (default): other sequences' replicas join
- *      the matching targets; "host_map_log" 1 (default; 0 under bshot_odom): keep the GPU map's
+ *      the matching targets; "xchg_index" 1 (default): the exchange indexes every gathered offer into
+ *      the replicas at once (iss stream), 0: logs them in HBM and indexes on read; "host_map_log" 1 (default; 0 under bshot_odom): keep the GPU map's
  *      insert log so the host Map view (LidarOdometry::getKeypoints, getBlockKeypoints) can be
  *      rebuilt -- without it host memory stays flat over a run and that view is unavailable;
  *      "map_sync" 1 (default): the GPU map insert is waited for and bshot_frame_stats.map_size

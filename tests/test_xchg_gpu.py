@@ -55,37 +55,50 @@ def test_rccl_exchange_self_replica():
         x.close()
 
 
-def test_exchange_sim_peers_replicas():
+@pytest.mark.parametrize("index,peers", [(1, 3), (0, 3), (1, 10)])
+def test_exchange_sim_peers_replicas(index, peers):
     # bshot_odom_exchange_sim (bench.py --sim-peers): every simulated peer's replica receives this
-    # rank's batch, so each must equal the own map (entries, block order, size) sweep after sweep
+    # rank's batch, so each must equal the own map (entries, block order, size) sweep after sweep --
+    # indexed at once (xchg_index 1: batched inserts of up to 8 replicas; 10 peers take two batches)
+    # or from the log on read (0)
     uid = bshot_py.Exchange.unique_id()
     x = bshot_py.Exchange(uid, 1, 0, 0, K)
     od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+    od.set_option("xchg_index", index)
     try:
+        prev = None
         for f, xyz in enumerate(_frames(n=4)):
+            rq = od.gpu_replica_query(peers, prev[0][:3, 3]) if prev is not None else None
             st = od.process(xyz)
-            od.exchange_sim(x, 3)
+            if rq is not None:  # the last peer's replica is the own map this sweep's matching read
+                tx, tb = od.target()
+                m = len(tx) - prev[1]
+                assert m == len(rq[0]) and m > 0
+                assert np.array_equal(_u(tx[:m]), _u(rq[0])) and np.array_equal(tb[:m], rq[1]), f
+            od.exchange_sim(x, peers)
             pos = np.array(st.pose, np.float32).reshape(4, 4)[:3, 3]
             ref = od.gpu_replica_query(1, pos)
-            for r in (1, 2, 3):
+            for r in range(1, peers + 1):
                 assert od.gpu_replica_size(r) == st.map_size, (f, r)
                 got = od.gpu_replica_query(r, pos)
                 assert np.array_equal(_u(got[0]), _u(ref[0])) and np.array_equal(got[1], ref[1]), (f, r)
             assert od.gpu_replica_size(0) == 0  # this rank's own replica is not fed (include_self off)
+            prev = (np.array(st.pose, np.float32).reshape(4, 4), st.n_keypoints)
     finally:
         od.close()
         x.close()
 
 
 def test_exchange_log_replayed_in_order(monkeypatch):
-    """The exchange logs every gathered offer in HBM and indexes the replicas only when one is read:
-    nine sweeps' offers accumulate (a 200 KB log holds four: it is replayed into the replicas three
+    """Replica policy xchg_index 0: the exchange logs every gathered offer in HBM and indexes the
+    replicas only when one is read: nine sweeps' offers accumulate (a 200 KB log holds four: it is replayed into the replicas three
     times on the way), and the replica read before the last sweep must equal the own map the last
     sweep's matching reads (entries, libstdc++ block order, descriptors)."""
     monkeypatch.setenv("BSHOT_XCHG_LOG_KB", "200")
     uid = bshot_py.Exchange.unique_id()
     x = bshot_py.Exchange(uid, 1, 0, 0, K)
     od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=K))
+    od.set_option("xchg_index", 0)  # the lazy replica policy
     try:
         frames = _frames(n=10)
         prev = None
