@@ -333,8 +333,8 @@ class Context:
         self.L.bshot_stage_reset(self.h)
 
     def work(self):
-        w = (ctypes.c_int64 * 8)()
-        self.L.bshot_work_counters(self.h, w, 8)
+        w = (ctypes.c_int64 * 12)()
+        self.L.bshot_work_counters(self.h, w, 12)
         return list(w)
 
     def sync(self):

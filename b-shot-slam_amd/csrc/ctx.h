@@ -101,6 +101,7 @@ struct CloudState {
     PinBuf<int> h_err;  // [0] SR, [1] ISS
     hipEvent_t ev_loaded = nullptr, ev_sr = nullptr, ev_iss = nullptr;
     bool fine_ladder = false;  // 4 grids + 7-step sqrt(2) radius ladder (opt_ladder4)
+    bool iss_lvl = false;      // grid_iss is the ladder's fifth level (cells r/32, the ladder's points)
     void fix_ladder(bool four) {
         fine_ladder = four;
         ladder[0] = four ? &grid_l16 : &grid_fine;
@@ -147,7 +148,7 @@ struct bshot_ctx {
     int opt_rank_max = -1;      // k_shot_rank_wg's in-place threshold (-1: RK_RANKMAX; 0: every span sorted)
     int opt_rank_wg = 2;        // SHOT rank kernel: 0 wave per 64-rank chunk, 1 workgroup per keypoint, 2 by neighbourhood size
     int opt_sr_start = 80;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
-    int opt_iss_grid = 1;       // ISS on the SR ladder's finest grid when its cell >= 2 x salient radius (0: own grid)
+    int opt_iss_grid = 1;       // ISS on the SR ladder's points: its fifth level, cells r/32 (0: own grid)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
 
     DBuf<int> errw;  // describe-stage error bits (normals)
@@ -181,7 +182,6 @@ struct bshot_ctx {
     bsh::VeloState* velo = nullptr;  // GPU packet decode state (csrc/velodyne.hip), created on first use
     DBuf<unsigned int> sbh, sbst;  // bucketed gather: per-keypoint d2 histogram and bucket starts
     // lookahead keypoint gather (ctx_gather_kps_async): own index and staging buffers
-    DBuf<int> kidx;
     PinBuf<int> p_kidx;
     PinBuf<float> p_kps3;
     int opt_chunk_blocks = 0;  // grid cap of the 64-rank chunk kernels (0: one block per 4 chunks)
@@ -256,7 +256,6 @@ struct bshot_ctx {
     PinBuf<int> p_rhyp, p_rcnt;
 
     // generic gather
-    DBuf<int> gidx;
     DBuf<float> gout;
 
     // pinned staging of per-frame host<->device transfers (pageable copies stall behind other
@@ -276,7 +275,8 @@ struct bshot_ctx {
     std::vector<hipEvent_t> evpool;
     double stage_ms[BSHOT_NSTAGES] = {0};
     int64_t stage_n[BSHOT_NSTAGES] = {0};
-    int64_t work[8] = {0};
+    int64_t work[12] = {0};
+    DBuf<int> iqstat;  // ICP host loop: cumulative grid searches after iteration 0, and the most one wave took in an iteration
 
     int fail(const char* what, hipError_t e);
     int fail(const std::string& what, int code);

@@ -164,6 +164,7 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
     s.n = n;
     s.d_xyz = d_xyz;
     s.grids_ok = false;
+    s.iss_lvl = false;
     s.prefetched = false;
     s.sr_state = 0;
     s.iss_state = 0;
@@ -174,7 +175,15 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
         const int sg1 = c->stage_begin(BSHOT_STAGE_GRID, st);
         if (c->opt_ladder4) {
             bsh::DevGrid* const lad[4] = {&s.grid_l16, &s.grid_fine, &s.grid_l4, &s.grid_coarse};
-            HIPCHK(grid_build_ladder(lad, d_xyz, n, c->prm.seg_radius * 0.0625f, s.pts4.p, st), "grid build (ladder)");
+            // ISS's grid is the ladder's fifth, finest level (cells r/32) when those cells are at least
+            // half the salient radius (no sort of its own)
+            const float c0 = c->prm.seg_radius * 0.0625f;
+#ifndef ISS_LEVEL5
+#define ISS_LEVEL5 1  // 0: ISS on the SR ladder's level 0 (cells r/16) as in round 4 (A/B)
+#endif
+            s.iss_lvl = ISS_LEVEL5 && c->opt_iss_grid && 0.5f * c0 >= 0.5f * c->prm.iss_salient;  // cells r/32 >= salient / 2
+            HIPCHK(grid_build_ladder(lad, d_xyz, n, c0, s.pts4.p, st, 0xFu, 0, s.iss_lvl ? &s.grid_iss : nullptr),
+                   "grid build (ladder)");
         } else {
             HIPCHK(grid_build(s.grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, s.pts4.p, st), "grid build (r/8)");
             HIPCHK(grid_build(s.grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, s.pts4.p, st), "grid build (r/2)");
@@ -202,9 +211,9 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
                                 c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks, c->opt_sr_xcd_chunk),
                "seg_ratio launch");
         c->stage_end(sg2, st);
-        HIPCHK(kcopy(s.h_ratio.p, s.ratio.p, sizeof(float) * n, st), "D2H ratio");
     }
-    HIPCHK(kcopy(s.h_err.p, s.errw.p, sizeof(int), st), "D2H err");
+    HIPCHK(kcopy2(s.h_ratio.p, s.ratio.p, sizeof(float) * (size_t)(n > 0 ? n : 0), s.h_err.p, s.errw.p, sizeof(int), st),
+           "D2H ratio + err");
     HIPCHK(hipEventRecord(s.ev_sr, st), "record sr");
     s.sr_state = 1;
     return BSHOT_OK;
@@ -223,24 +232,25 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(kfill(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
-        // the SR ladder's finest grid serves ISS when its cell holds the salient ball's cube in
-        // 2 x 2 x 2 cells (r/16 = 187.5 mm >= 2 x 60 mm at the reference's settings): no sort of
-        // its own (the ISS kernels visit the same points, in cells that hold more of them)
-        const bool reuse = c->opt_iss_grid && c->opt_ladder4 && s.fine_ladder &&
-                           s.grid_l16.n == n && s.grid_l16.cell >= 2.f * c->prm.iss_salient;
+        // ISS on the SR ladder's points, no sort of its own: the ladder's fifth level (cells r/32 =
+        // 93.75 mm at the reference's settings, <= 3 per axis around a 60 mm ball) when the ladder
+        // built it, else its finest SR level when that cell holds the ball's cube in 2 x 2 x 2 cells
+        const bool lvl5 = s.fine_ladder && s.iss_lvl && s.grid_iss.n == n;
+        const bool reuse = lvl5 || (c->opt_iss_grid && c->opt_ladder4 && s.fine_ladder && s.grid_l16.n == n &&
+                                    s.grid_l16.cell >= 2.f * c->prm.iss_salient);
         if (!reuse)
             HIPCHK(grid_build(s.grid_iss, s.d_xyz, n, c->prm.iss_salient * (float)c->opt_iss_cell, s.pts4.p, st, false),
                    "grid build (ISS)");
         c->hmark("Q_iss_grid");
-        HIPCHK(launch_iss(reuse ? s.grid_l16 : s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
+        HIPCHK(launch_iss(reuse && !lvl5 ? s.grid_l16 : s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
                           s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks),
                "iss launch");
         c->stage_end(sg3, st);
         c->hmark("Q_iss_k");
-        HIPCHK(kcopy(s.h_flag.p, s.issflag.p, n, st), "D2H iss");
     }
-    HIPCHK(kcopy(s.h_err.p + 1, s.errw.p + 1, sizeof(int), st), "D2H err");
+    HIPCHK(kcopy2(s.h_flag.p, s.issflag.p, (size_t)(n > 0 ? n : 0), s.h_err.p + 1, s.errw.p + 1, sizeof(int), st),
+           "D2H iss + err");
     HIPCHK(hipEventRecord(s.ev_iss, st), "record iss");
     s.iss_state = 1;
     return BSHOT_OK;
@@ -615,15 +625,20 @@ int ctx_match_dev(bshot_ctx* c, int na, int nb) {
     return BSHOT_OK;
 }
 
-int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst) {
-    HIPCHK(c->gidx.ensure(k > 0 ? k : 1), "alloc gidx");
+// gathers read their indices from pinned staging inside the kernel (no upload launch); the host
+// copy, when asked for, is written by the same kernel
+static int gather_io(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst,
+                     float* hout) {
     HIPCHK(dst.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc gather out");
     if (k <= 0) return BSHOT_OK;
     HIPCHK(c->p_gidx.ensure(k), "alloc pinned idx");
     std::memcpy(c->p_gidx.p, h_idx, sizeof(int) * k);
-    HIPCHK(kcopy(c->gidx.p, c->p_gidx.p, sizeof(int) * k, st), "H2D idx");
-    HIPCHK(launch_gather(S.pts4.p, c->gidx.p, k, dst.p, st), "gather");
+    HIPCHK(launch_gather_io(S.pts4.p, c->p_gidx.p, k, dst.p, hout, st), "gather");
     return BSHOT_OK;
+}
+
+int ctx_gather_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst) {
+    return gather_io(c, S, st, h_idx, k, dst, nullptr);
 }
 
 int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst) {
@@ -632,10 +647,9 @@ int ctx_gather(bshot_ctx* c, const int* h_idx, int k, DBuf<float>& dst) {
 
 int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k, DBuf<float>& dst,
                        float* out) {
-    int rc = ctx_gather_on(c, S, st, h_idx, k, dst);
+    if (k > 0) HIPCHK(c->p_g3.ensure(3 * (size_t)k), "alloc pinned gather");
+    int rc = gather_io(c, S, st, h_idx, k, dst, k > 0 ? c->p_g3.p : nullptr);
     if (rc || k <= 0) return rc;
-    HIPCHK(c->p_g3.ensure(3 * (size_t)k), "alloc pinned gather");
-    HIPCHK(kcopy(c->p_g3.p, dst.p, sizeof(float) * 3 * k, st), "D2H gather");
     HIPCHK(hipStreamSynchronize(st), "sync gather");
     std::memcpy(out, c->p_g3.p, sizeof(float) * 3 * k);
     return BSHOT_OK;
@@ -645,15 +659,12 @@ int ctx_gather_host_on(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h
 // D2H of the coordinates into c->p_kps3 are queued on st with buffers of their own (the ISS gather
 // runs concurrently); the caller syncs st before reading c->p_kps3
 int ctx_gather_kps_async(bshot_ctx* c, CloudState& S, hipStream_t st, const int* h_idx, int k) {
-    HIPCHK(c->kidx.ensure(k > 0 ? k : 1), "alloc kidx");
     HIPCHK(c->kps.ensure(3 * (size_t)(k > 0 ? k : 1)), "alloc kps");
     if (k <= 0) return BSHOT_OK;
     HIPCHK(c->p_kidx.ensure(k), "alloc pinned kidx");
     HIPCHK(c->p_kps3.ensure(3 * (size_t)k), "alloc pinned kps");
     std::memcpy(c->p_kidx.p, h_idx, sizeof(int) * k);
-    HIPCHK(kcopy(c->kidx.p, c->p_kidx.p, sizeof(int) * k, st), "H2D kidx");
-    HIPCHK(launch_gather(S.pts4.p, c->kidx.p, k, c->kps.p, st), "gather kps");
-    HIPCHK(kcopy(c->p_kps3.p, c->kps.p, sizeof(float) * 3 * k, st), "D2H kps");
+    HIPCHK(launch_gather_io(S.pts4.p, c->p_kidx.p, k, c->kps.p, c->p_kps3.p, st), "gather kps");
     return BSHOT_OK;
 }
 
@@ -667,7 +678,8 @@ int ctx_sync_main(bshot_ctx* c) {
 }
 
 // the ICP targets' nested grids (cells 1000, 2000, 4000, 8000 mm, all hashed) from one
-// nested-key sort of d_tgt; float4 targets in index order -> itgt
+// nested-key sort of d_tgt; float4 targets in index order -> itgt. A sort-free build by counting
+// (four launches instead of ~13) measured 2-4 % slower end to end (profiles/r05g_ab_*.txt)
 static hipError_t icp_grids(bshot_ctx* c, const float* d_tgt, int nt, int min_cap) {
     DevGrid* lad[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
     return grid_build_ladder(lad, d_tgt, nt, 1000.f, c->itgt.p, c->stream, 0xFu, min_cap);
@@ -724,7 +736,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             // workgroup to arrive); the stopping step writes the composed transform and the iteration
             // count to coherent pinned memory, seq last. The host waits once.
             HIPCHK(c->ipos.ensure(ns), "alloc icp positions");
-            HIPCHK(c->irec.ensure(7 * (size_t)ns), "alloc icp records");
+            HIPCHK(c->irec.ensure(7 * (size_t)((ns + 3) & ~3)), "alloc icp records");  // 16-B aligned rows
             HIPCHK(c->ictl.ensure(1), "alloc icp state");
             HIPCHK(c->isync.ensure(2), "alloc icp sync");
             c->p_iout.coherent = true;
@@ -790,8 +802,12 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             HIPCHK(launch_icp_lists_host(d_src0, ns, g4, c->itgt.p, nt, ICP_LIST_CAP, c->ilst.p, c->ilsd.p, c->ilcnt.p,
                                          c->ilcen.p, c->p_ibest.p, done0, c->stream),
                    "icp lists");
+            if (!c->iqstat.p) {
+                HIPCHK(c->iqstat.ensure(2), "alloc icp stats");
+                HIPCHK(kfill(c->iqstat.p, 0, 2 * sizeof(int), c->stream), "zero icp stats");
+            }
             HIPCHK(launch_icp_iterations(d_src0, ns, 1, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilcen.p, ICP_LIST_CAP, g4,
-                                         c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p, c->stream),
+                                         c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p, c->stream, c->iqstat.p),
                    "icp iterations");
             c->stage_end(sg14);
             auto release = [&](int go) { __atomic_store_n(&sy->go, go, __ATOMIC_RELEASE); };
@@ -846,6 +862,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                 }
                 const long long t_b = ns_now();
                 c->work[2] += t_b - t_a;              // host wait for the keys
+                if (it == j_lists) c->work[8] += t_b - t_a;  // of which: the lists kernel's (iteration 0 or a restart)
                 if (it > 0) c->work[4] += t_a - tw;  // host step between two waits
                 const unsigned long long* best = c->p_ibest.p + (size_t)ns * (it & 1);
                 for (int i = 0; i < ns; ++i) {
@@ -991,12 +1008,12 @@ void bshot_destroy(bshot_ctx* c) {
     c->p_nrm.release(); c->normals_snap.release();
     if (c->ev_xyz) (void)hipEventDestroy(c->ev_xyz);
     c->rpts.release(); c->rhyp.release(); c->rcnt.release(); c->p_rpts.release(); c->p_rhyp.release(); c->p_rcnt.release();
-    c->sbh.release(); c->sbst.release(); c->kidx.release(); c->p_kidx.release(); c->p_kps3.release();
+    c->sbh.release(); c->sbst.release(); c->p_kidx.release(); c->p_kps3.release();
     bsh::pre_free(c->prep);
     c->prep = nullptr;
     bsh::velo_free(c->velo);
     c->velo = nullptr;
-    c->gidx.release(); c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->p_iout.release(); c->p_isync.release(); c->p_ibest.release(); c->p_idone.release(); c->p_src2.release(); c->ipos.release(); c->ilcen.release(); c->irec.release(); c->ictl.release(); c->isync.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release();
+    c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->p_iout.release(); c->p_isync.release(); c->p_ibest.release(); c->p_idone.release(); c->p_src2.release(); c->ipos.release(); c->ilcen.release(); c->irec.release(); c->ictl.release(); c->isync.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release(); c->iqstat.release();
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
@@ -1284,8 +1301,16 @@ int bshot_work_counters(bshot_ctx* c, int64_t* out, int n) {
     if (!c) return BSHOT_EINVAL;
     c->work[6] = g_regrow_n.load();
     c->work[7] = g_regrow_bytes.load();
-    for (int i = 0; i < n && i < 8; ++i) out[i] = c->work[i];
-    return 8;
+    if (n > 9 && c->iqstat.p) {
+        int q[2] = {0, 0};
+        if (hipStreamSynchronize(c->stream) == hipSuccess &&
+            hipMemcpy(q, c->iqstat.p, sizeof(q), hipMemcpyDeviceToHost) == hipSuccess) {
+            c->work[9] = q[0];
+            c->work[10] = q[1];
+        }
+    }
+    for (int i = 0; i < n && i < 12; ++i) out[i] = c->work[i];
+    return 12;
 }
 
 }  // extern "C"

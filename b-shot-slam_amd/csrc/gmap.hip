@@ -200,7 +200,9 @@ __global__ void k_gmap_segments(const unsigned long long* __restrict__ keys, int
 // numbered by an exclusive scan of the run starts (deterministic, no counter to clear). Writes the
 // sorted indices to vals_out and m.ctr[GM_NSEG].
 #define GM_SORT_MAX 4096
-#define GM_SORT_T 1024
+#ifndef GM_SORT_T
+#define GM_SORT_T 1024  // 256 threads: 40 -> 85 us per launch under load, the same sweeps/s (r05g)
+#endif
 __device__ __forceinline__ void sort_segments_wg(const unsigned long long* __restrict__ keys,
                                                  const unsigned int* __restrict__ vals, int k, GMapDev m,
                                                  unsigned int* __restrict__ vals_out, int* __restrict__ seg) {
@@ -544,18 +546,23 @@ __global__ void k_gmap_qcount(GMapDev m, int x0, int y0, int z0, int ny, int nz,
     cnt[t] = b >= 0 ? m.blk[b].n : 0;
 }
 
-// exclusive scan of cnt[0, npos) in one workgroup of 1024 threads; total -> *tot
-__global__ void __launch_bounds__(1024) k_gmap_scan(const int* __restrict__ cnt, int npos, int* __restrict__ off,
-                                                    int* __restrict__ tot) {
-    __shared__ int part[1024];
+// exclusive scan of cnt[0, npos) in one workgroup; total -> *tot. 256 threads: a one-workgroup
+// kernel of the main stream needs a CU with that many free wave slots, and under the lookahead's
+// load a 1024-thread workgroup (16 waves on one CU) waited for one to drain
+#ifndef GM_SCAN_T
+#define GM_SCAN_T 256
+#endif
+__global__ void __launch_bounds__(GM_SCAN_T) k_gmap_scan(const int* __restrict__ cnt, int npos, int* __restrict__ off,
+                                                         int* __restrict__ tot) {
+    __shared__ int part[GM_SCAN_T];
     const int t = threadIdx.x;
-    const int per = (npos + 1023) / 1024;
+    const int per = (npos + GM_SCAN_T - 1) / GM_SCAN_T;
     const int a = t * per, e = min(npos, a + per);
     int s = 0;
     for (int i = a; i < e; ++i) s += cnt[i];
     part[t] = s;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
+    for (int d = 1; d < GM_SCAN_T; d <<= 1) {
         const int v = t >= d ? part[t - d] : 0;
         __syncthreads();
         part[t] += v;
@@ -563,7 +570,7 @@ __global__ void __launch_bounds__(1024) k_gmap_scan(const int* __restrict__ cnt,
     }
     int run = t > 0 ? part[t - 1] : 0;
     for (int i = a; i < e; ++i) { off[i] = run; run += cnt[i]; }
-    if (t == 1023) *tot = part[1023];
+    if (t == GM_SCAN_T - 1) *tot = part[GM_SCAN_T - 1];
 }
 
 // one wave per loop position: the block's entries in iteration order (mode 1) or insertion order
@@ -945,7 +952,7 @@ static int query_count(bshot_ctx* c, GMap& g, const QueryBox& q) {
     int* cnt = g.qcnt.p;
     bsk::k_gmap_qcount<<<(q.npos + 255) / 256, 256, 0, c->stream>>>(dev_view(g), q.x0, q.y0, q.z0, q.ny, q.nz, q.npos, cnt,
                                                                     cnt + q.npos);
-    bsk::k_gmap_scan<<<1, 1024, 0, c->stream>>>(cnt, q.npos, cnt + 2 * q.npos, cnt + 3 * q.npos);
+    bsk::k_gmap_scan<<<1, GM_SCAN_T, 0, c->stream>>>(cnt, q.npos, cnt + 2 * q.npos, cnt + 3 * q.npos);
     HIPCHK(kcopy(g.p_ctr.p + GM_QTOT, cnt + 3 * q.npos, sizeof(int), c->stream),
            "D2H map total");
     g.q_active = true;
@@ -1089,18 +1096,16 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
     // ISS gather, which runs concurrently
     GMap& g = *c->gmap;
     HIPCHK(g.p_tgt.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc pinned targets");
-    if (nb > 0)
-        HIPCHK(kcopy(g.p_tgt.p, c->gtgt.p, sizeof(float) * 3 * nb, c->stream),
-               "D2H targets");
     const bool run = na > 0 && nb > 0;
     if (run) {
         HIPCHK(c->p_left.ensure(2 * (size_t)na + nb), "alloc pinned match out");
         rc = ctx_match_dev(c, na, nb);
         if (rc) return rc;
-        HIPCHK(kcopy(c->p_left.p, c->left.p, sizeof(int) * (2 * (size_t)na + nb),
-                              c->stream),
-               "D2H match");
     }
+    // the targets' positions and the match result in one launch
+    HIPCHK(kcopy2(g.p_tgt.p, c->gtgt.p, sizeof(float) * 3 * (size_t)(nb > 0 ? nb : 0), c->p_left.p, c->left.p,
+                  run ? sizeof(int) * (2 * (size_t)na + nb) : 0, c->stream),
+           "D2H targets + match");
     c->hmark("M_m_launched");
     HIPCHK(hipStreamSynchronize(c->stream), "sync match");
     c->hmark("M_m_synced");

@@ -69,19 +69,21 @@ __global__ void k_grid_cells(const unsigned long long* __restrict__ keys, const 
     atomicAdd(ncells, 1);
 }
 
-// ---- nested ladder grids (cells c, 2c, 4c, 8c) from ONE sort -------------------------------
+// ---- nested ladder grids (cells c/2, c, 2c, 4c, 8c) from ONE sort ------------------------
 // floor(x / (2^L c)) == floor(x / c) >> L exactly (division by a power of two commutes with the
-// double rounding), so a level-L cell is a prefix of the hierarchical key
-//   (18-bit biased level-3 x, y, z) | level-2 child bits | level-1 child bits | level-0 child bits
-// (63 bits; the radix sort's 8 passes are those of any key over 56 bits) and points sorted by that
-// key are contiguous per cell at every level. The level-0 range |ix| < 2^20 is that of cell_key, so
-// every grid of the ladder indexes the same points (+-196 km per axis at c0 = 187.5 mm).
+// double rounding), so a cell of any level is a prefix of the hierarchical key
+//   (17-bit biased level-3 x, y, z) | level-2 | level-1 | level-0 | level-(-1) child bits
+// (63 bits) and points sorted by that key are contiguous per cell at every level. The range rule
+// |ix| < 2^20 at the finest level (cells c/2: cell_key's range; +-98 km per axis at c = 187.5 mm,
+// +-524 km at the ICP's c = 1000 mm) keeps the level-3 coordinate in 17 bits; every grid of the
+// ladder indexes the same points. The finest level (c/2) is ISS's grid when the caller asks for it.
 __device__ __forceinline__ bool ladder_cells(float x, float y, float z, float c0, int& ix, int& iy, int& iz) {
     if (!(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z))) return false;
-    ix = cell_of(x, c0);
-    iy = cell_of(y, c0);
-    iz = cell_of(z, c0);
-    const int lim = 1 << 20;  // cell_key's level-0 range; level-3 coordinate fits 18 bits biased
+    const float ch = c0 * 0.5f;
+    ix = cell_of(x, ch);
+    iy = cell_of(y, ch);
+    iz = cell_of(z, ch);
+    const int lim = 1 << 20;
     return ix > -lim && ix < lim && iy > -lim && iy < lim && iz > -lim && iz < lim;
 }
 
@@ -92,51 +94,79 @@ __global__ void k_ladder_keys(const float* __restrict__ xyz, int n, float c0, un
     const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
     pts4[i] = make_float4(x, y, z, __uint_as_float((unsigned)i));
     unsigned long long k = BS_EMPTY_KEY;
-    int ix, iy, iz;
+    int ix, iy, iz;  // cells c0 / 2
     if (ladder_cells(x, y, z, c0, ix, iy, iz)) {
-        const unsigned long long x3 = (unsigned)((ix >> 3) + (1 << 17)), y3 = (unsigned)((iy >> 3) + (1 << 17)),
-                                 z3 = (unsigned)((iz >> 3) + (1 << 17));
-        k = (x3 << 45) | (y3 << 27) | (z3 << 9);
+        const unsigned long long x3 = (unsigned)((ix >> 4) + (1 << 16)), y3 = (unsigned)((iy >> 4) + (1 << 16)),
+                                 z3 = (unsigned)((iz >> 4) + (1 << 16));
+        k = (x3 << 46) | (y3 << 29) | (z3 << 12);
 #pragma unroll
-        for (int L = 2; L >= 0; --L) {
-            const unsigned cbits = (unsigned)((((ix >> L) & 1) << 2) | (((iy >> L) & 1) << 1) | ((iz >> L) & 1));
-            k |= (unsigned long long)cbits << (3 * L);
+        for (int m = 3; m >= 1; --m) {  // the child bits of levels 2, 1, 0, -1 (cells c0/2 >> m)
+            const unsigned cbits = (unsigned)((((ix >> m) & 1) << 2) | (((iy >> m) & 1) << 1) | ((iz >> m) & 1));
+            k |= (unsigned long long)cbits << (3 * m);
         }
+        k |= (unsigned long long)(((ix & 1) << 2) | ((iy & 1) << 1) | (iz & 1));
     }
     keys[i] = k;
     vals[i] = (unsigned)i;
 }
 
-// level-L cells: runs of equal key >> 3L; table entries keyed by the level's own cell_key
-__global__ void k_ladder_cells(const unsigned long long* __restrict__ keys, const unsigned int* __restrict__ vals,
-                               const float4* __restrict__ pts4, int n, int L, float c0,
-                               CellEntry* __restrict__ table, unsigned int mask, float4* __restrict__ spts,
-                               int write_spts) {
+// the levels' hash tables of one ladder build, cleared and filled in one launch
+// each: entries 0..3 = levels 0..3 (cells c0 .. 8 c0), entry 4 = the finest level (c0 / 2)
+#define GRID_LEVELS 5
+struct Tables4 {
+    CellEntry* t[GRID_LEVELS];
+    unsigned int mask[GRID_LEVELS];
+    unsigned int H[GRID_LEVELS];
+};
+// a level's cell in the ladder's finest cells (c0 / 2) and its prefix shift in the key
+__device__ __forceinline__ int level_shift(int L) { return L == 4 ? 0 : L + 1; }
+
+__global__ void k_grid_clear4(Tables4 T, unsigned level_mask) {
+    const unsigned int i = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int L = 0; L < GRID_LEVELS; ++L)
+        if (((level_mask >> L) & 1u) && i < T.H[L]) {
+            T.t[L][i].key = BS_EMPTY_KEY;
+            T.t[L][i].start = 0;
+            T.t[L][i].count = 0;
+        }
+}
+
+// the cells of every level in level_mask at once, and the points in key order
+__global__ void k_ladder_cells4(const unsigned long long* __restrict__ keys, const unsigned int* __restrict__ vals,
+                                const float4* __restrict__ pts4, int n, float c0, Tables4 T, unsigned level_mask,
+                                float4* __restrict__ spts) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const float4 p = pts4[vals[j]];
-    if (write_spts) spts[j] = p;
+    spts[j] = p;
     const unsigned long long k = keys[j];
-    if (k == BS_EMPTY_KEY || L < 0) return;  // L < 0: scatter only
-    const unsigned long long pk = k >> (3 * L);
-    if (j > 0 && (keys[j - 1] >> (3 * L)) == pk) return;
-    int lo = j + 1, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((keys[mid] >> (3 * L)) == pk) lo = mid + 1;
-        else hi = mid;
-    }
+    if (k == BS_EMPTY_KEY) return;
+    const unsigned long long km1 = j > 0 ? keys[j - 1] : BS_EMPTY_KEY;
     int ix, iy, iz;
     ladder_cells(p.x, p.y, p.z, c0, ix, iy, iz);
-    const unsigned long long ck = cell_key(ix >> L, iy >> L, iz >> L);
-    unsigned int h = hash_key(ck) & mask;
-    while (true) {
-        const unsigned long long prev = atomicCAS(&table[h].key, BS_EMPTY_KEY, ck);
-        if (prev == BS_EMPTY_KEY) break;
-        h = (h + 1) & mask;
+#pragma unroll
+    for (int L = 0; L < GRID_LEVELS; ++L) {
+        if (!((level_mask >> L) & 1u)) continue;
+        const int m = level_shift(L);
+        const unsigned long long pk = k >> (3 * m);
+        if (j > 0 && (km1 >> (3 * m)) == pk) continue;  // not the first of its run at this level
+        int lo = j + 1, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((keys[mid] >> (3 * m)) == pk) lo = mid + 1;
+            else hi = mid;
+        }
+        const unsigned long long ck = cell_key(ix >> m, iy >> m, iz >> m);
+        unsigned int h = hash_key(ck) & T.mask[L];
+        while (true) {
+            const unsigned long long prev = atomicCAS(&T.t[L][h].key, BS_EMPTY_KEY, ck);
+            if (prev == BS_EMPTY_KEY) break;
+            h = (h + 1) & T.mask[L];
+        }
+        T.t[L][h].start = (unsigned)j;
+        T.t[L][h].count = (unsigned)(lo - j);
     }
-    table[h].start = (unsigned)j;
-    table[h].count = (unsigned)(lo - j);
 }
 
 }  // namespace bsk
@@ -153,13 +183,23 @@ static unsigned int pow2_at_least(unsigned int x) {
 // g[0..3]: grids of cell c0, 2 c0, 4 c0, 8 c0 built from one 63-bit radix sort; g[0] owns the
 // sort buffers and the cell-sorted points, g[1..3] own only their hash tables and alias g[0].spts
 hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s,
-                             unsigned level_mask, int min_cap) {
+                             unsigned level_mask, int min_cap, DevGrid* finer) {
     hipError_t e;
     DevGrid& g0 = *gp[0];
     bool fresh = n > g0.cap || !g0.keys || g0.alias;
     for (int L = 1; L < 4; ++L) fresh = fresh || !gp[L]->alias || gp[L]->spts != g0.spts || !gp[L]->table;
+    if (finer && !fresh && (!finer->alias || finer->spts != g0.spts || !finer->table || finer->cap != g0.cap)) {
+        // the finest level joins an existing ladder: its own table, the ladder's points
+        grid_free(*finer, true);
+        finer->cap = g0.cap;
+        finer->H = pow2_at_least(2u * (unsigned)g0.cap);
+        if ((e = hipMalloc(&finer->table, sizeof(CellEntry) * finer->H))) return e;
+        finer->spts = g0.spts;
+        finer->alias = true;
+    }
     if (fresh) {
         for (int L = 0; L < 4; ++L) grid_free(*gp[L], true);
+        if (finer) grid_free(*finer, true);
         g0.cap = std::max(n + n / 4 + 1024, min_cap);
         note_regrow("ladder grids", (size_t)g0.cap * 48);
         if ((e = hipMalloc(&g0.keys, sizeof(unsigned long long) * g0.cap))) return e;
@@ -183,27 +223,42 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
                 gl.alias = true;
             }
         }
+        if (finer) {
+            finer->cap = g0.cap;
+            finer->H = pow2_at_least(2u * (unsigned)g0.cap);
+            if ((e = hipMalloc(&finer->table, sizeof(CellEntry) * finer->H))) return e;
+            finer->spts = g0.spts;
+            finer->alias = true;
+        }
     }
     const int B = 256;
     bsk::k_ladder_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, c0, g0.keys, g0.vals, d_pts4);
     size_t tb = g0.tmp_bytes;
     if ((e = rocprim::radix_sort_pairs(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 63, s)))
         return e;
-    for (int L = 0; L < 4; ++L) {
-        DevGrid& gl = *gp[L];
-        gl.n = n;
-        gl.cell = c0 * (float)(1 << L);
-        // level 0 always scatters the sorted points (the other levels alias them)
-        if (L > 0 && !((level_mask >> L) & 1u)) continue;
-        if (L == 0 && !(level_mask & 1u)) {
-            bsk::k_ladder_cells<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, -1, c0, gl.table, gl.H - 1,
-                                                              g0.spts, 1);
+    // the levels' tables: one clear and one fill launch for all of them (the sorted points are
+    // always scattered: the other levels alias them)
+    bsk::Tables4 T;
+    unsigned int hmax = 0;
+    level_mask &= 0xFu;
+    for (int L = 0; L < 5; ++L) {
+        DevGrid* gl = L < 4 ? gp[L] : finer;
+        if (!gl) {
+            T.t[L] = nullptr;
+            T.mask[L] = 0;
+            T.H[L] = 0;
             continue;
         }
-        bsk::k_grid_clear<<<(gl.H + B - 1) / B, B, 0, s>>>(gl.table, gl.H);
-        bsk::k_ladder_cells<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, L, c0, gl.table, gl.H - 1,
-                                                          g0.spts, L == 0);
+        gl->n = n;
+        gl->cell = L < 4 ? c0 * (float)(1 << L) : c0 * 0.5f;
+        T.t[L] = gl->table;
+        T.mask[L] = gl->H - 1;
+        T.H[L] = gl->H;
+        if (L == 4) level_mask |= 1u << 4;
+        if ((level_mask >> L) & 1u) hmax = std::max(hmax, gl->H);
     }
+    if (hmax) bsk::k_grid_clear4<<<(hmax + B - 1) / B, B, 0, s>>>(T, level_mask);
+    bsk::k_ladder_cells4<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, c0, T, level_mask, g0.spts);
     return hipGetLastError();
 }
 

@@ -170,10 +170,12 @@ __device__ __forceinline__ void icp_put_flag(int* p, int v) {
 #ifndef ICP_WAVES
 #define ICP_WAVES 4
 #endif
-// per-source Umeyama record of an iteration, SoA rows of ns floats in rec: source xyz (the source's
-// current position), its NN target xyz, the NN's d2
+// per-source Umeyama record of an iteration, SoA rows in rec (row stride icp_rs(ns): 16-B aligned
+// rows): source xyz (the source's current position), its NN target xyz, the NN's d2
+__host__ __device__ __forceinline__ int icp_rs(int ns) { return (ns + 3) & ~3; }
 __device__ __forceinline__ void icp_put_rec(float* rec, int ns, int i, float qx, float qy, float qz, float4 t,
                                             unsigned long long m) {
+    ns = icp_rs(ns);
     rec[i] = qx;
     rec[(size_t)ns + i] = qy;
     rec[2 * (size_t)ns + i] = qz;
@@ -266,7 +268,7 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
                                                                  const float4* __restrict__ lcen, int cap, IcpGrids G,
                                                                  const float4* __restrict__ tgt4, int nt, int max_iter,
                                                                  const bsh::IcpSync* sy, int* done,
-                                                                 unsigned long long* best) {
+                                                                 unsigned long long* best, int* qstat) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     __shared__ CandLds cl;
     __shared__ float4 q_queue[ICPH_THREADS];
@@ -356,6 +358,10 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
         }
         __builtin_amdgcn_wave_barrier();
         const int nqueued = nq;
+        if (qstat && lane == 0 && nqueued) {  // instrumentation (bshot_work_counters 9, 10): grid searches
+            atomicAdd(&qstat[0], nqueued);
+            atomicMax(&qstat[1], nqueued);
+        }
         for (int t = 0; t < nqueued; ++t) {
             // the exact grid search, then a new list around the current position (its owner lane
             // takes over the new centre, count and radius below), so a source that outgrew its list
@@ -427,19 +433,19 @@ __device__ __forceinline__ float chain_sum_f(const float* a, int k0, int n, floa
 __device__ __forceinline__ float chain_dot_f(const float* e, const float* f, int k0, int n, float acc) {
     int k = k0;
     for (; k < n && (k & 3); ++k) acc = acc + e[k] * f[k];
-    while (k + 32 <= n) {
-        float4 u[8], v[8];
+    while (k + 16 <= n) {
+        float4 u[4], v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
             u[j] = *reinterpret_cast<const float4*>(e + k + 4 * j);
             v[j] = *reinterpret_cast<const float4*>(f + k + 4 * j);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
             const float p0 = u[j].x * v[j].x, p1 = u[j].y * v[j].y, p2 = u[j].z * v[j].z, p3 = u[j].w * v[j].w;
             acc = acc + p0; acc = acc + p1; acc = acc + p2; acc = acc + p3;
         }
-        k += 32;
+        k += 16;
     }
     for (; k + 4 <= n; k += 4) {
         const float4 u = *reinterpret_cast<const float4*>(e + k);
@@ -472,11 +478,19 @@ __device__ __forceinline__ double chain_sum_d(const float* a, int k0, int n, dou
     return acc;
 }
 
-#define ICPR_THREADS 256
+// 4 waves per workgroup (256 sources), up to 2048 records staged in LDS at once. A one-wave form
+// with 256-record chunks (~10 KB of LDS, 128 VGPRs, so that its workgroups fit beside SR's) was
+// slower in the pipeline: 1.34 vs 1.11 ms per ICP call (profiles/r05d_icp_ab.txt) -- the step's
+// sequential chains then share one wave (PCL's MSE chain after the covariance instead of beside it)
+#ifndef ICPR_WAVES
 #define ICPR_WAVES 4
+#endif
+#define ICPR_THREADS (64 * ICPR_WAVES)
 #ifndef ICPR_CH
 #define ICPR_CH 2048  // records staged in LDS at once by the stepping workgroup (7 floats each)
 #endif
+// PCL's MSE chain: wave 1's lane 0 beside wave 0's covariance lanes, or lane 9 of a lone wave
+#define ICPR_MSE_LANE(wave, lane) (ICPR_WAVES > 1 ? ((wave) == 1 && (lane) == 0) : ((lane) == 9))
 
 __device__ __forceinline__ void st_dev(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ float ld_dev(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -487,6 +501,7 @@ __device__ __forceinline__ double ld_dev_d(const double* p) { return __hip_atomi
 
 __device__ __forceinline__ void icp_put_rec_dev(float* rec, int ns, int i, float qx, float qy, float qz, float4 t,
                                                 unsigned long long m) {
+    ns = icp_rs(ns);
     st_dev(rec + i, qx);
     st_dev(rec + (size_t)ns + i, qy);
     st_dev(rec + 2 * (size_t)ns + i, qz);
@@ -497,25 +512,50 @@ __device__ __forceinline__ void icp_put_rec_dev(float* rec, int ns, int i, float
 }
 
 // the step of one iteration by the whole (last-arriving) workgroup: Umeyama of the records, the
-// composed transform and PCL's convergence test into ctl; a stop writes out
+// composed transform and PCL's convergence test into ctl; a stop writes out.
+// The records are staged in LDS chunk by chunk: every thread issues its share of the chunk's
+// coherent (agent-scope) loads at once into registers, and the next chunk's are in flight while the
+// current chunk's chains run (a load-then-store loop waited for each load: ~56 serialised L2 round
+// trips per step).
 __device__ __forceinline__ void icp_step(int ns, const float* rec, int max_iter, bsh::IcpCtl* ctl, bsh::IcpOut* out,
                                          int seq, float* srec, float* smean, float* sacc, double* smse) {
     const int tid = threadIdx.x, lane = lane_id();
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool big = ns > ICPR_CH;
     const int chs = big ? ICPR_CH : ((ns + 3) & ~3);  // LDS row stride (16-B aligned rows)
+    const int rs = icp_rs(ns);
     const float one_over_n = 1.f / (float)ns;
-    auto stage = [&](int c0, int cn) {
+    static_assert(ICPR_CH % (4 * ICPR_THREADS) == 0, "a chunk row is whole float4s, one per thread");
+    constexpr int PF = ICPR_CH / (4 * ICPR_THREADS);  // float4s per thread per row
+    float4 nx[7][PF];
+    auto fetch = [&](int c0) {  // rows [c0, c0 + chs) -> registers (a row tail past rs is never read)
+#pragma unroll
         for (int c = 0; c < 7; ++c)
-            for (int k = tid; k < cn; k += ICPR_THREADS) srec[c * chs + k] = ld_dev(rec + (size_t)c * ns + c0 + k);
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int k = 4 * (tid + u * ICPR_THREADS);
+                const float* r = rec + (size_t)c * rs + (c0 + k < rs ? c0 + k : 0);
+                nx[c][u] = make_float4(ld_dev(r), ld_dev(r + 1), ld_dev(r + 2), ld_dev(r + 3));
+            }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int c = 0; c < 7; ++c)
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int k = 4 * (tid + u * ICPR_THREADS);
+                if (k < chs) *reinterpret_cast<float4*>(srec + c * chs + k) = nx[c][u];
+            }
     };
     // ---- means: lanes 0..5 of wave 0, source order (the first element starts the sum)
     float acc = 0.f;
+    fetch(0);
     for (int c0 = 0; c0 < ns; c0 += chs) {
         const int cn = ns - c0 < chs ? ns - c0 : chs;
-        if (c0 > 0) __syncthreads();
-        stage(c0, cn);
+        __syncthreads();  // the previous chunk's chains are done with srec
+        put();
         __syncthreads();
+        if (c0 + chs < ns) fetch(c0 + chs);  // in flight during this chunk's chains
         if (wave == 0 && lane < 6) {
             const float* a = srec + lane * chs;
             if (c0 == 0) acc = chain_sum_f(a, 1, cn, a[0]);
@@ -523,8 +563,9 @@ __device__ __forceinline__ void icp_step(int ns, const float* rec, int max_iter,
         }
     }
     if (wave == 0 && lane < 6) smean[lane] = acc * one_over_n;
+    if (big) fetch(0);
     __syncthreads();
-    // ---- cross-covariance (wave 0, lane r * 3 + c) and PCL's MSE (wave 1, lane 0)
+    // ---- cross-covariance (wave 0, lane r * 3 + c) and PCL's MSE
     const float sm0 = smean[0], sm1 = smean[1], sm2 = smean[2], dm0 = smean[3], dm1 = smean[4], dm2 = smean[5];
     float cov = 0.f;
     double mse = 0.0;
@@ -532,8 +573,9 @@ __device__ __forceinline__ void icp_step(int ns, const float* rec, int max_iter,
         const int cn = ns - c0 < chs ? ns - c0 : chs;
         if (big) {
             __syncthreads();
-            stage(c0, cn);
+            put();
             __syncthreads();
+            if (c0 + chs < ns) fetch(c0 + chs);
         }
         // centre in place: s - sm, d - dm (the host's s0..s2, d0..d2)
         for (int t = tid; t < 6 * cn; t += ICPR_THREADS) {
@@ -547,12 +589,12 @@ __device__ __forceinline__ void icp_step(int ns, const float* rec, int max_iter,
             const float* f = srec + (lane % 3) * chs;      // s_c - sm_c
             if (c0 == 0) cov = chain_dot_f(e, f, 1, cn, e[0] * f[0]);
             else cov = chain_dot_f(e, f, 0, cn, cov);
-        } else if (wave == 1 && lane == 0) {
+        } else if (ICPR_MSE_LANE(wave, lane)) {
             mse = chain_sum_d(srec + 6 * chs, 0, cn, mse);
         }
     }
     if (wave == 0 && lane < 9) sacc[lane] = cov;
-    if (wave == 1 && lane == 0) *smse = mse;
+    if (ICPR_MSE_LANE(wave, lane)) *smse = mse;
     __syncthreads();
     // ---- the step, PCL's convergence test (the host loop's order: the step is composed first, then
     // max_iter, the transformation epsilon, the MSE epsilon)
@@ -599,7 +641,15 @@ __device__ __forceinline__ void icp_step(int ns, const float* rec, int max_iter,
 }
 
 // sync[0]: arrivals (nb per iteration), sync[1]: the last released iteration (zeroed by k_icp_lists)
-__global__ void __launch_bounds__(ICPR_THREADS) k_icp_run(int ns, float4* lst, float* lsd, int* lcnt,
+#ifndef ICPR_WPE
+#define ICPR_WPE 0  // no cap (a cap of 128 VGPRs spills)
+#endif
+#if ICPR_WPE > 0
+#define ICPR_ATTR __attribute__((amdgpu_waves_per_eu(ICPR_WPE)))
+#else
+#define ICPR_ATTR
+#endif
+__global__ void __launch_bounds__(ICPR_THREADS) ICPR_ATTR k_icp_run(int ns, float4* lst, float* lsd, int* lcnt,
                                                           float4* __restrict__ lcen, float4* __restrict__ pos, int cap,
                                                           IcpGrids G, const float4* __restrict__ tgt4, int nt, float* rec,
                                                           int max_iter, bsh::IcpCtl* ctl, unsigned int* sync,
@@ -735,6 +785,18 @@ __global__ void k_gather(const float4* __restrict__ pts4, const int* __restrict_
     }
 }
 
+// the same with the indices read straight from the caller's pinned staging and the coordinates also
+// written to pinned staging (hout, nullable): one launch instead of copy + gather + copy
+__global__ void k_gather_io(const float4* __restrict__ pts4, const int* __restrict__ h_idx, int k,
+                            float* __restrict__ out, float* __restrict__ hout) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) {
+        const float4 p = pts4[h_idx[i]];
+        out[3 * i] = p.x; out[3 * i + 1] = p.y; out[3 * i + 2] = p.z;
+        if (hout) { hout[3 * i] = p.x; hout[3 * i + 1] = p.y; hout[3 * i + 2] = p.z; }
+    }
+}
+
 }  // namespace bsk
 
 namespace bsh {
@@ -748,6 +810,12 @@ hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t 
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     bsk::k_gather<<<(k + 255) / 256, 256, 0, s>>>(pts4, idx, k, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_io(const float4* pts4, const int* h_idx, int k, float* out, float* hout, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    bsk::k_gather_io<<<(k + 255) / 256, 256, 0, s>>>(pts4, h_idx, k, out, hout);
     return hipGetLastError();
 }
 
@@ -792,11 +860,12 @@ hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const
 
 hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4* lst, const float* lsd, const int* lcnt,
                                  const float4* lcen, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
-                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s) {
+                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s,
+                                 int* qstat) {
     if (ns <= 0 || nt <= 0 || max_iter <= j0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
     bsk::k_icp_iterations<<<icp_iter_blocks(ns), ICPH_THREADS, 0, s>>>(src0, ns, j0, lst, lsd, lcnt, lcen, cap, icp_views(g4),
-                                                                      tgt4, nt, max_iter, sy, done, best);
+                                                                      tgt4, nt, max_iter, sy, done, best, qstat);
     return hipGetLastError();
 }
 

@@ -301,25 +301,31 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
             for (; j < ct; ++j) take(g.spts[st + j]);
             return cnt <= ISS_LCAP;
         };
-        if (x1 - x0 <= 1 && y1 - y0 <= 1 && z1 - z0 <= 1) {
-            // cell >= 2 x radius: at most 2 x 2 x 2 cells; first probes of all 8 issued together
-            unsigned long long ck[8];
-            CellEntry e[8];
+        const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+        if (nx <= 3 && ny <= 3 && nz <= 3) {
+            // cell >= radius: at most 3 x 3 x 3 cells, visited 8 at a time with the first probes of
+            // the 8 issued together (one batch when the cell is >= 2 x radius)
+            const int ncell = nx * ny * nz;
+            bool go = true;
+            for (int b0 = 0; go && b0 < ncell; b0 += 8) {
+                unsigned long long ck[8];
+                CellEntry e[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int ix = x0 + (u >> 2), iy = y0 + ((u >> 1) & 1), iz = z0 + (u & 1);
-                ck[u] = (ix <= x1 && iy <= y1 && iz <= z1) ? cell_key(ix, iy, iz) : BS_EMPTY_KEY;
-            }
+                for (int u = 0; u < 8; ++u) {
+                    const int v = b0 + u, iz = z0 + v % nz, r = v / nz, iy = y0 + r % ny, ix = x0 + r / ny;
+                    ck[u] = v < ncell ? cell_key(ix, iy, iz) : BS_EMPTY_KEY;
+                }
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (ck[u] != BS_EMPTY_KEY) e[u] = g.table[hash_key(ck[u]) & g.mask];
+                for (int u = 0; u < 8; ++u)
+                    if (ck[u] != BS_EMPTY_KEY) e[u] = g.table[hash_key(ck[u]) & g.mask];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (ck[u] == BS_EMPTY_KEY) continue;
-                unsigned int st = 0, ct = 0;
-                if (e[u].key == ck[u]) { st = e[u].start; ct = e[u].count; }
-                else if (e[u].key != BS_EMPTY_KEY && !grid_lookup(g, ck[u], st, ct)) ct = 0;
-                if (ct && !scan_cell(st, ct)) break;
+                for (int u = 0; u < 8; ++u) {
+                    if (ck[u] == BS_EMPTY_KEY) continue;
+                    unsigned int st = 0, ct = 0;
+                    if (e[u].key == ck[u]) { st = e[u].start; ct = e[u].count; }
+                    else if (e[u].key != BS_EMPTY_KEY && !grid_lookup(g, ck[u], st, ct)) ct = 0;
+                    if (ct && !scan_cell(st, ct)) { go = false; break; }
+                }
             }
         } else {
             bool go = true;

@@ -10,6 +10,8 @@
 // synchronised with the stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace bsk {
@@ -52,6 +54,36 @@ __global__ void __launch_bounds__(KC_THREADS) k_fill1(unsigned char* __restrict_
     for (size_t i = (size_t)blockIdx.x * KC_THREADS + threadIdx.x; i < n; i += stride) dst[i] = b;
 }
 
+// up to KC_JOBS copies in one launch (blockIdx.y = the copy), each with its own alignment path
+#define KC_JOBS 4
+struct CopyJob {
+    unsigned char* d;
+    const unsigned char* s;
+    size_t bytes;
+    int align;  // 16, 4 or 1: the widest unit both pointers are aligned to
+};
+struct CopyJobs {
+    CopyJob j[KC_JOBS];
+};
+
+__global__ void __launch_bounds__(KC_THREADS) k_copy_multi(CopyJobs J) {
+    const CopyJob& jb = J.j[blockIdx.y];
+    const size_t stride = (size_t)gridDim.x * KC_THREADS;
+    const size_t t0 = (size_t)blockIdx.x * KC_THREADS + threadIdx.x;
+    size_t body = 0;
+    if (jb.align == 16) {
+        const size_t n = jb.bytes / 16;
+        for (size_t i = t0; i < n; i += stride) reinterpret_cast<uint4*>(jb.d)[i] = reinterpret_cast<const uint4*>(jb.s)[i];
+        body = 16 * n;
+    } else if (jb.align == 4) {
+        const size_t n = jb.bytes / 4;
+        for (size_t i = t0; i < n; i += stride)
+            reinterpret_cast<unsigned int*>(jb.d)[i] = reinterpret_cast<const unsigned int*>(jb.s)[i];
+        body = 4 * n;
+    }
+    for (size_t i = body + t0; i < jb.bytes; i += stride) jb.d[i] = jb.s[i];
+}
+
 }  // namespace bsk
 
 namespace bsh {
@@ -83,6 +115,38 @@ hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s, int ma
         bsk::k_copy1<<<kc_blocks(bytes, max_blocks), KC_THREADS, 0, s>>>(d, p, bytes);
     }
     return hipGetLastError();
+}
+
+hipError_t kcopy_n(int n, void* const* dst, const void* const* src, const size_t* bytes, hipStream_t s) {
+    bsk::CopyJobs J;
+    int m = 0;
+    size_t units = 0;
+    for (int i = 0; i < n; ++i) {
+        if (bytes[i] == 0 || dst[i] == src[i]) continue;
+        if (!dst[i] || !src[i]) return hipErrorInvalidValue;
+        if (m == KC_JOBS) {  // more copies than one launch takes: the rest in further launches
+            if (hipError_t e = kcopy_n(n - i, dst + i, src + i, bytes + i, s)) return e;
+            break;
+        }
+        const uintptr_t a = (uintptr_t)dst[i] | (uintptr_t)src[i];
+        bsk::CopyJob& jb = J.j[m++];
+        jb.d = static_cast<unsigned char*>(dst[i]);
+        jb.s = static_cast<const unsigned char*>(src[i]);
+        jb.bytes = bytes[i];
+        jb.align = (a & 15) == 0 ? 16 : ((a & 3) == 0 ? 4 : 1);
+        units = std::max(units, bytes[i] / (size_t)jb.align);
+    }
+    if (m == 0) return hipSuccess;
+    if (m == 1) return kcopy(J.j[0].d, J.j[0].s, J.j[0].bytes, s);
+    bsk::k_copy_multi<<<dim3(kc_blocks(units), m), KC_THREADS, 0, s>>>(J);
+    return hipGetLastError();
+}
+
+hipError_t kcopy2(void* d0, const void* s0, size_t b0, void* d1, const void* s1, size_t b1, hipStream_t s) {
+    void* d[2] = {d0, d1};
+    const void* src[2] = {s0, s1};
+    const size_t b[2] = {b0, b1};
+    return kcopy_n(2, d, src, b, s);
 }
 
 hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s) {

@@ -11,6 +11,9 @@ namespace bsh {
 // max_blocks: grid cap (a bulk copy that reads host memory holds its CUs for the transfer's
 // duration; a small grid leaves the rest to the concurrent kernels)
 hipError_t kcopy(void* dst, const void* src, size_t bytes, hipStream_t s, int max_blocks = 0);
+// n copies in one launch where possible (up to 4 per launch; an empty or self copy is skipped)
+hipError_t kcopy_n(int n, void* const* dst, const void* const* src, const size_t* bytes, hipStream_t s);
+hipError_t kcopy2(void* d0, const void* s0, size_t b0, void* d1, const void* s1, size_t b1, hipStream_t s);
 hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s);
 
 // g4: the radius-ladder grids (cells r/16, r/8, r/4, r/2 for ladder modes 1, 2; r/8, r/8, r/2, r/2
@@ -49,13 +52,18 @@ hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, in
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
 hipError_t launch_gather(const float4* pts4, const int* idx, int k, float* out, hipStream_t s);
+// gather with the indices in pinned host memory (read by the kernel) and an optional pinned copy of
+// the coordinates (hout)
+hipError_t launch_gather_io(const float4* pts4, const int* h_idx, int k, float* out, float* hout, hipStream_t s);
 // A11 ICP nearest neighbours on the targets' nested grids g4 (cells 1000, 2000, 4000, 8000 mm, all
 // hashed) and float4 targets tgt4 (index order). Iteration 0: the exact 1-NN keys of src0 into
 // best_out, and per source a candidate list (cap float4 entries: target xyz + index bits, and their
 // distances from the list's centre, in ascending order; entry e of source i at [e * ns + i]), its
 // count (-1: none) and radius. Iteration >= 1: the sources moved by T16 (src_in -> src_out) and
 // their exact 1-NN keys; keys (d2 bits << 32 | index) land in best_out (pinned host memory).
+#ifndef ICP_LIST_CAP
 #define ICP_LIST_CAP 128
+#endif
 // the result of one ICP call (coherent pinned host memory): the composed transform, the iteration
 // count, then seq (written last, after the others have reached host memory)
 struct IcpOut {
@@ -84,7 +92,8 @@ hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const
 // 1-NN key in best[(j & 1) * ns + i] (pinned) and sets done[w] = j
 hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4* lst, const float* lsd, const int* lcnt,
                                  const float4* lcen, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
-                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s);
+                                 int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s,
+                                 int* qstat = nullptr);
 // the loop state of one ICP call (device memory): the last step, the composed transform, PCL's
 // previous MSE, the iteration count and the stop flag every queued kernel checks first
 struct IcpCtl {

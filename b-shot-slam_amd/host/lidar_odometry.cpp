@@ -332,10 +332,8 @@ void LidarOdometry::runAhead(Lookahead& la) {
         fail("alloc pinned");
     for (int attempt = 0; attempt < 3; ++attempt) {
         c->p_err.p[0] = 0;
-        if (k > 0 && (bsh::kcopy(c->p_bits.p, c->bits.p, sizeof(uint32_t) * 11 * k,
-                                     c->side) != hipSuccess ||
-                      bsh::kcopy(c->p_err.p, c->errw.p, 4 * sizeof(int), c->side) !=
-                          hipSuccess))
+        if (k > 0 && bsh::kcopy2(c->p_bits.p, c->bits.p, sizeof(uint32_t) * 11 * k, c->p_err.p, c->errw.p,
+                                 4 * sizeof(int), c->side) != hipSuccess)
             fail("D2H bits");
         if (hipStreamSynchronize(c->side) != hipSuccess) fail("lookahead sync");
         if (k > 0 && bsh::ctx_describe_replan(c, c->p_err.p)) {
@@ -456,10 +454,8 @@ void LidarOdometry::computeDescriptors() {
     for (int attempt = 0; attempt < 3; ++attempt) {
         ctx_->p_err.p[0] = 0;
         if (k > 0) {
-            if (bsh::kcopy(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k,
-                               ctx_->stream) != hipSuccess ||
-                bsh::kcopy(ctx_->p_err.p, ctx_->errw.p, 4 * sizeof(int), ctx_->stream) !=
-                    hipSuccess)
+            if (bsh::kcopy2(ctx_->p_bits.p, ctx_->bits.p, sizeof(uint32_t) * 11 * k, ctx_->p_err.p, ctx_->errw.p,
+                            4 * sizeof(int), ctx_->stream) != hipSuccess)
                 check(BSHOT_EHIP, "D2H bits");
         }
         check(bsh::ctx_sync_main(ctx_), "describe sync");

@@ -165,8 +165,8 @@ int ransac_impl(bshot_ctx* ctx, const float* src_xyz, int ns, const float* tgt_x
         std::memcpy(c->p_rhyp.p, spos.data(), sizeof(int) * 3 * nhyp);
         const int sg = c->stage_begin(BSHOT_STAGE_RANSAC);
         // kernel copies from / into the pinned staging buffers (csrc/kcopy.hip): no copy engine
-        if (bsh::kcopy(c->rpts.p, c->p_rpts.p, sizeof(float) * np, c->stream) ||
-            bsh::kcopy(c->rhyp.p, c->p_rhyp.p, sizeof(int) * 3 * nhyp, c->stream) ||
+        if (bsh::kcopy2(c->rpts.p, c->p_rpts.p, sizeof(float) * np, c->rhyp.p, c->p_rhyp.p, sizeof(int) * 3 * nhyp,
+                        c->stream) ||
             bsh::launch_ransac_score(c->rpts.p, c->rpts.p + 3 * nidx, nidx, c->rhyp.p, nhyp, thr2, c->rcnt.p,
                                      c->stream) ||
             bsh::kcopy(c->p_rcnt.p, c->rcnt.p, sizeof(int) * nhyp, c->stream))

@@ -402,8 +402,8 @@ def main():
     wc_main = None
     if os.environ.get("BENCH_INTERVALS"):
         import ctypes
-        wc = (ctypes.c_int64 * 8)()
-        bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 8)
+        wc = (ctypes.c_int64 * 12)()
+        bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 12)
         wc_main = list(wc)
     if xchg is not None:
         xchg.close()

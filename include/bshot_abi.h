@@ -342,7 +342,9 @@ void bshot_set_timing(bshot_ctx* c, int enabled);
  * host plan after the device plan ran out of capacity (cumulative); ICP, cumulative: [2] ns the host
  * waited for nearest neighbours (or, option icp_device, for the device loop's result), [3] restarts
  * of the iterations after their kernel outwaited a stalled host, [4] ns of host work between two
- * waits, [5] iterations; [6] / [7] pool regrowths (count / bytes) */
+ * waits, [5] iterations; [6] / [7] pool regrowths (count / bytes); ICP host loop: [8] ns of [2] spent
+ * waiting for the lists kernel (iteration 0 or a restart), [9] grid searches after iteration 0 (sources
+ * that left their candidate lists), [10] the most one wave took in one iteration. Returns the count (12). */
 int bshot_work_counters(bshot_ctx* c, int64_t* out, int n);
 /* instrumentation (outside timed regions): sum over all points of the current cloud of
  * |B(p, R)| (strict d2 < R^2, self included) -> the P_sr / P_iss work figures of SURVEY.md §8(d). */
