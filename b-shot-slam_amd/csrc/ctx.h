@@ -147,6 +147,7 @@ struct bshot_ctx {
     int hf_pack_ok = 0;         // that check's result for this context's device (bshot_create)
     int opt_rank_max = -1;      // k_shot_rank_wg's in-place threshold (-1: RK_RANKMAX; 0: every span sorted)
     int opt_rank_wg = 2;        // SHOT rank kernel: 0 wave per 64-rank chunk, 1 workgroup per keypoint, 2 by neighbourhood size
+    int opt_desc_slices = 1;    // the histogram / rank_wg kernels in this many launches (LPT slices)
     int opt_sr_start = 80;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_grid = 1;       // ISS on the SR ladder's points: its fifth level, cells r/32 (0: own grid)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)

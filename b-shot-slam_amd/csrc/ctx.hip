@@ -517,6 +517,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         A.bstart = c->sbst.p;
         A.max_blocks = c->opt_chunk_blocks > 0 ? c->opt_chunk_blocks : 8192;  // chunk kernels grid-stride to cb[k]
         A.rank_wg = rank_wg_for(c, k, c->seg_hint);
+        A.slices = c->opt_desc_slices;
         A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
         A.cinfo = seg_cap < 0x7FFFFFFFll ? c->cinfo.p : nullptr;
         A.rank_max = c->opt_rank_max;
@@ -588,6 +589,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     A.bstart = c->sbst.p;
     A.max_blocks = c->opt_chunk_blocks;
     A.rank_wg = rank_wg_for(c, k, total);
+    A.slices = c->opt_desc_slices;
     A.hf_pack = c->opt_hist_pack && c->hf_pack_ok;
     A.rank_max = c->opt_rank_max;
     A.cinfo = total < 0x7FFFFFFFll ? c->cinfo.p : nullptr;
@@ -1277,6 +1279,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "rank_max") c->opt_rank_max = value;
     else if (k == "hist_pack") c->opt_hist_pack = value ? 1 : 0;
     else if (k == "rank_wg") c->opt_rank_wg = value < 0 ? 0 : (value > 2 ? 2 : value);
+    else if (k == "desc_slices") c->opt_desc_slices = value < 1 ? 1 : (value > 64 ? 64 : value);
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "xchg_index") c->opt_xchg_index = value ? 1 : 0;

@@ -18,6 +18,8 @@
 // ceil(n_q / 64) (k_desc_plan, or the host plan after an overflow).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "bshot_math.h"
 #include "dev_common.h"
 #include "kernels.h"
@@ -845,7 +847,13 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
         if (A.n_chunks > 0) {
             bsk::k_chunk_owner<<<A.k, 256, 0, s>>>(A.k, A.cb, A.owner, A.offs, A.cinfo);
             if (A.rank_wg) {
-                if ((e = launch_shot_rank_wg(A.k, A.R, A.perm, A.offs, A.bstart, A.seg, A.sorted, s, A.rank_max))) return e;
+                // slices (option desc_slices): consecutive ranges of the LPT order, each launch shorter, so
+                // the main stream's small grids find CUs between them; results do not depend on it
+                const int step = (A.k + A.slices - 1) / (A.slices > 0 ? A.slices : 1);
+                for (int s0 = 0; s0 < A.k; s0 += step)
+                    if ((e = launch_shot_rank_wg(std::min(step, A.k - s0), A.R, A.perm + s0, A.offs, A.bstart, A.seg, A.sorted, s,
+                                                 A.rank_max)))
+                        return e;
             } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s, A.cinfo,
                                              A.max_blocks))) {
                 return e;
@@ -872,12 +880,16 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
         bsk::k_hist_fused<HF_NW, HF_PACK><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
                                                                A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
 #endif
-    if (A.hf_pack)
-        bsk::k_hist_fused<HF_NW, HF_PACK><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
-                                                               A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
-    else
-        bsk::k_hist_fused<HF_NW, 0><<<A.k, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, A.k, A.R, A.perm, A.offs, A.cb,
-                                                         A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
+    const int step = (A.k + A.slices - 1) / (A.slices > 0 ? A.slices : 1);
+    for (int s0 = 0; s0 < A.k; s0 += step) {
+        const int m = std::min(step, A.k - s0);
+        if (A.hf_pack)
+            bsk::k_hist_fused<HF_NW, HF_PACK><<<m, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, m, A.R, A.perm + s0, A.offs,
+                                                                   A.cb, A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
+        else
+            bsk::k_hist_fused<HF_NW, 0><<<m, 64 * HF_NW, 0, s>>>(A.pts4, A.normals, A.kps, m, A.R, A.perm + s0, A.offs, A.cb,
+                                                             A.sorted, A.eig, A.okf, A.rf, A.ok, A.shot, A.bits);
+    }
     return hipGetLastError();
 }
 

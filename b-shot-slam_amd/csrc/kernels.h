@@ -140,6 +140,7 @@ struct Describe2Args {
     int rank_wg = 0;     // 1: k_shot_rank_wg (workgroup per keypoint, large neighbourhoods); 0: k_shot_rank
     int rank_max = -1;   // k_shot_rank_wg: spans whose buckets all hold <= this many keys rank in place (-1: default)
     int hf_pack = 1;     // 1: the SHOT apply packs several ranks per ds_add_f32 (needs lds_lane_order_check() == 0)
+    int slices = 1;      // the workgroup-per-keypoint kernels (histogram, rank_wg) in this many launches over perm
 };
 hipError_t launch_describe2(const Describe2Args& a, int part, hipStream_t s);
 // mismatches of same-address ds_add_f32 lanes against ascending lane order on the current device

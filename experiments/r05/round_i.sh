@@ -7,3 +7,9 @@ T=${1:-r05i}
 bash scripts/gpu_round.sh $T tests || exit 1
 bash scripts/gpu_config.sh ${T}_c3 --keypoints 600 --steps 1000 --warmup 20 --no-cpu-baseline || exit 1
 bash scripts/gpu_config.sh ${T}_c5 --sensor 1 --keypoints 4096 --shot-radius 5000 --steps 60 --warmup 10 --no-cpu-baseline
+# config 5: the histogram / rank_wg kernels in LPT slices (option desc_slices) vs one launch each
+O=$R/gpurun_out
+for i in 1 2; do for S in 1 4; do
+  timeout -k 10 300 python bench.py --sensor 1 --keypoints 4096 --shot-radius 5000 --steps 60 --warmup 10 --no-cpu-baseline --no-upload-leg --opt desc_slices=$S > $O/${T}_c5s$S.json 2> $O/${T}_c5s$S.err || exit 1
+  python3 -c "import json; d=json.load(open('$O/${T}_c5s$S.json')); print('desc_slices $S', $i, d['value'], d['ms_per_step_median'], d['host_ms_per_sweep'])" | tee -a $O/${T}_c5_slices.txt
+done; done

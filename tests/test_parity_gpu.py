@@ -350,12 +350,14 @@ def test_ransac_scores_kernel(ctx, nidx, nhyp):
     assert g.min() >= 0 and g.max() <= nidx
 
 
-@pytest.mark.parametrize("rank_wg,rank_max", [(0, -1), (1, -1), (1, 0), (1, 1 << 30)])
-def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg, rank_max):
+@pytest.mark.parametrize("rank_wg,rank_max,slices", [(0, -1, 1), (1, -1, 1), (1, 0, 1), (1, 1 << 30, 1), (1, -1, 3),
+                                                     (0, -1, 7)])
+def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg, rank_max, slices):
     """The two SHOT rank kernels (a wave per 64-rank chunk; a workgroup per keypoint staging
     whole-bucket spans in LDS, each span ranked in place or bitonic-sorted: rank_max 0 sorts every
     span, 2^30 ranks every span in place) give the host-planned describe's bits and histograms
-    exactly, on the device plan and on the host plan."""
+    exactly, on the device plan and on the host plan; so do the histogram and rank_wg kernels
+    launched in LPT slices (option desc_slices)."""
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 2048)
     kps = cloud[kidx]
@@ -365,6 +367,7 @@ def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg, rank_max):
     ref_bits, ref_shot, _ = ctx.describe(kps)
     ctx.set_option("rank_wg", rank_wg)
     ctx.set_option("rank_max", rank_max)
+    ctx.set_option("desc_slices", slices)
     try:
         for hint in (0, 1 << 30):
             ctx.set_option("dev_plan_hint", hint)
@@ -374,6 +377,7 @@ def test_describe_rank_kernels_agree(ctx, cloud, sr_ref, rank_wg, rank_max):
     finally:
         ctx.set_option("rank_wg", 2)
         ctx.set_option("rank_max", -1)
+        ctx.set_option("desc_slices", 1)
 
 
 def test_lds_lane_order_check(ctx):
