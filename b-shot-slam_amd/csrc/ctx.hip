@@ -731,6 +731,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
         const DevGrid* g4[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
         HIPCHK(c->ilcen.ensure(ns), "alloc icp list centres");
         const float* d_src0 = c->p_src.p;
+        bool dev_done = false;
         if (c->opt_icp_device) {
             // PCL's loop on the device (csrc/icp.hip): k_icp_lists finds iteration 0's exact 1-NN and
             // every source's candidate list, then one persistent k_icp_run iterates (per iteration:
@@ -761,14 +762,21 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             }
             if (!seen) {
                 HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
-                if (__atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) != seq)
-                    return c->fail("icp: the loop kernel finished without its result", BSHOT_EHIP);
+                seen = __atomic_load_n(&out->seq, __ATOMIC_ACQUIRE) == seq;
             }
             c->work[2] += ns_now() - t_a;  // host wait for the device loop
-            std::memcpy(fin.m, out->T, sizeof(fin.m));
-            it = out->iters;
-            c->work[5] += it;
-        } else {
+            if (seen) {
+                std::memcpy(fin.m, out->T, sizeof(fin.m));
+                it = out->iters;
+                c->work[5] += it;
+                dev_done = true;
+            } else {
+                // the grid-wide loop timed out (its workgroups were not all resident at once, ADVICE
+                // r04): the call runs the host loop below from the start instead of failing
+                ++c->work[3];
+            }
+        }
+        if (!dev_done) {
             // PCL's loop on the host (float Umeyama, convergence), the exact 1-NN of every iteration on
             // the device: one launch for iteration 0 (keys + every source's candidate list) and one
             // persistent launch for the rest, handed over through coherent pinned memory: the host

@@ -7,6 +7,8 @@
 //                  strictly larger third eigenvalue -> flag[i]
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "bshot_math.h"
 #include "dev_cand.h"
 #include "dev_common.h"
@@ -38,10 +40,15 @@ __device__ __forceinline__ double iss_third(const double* sm, double g21, double
 
 // wave/point fallback for the points whose neighbourhood overflowed the lane kernel's list:
 // ovf[0] = count, ovf[1..] = point indices
+// nml != null (nonmax <= salient): a point whose non-max neighbours (a prefix of its sorted list) number
+// at most 32 also gets its NMS list, as the lane kernel's points do (nmc >= 0: k_iss_nms_list
+// decides it; -1 leaves it to the wave NMS)
 __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, const float4* __restrict__ pts4,
                                                                 const int* __restrict__ ovf, float salient, int min_nn,
                                                                 double g21, double g32, double* __restrict__ third,
-                                                                int* __restrict__ err) {
+                                                                int* __restrict__ err, unsigned int r2nm_bits,
+                                                                unsigned int* __restrict__ nml, int* __restrict__ nmc,
+                                                                int n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     IssLds* L = reinterpret_cast<IssLds*>(smem) + wave;
@@ -81,6 +88,16 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
                 for (int i = cnt + lane; i < P; i += 64) L->list[i] = ~0ull;
                 __builtin_amdgcn_wave_barrier();
                 wave_bitonic(L->list, P);
+                if (nml) {
+                    // the non-max prefix of the sorted list: its length, then its indices when they fit
+                    int cnm = 0;
+                    for (int r = lane; r < cnt; r += 64)
+                        cnm += __popcll(__ballot((unsigned int)(L->list[r] >> 32) < r2nm_bits));
+                    if (cnm <= 32) {
+                        if (lane < cnm) nml[(size_t)lane * n + q] = (unsigned int)L->list[lane];
+                        if (lane == 0) nmc[q] = cnm;
+                    }
+                }
                 // neighbour offsets in double (neigh - central), rank order
                 const double cx = c.x, cy = c.y, cz = c.z;
                 const int half = ISS_CAP / 2;
@@ -135,6 +152,9 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
 #define ISS_LCAP 32
 #endif
 #define ISS_LBLOCK 64
+#ifndef ISS_SCAN
+#define ISS_SCAN 4  // points of a cell loaded at once by a lane (8: 108 VGPRs, the same sweeps/s, r05i)
+#endif
 #ifndef ISS_MERGE32
 #define ISS_MERGE32 1  // 0: the 32-key register network (A/B)
 #endif
@@ -290,16 +310,19 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
             }
         };
         // returns false once the lane overflowed (no need to look further)
+        // a cell's points ISS_SCAN at a time, every load issued together (the tail too: the index is
+        // clamped and the extra points skipped), one L2 round trip per group
         auto scan_cell = [&](unsigned int st, unsigned int ct) -> bool {
-            unsigned int j = 0;
-            for (; j + 4 <= ct; j += 4) {
-                const float4 p0 = g.spts[st + j], p1 = g.spts[st + j + 1], p2 = g.spts[st + j + 2],
-                             p3 = g.spts[st + j + 3];
-                take(p0); take(p1); take(p2); take(p3);
+            for (unsigned int j = 0; j < ct; j += ISS_SCAN) {
+                float4 p[ISS_SCAN];
+#pragma unroll
+                for (int u = 0; u < ISS_SCAN; ++u) p[u] = g.spts[st + (j + u < ct ? j + u : ct - 1)];
+#pragma unroll
+                for (int u = 0; u < ISS_SCAN; ++u)
+                    if (j + u < ct) take(p[u]);
                 if (cnt > ISS_LCAP) return false;
             }
-            for (; j < ct; ++j) take(g.spts[st + j]);
-            return cnt <= ISS_LCAP;
+            return true;
         };
         const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
         if (nx <= 3 && ny <= 3 && nz <= 3) {
@@ -399,13 +422,14 @@ __global__ void __launch_bounds__(256) k_iss_nms_list(int n, int min_nn, const d
 __global__ void __launch_bounds__(256) k_iss_nms_wave(GridView g, const float4* __restrict__ pts4, int n,
                                                       const int* __restrict__ ovf, int all, float nonmax, int min_nn,
                                                       const double* __restrict__ third,
-                                                      unsigned char* __restrict__ flag) {
+                                                      unsigned char* __restrict__ flag, const int* __restrict__ nmc) {
     const int lane = lane_id();
     const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     const int cnt_pts = all ? n : ovf[0];
     const float r2 = (float)((double)nonmax * (double)nonmax);
     for (int oi = wv; oi < cnt_pts; oi += nw) {
         const int q = all ? oi : ovf[1 + oi];
+        if (!all && nmc[q] >= 0) continue;  // decided from its list (k_iss_nms_list)
         const double tq = third[q];
         const float4 c = pts4[q];
         unsigned char f = 0;
@@ -461,14 +485,22 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
                                                                              g21, g32, third, ovf, nml, nmc);
     const size_t lds = sizeof(bsk::IssLds) * ISS_WAVES;
     // the overflow count is device-side: a fixed grid strides over it, idle waves exit at once
-    bsk::k_iss_scatter<<<ovf_blocks > 0 ? ovf_blocks : 4096, 64 * ISS_WAVES, lds, s>>>(g.view(), pts4, ovf, salient, min_nn, g21, g32, third, err);
+#ifndef ISS_OVF_NML
+#define ISS_OVF_NML 1  // 0: every overflow point through the wave NMS (A/B)
+#endif
+    const bool lists = ISS_OVF_NML && nonmax <= salient;
+    const float r2nm = (float)((double)nonmax * (double)nonmax);
+    unsigned int r2nm_bits;
+    std::memcpy(&r2nm_bits, &r2nm, sizeof r2nm_bits);
+    bsk::k_iss_scatter<<<ovf_blocks > 0 ? ovf_blocks : 4096, 64 * ISS_WAVES, lds, s>>>(
+        g.view(), pts4, ovf, salient, min_nn, g21, g32, third, err, r2nm_bits, lists ? nml : nullptr, nmc, n);
     if (nonmax <= salient) {
         // the non-max neighbours are a prefix of the lane kernel's sorted salient neighbours
         bsk::k_iss_nms_list<<<(n + 255) / 256, 256, 0, s>>>(n, min_nn, third, nml, nmc, flag);
         bsk::k_iss_nms_wave<<<nms_blocks > 0 ? nms_blocks : 1024, 256, 0, s>>>(g.view(), pts4, n, ovf, 0, nonmax, min_nn,
-                                                                               third, flag);
+                                                                               third, flag, nmc);
     } else {
-        bsk::k_iss_nms_wave<<<4096, 256, 0, s>>>(g.view(), pts4, n, ovf, 1, nonmax, min_nn, third, flag);
+        bsk::k_iss_nms_wave<<<4096, 256, 0, s>>>(g.view(), pts4, n, ovf, 1, nonmax, min_nn, third, flag, nmc);
     }
     return hipGetLastError();
 }

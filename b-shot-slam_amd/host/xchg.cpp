@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -89,6 +90,9 @@ struct bshot_xchg {
     hipEvent_t ev_inserted = nullptr;  // the replica inserts reading the log (or recv) are done (their stream)
     bool inserts_queued = false;
     bshot_ctx* jc = nullptr;  // the context whose replicas the log feeds
+    // the exchange call and a replica reader (quiesce, from another thread of the caller's) both index
+    // the log: mu guards the log and the insert queueing
+    std::mutex mu;
 };
 
 namespace {
@@ -143,6 +147,7 @@ int replay_log(bshot_ctx* c, bshot_xchg* x) {
 // exchange must not reach it any more (the log is dropped)
 int quiesce(void* arg, int detach) {
     auto* x = static_cast<bshot_xchg*>(arg);
+    std::lock_guard<std::mutex> lk(x->mu);
     if (detach) {
         x->log_entries.clear();
         x->jc = nullptr;
@@ -201,9 +206,12 @@ void bshot_xchg_destroy(bshot_xchg* x) {
     if (!x) return;
     // the context (still alive: its teardown would have detached it) must not call back into x; the
     // log's offers are indexed first, so its replicas stay complete
-    if (x->jc && x->jc->replica_quiesce_arg == x) {
-        (void)replay_log(x->jc, x);
-        x->jc->replica_quiesce = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(x->mu);
+        if (x->jc && x->jc->replica_quiesce_arg == x) {
+            (void)replay_log(x->jc, x);
+            x->jc->replica_quiesce = nullptr;
+        }
     }
     if (x->comm) rccl().destroy(x->comm);
     for (hipEvent_t* e : {&x->ev_inserted, &x->ev_rbuf[0], &x->ev_rbuf[1], &x->ev_gathered})
@@ -226,6 +234,7 @@ void bshot_xchg_destroy(bshot_xchg* x) {
 int bshot_odom_exchange_ctx(bshot_ctx* c, bshot_xchg* x, int include_self, int sim_peers) {
     if (!c || !x) return BSHOT_EINVAL;
     if (!c->gmap) return BSHOT_ESTATE;
+    std::lock_guard<std::mutex> lk(x->mu);
     if (x->jc && x->jc != c) return c->fail("exchange: already feeding another odometry's replicas", BSHOT_EINVAL);
     const size_t per = per_rank(x), img = per * x->nranks;
     c->hmark("M_x_begin");
