@@ -18,6 +18,9 @@
 namespace bsk {
 
 #define SG_BUCKETS 1024
+#ifndef SG_NT_STORE
+#define SG_NT_STORE 0  // 1: the gather's scattered key stores non-temporal (A/B of their write traffic)
+#endif
 
 // d2 bucket of the bucketed gather (k_shot_count/k_shot_gather_b/k_shot_rank): monotone in d2
 __device__ __forceinline__ int sg_bucket(float d2, float sc) {
@@ -195,7 +198,14 @@ __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, con
         __syncthreads();
         unsigned long long* out = seg + offs[q];
         for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
-            if (v) out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+            if (v) {
+                const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
+#if SG_NT_STORE
+                __builtin_nontemporal_store(key, &out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)]);
+#else
+                out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = key;
+#endif
+            }
         }, 0, wave, SG_WAVES);
         __syncthreads();  // cu and wsum are rewritten for the next keypoint
     }

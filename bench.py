@@ -405,6 +405,7 @@ def main():
         wc = (ctypes.c_int64 * 12)()
         bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc, 12)
         wc_main = list(wc)
+    used_xchg = xchg is not None  # the RCCL exchange ran in the timed region (its replica policy goes in the line)
     if xchg is not None:
         xchg.close()
         xchg = None
@@ -617,7 +618,7 @@ def main():
                         if a.sim_peers > 0 else "") +
                        ((" (replicas logged in HBM, indexed on read)" if a.xchg_lazy else
                          " (replicas indexed every sweep, inside the timed region)")
-                        if xchg is not None else "")},
+                        if used_xchg else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "upload_inclusive": upload_leg,
