@@ -167,7 +167,7 @@ struct bshot_ctx {
     DBuf<float> kps;
     DBuf<int> counts;
     DBuf<long long> offs;
-    DBuf<unsigned long long> seg;  // neighbour keys (d2 bits << 32 | idx), bucket-grouped (gather)
+    DBuf<unsigned int> seg;        // neighbour indices, bucket-grouped by d2 (gather)
     DBuf<unsigned int> segtmp;     // neighbour indices in (d2, idx) order (rank)
     DBuf<float> rf, shot;
     DBuf<int> ok;

@@ -5,7 +5,8 @@
 //   k_shot_count    workgroup/keypoint: |B(kp, R)| over the hashed grid + a 1024-bucket d2 histogram
 //   k_desc_plan     one workgroup: segment offsets, 64-rank chunk bases, LPT order, on the device
 //   k_excl_scan     one workgroup: segment offsets (host-planned describe after a plan overflow)
-//   k_shot_gather_b workgroup/keypoint: keys (d2 bits << 32 | idx) scattered bucket-grouped
+//   k_shot_gather_b workgroup/keypoint: neighbour indices scattered bucket-grouped (4 B each; the
+//                   rank kernels rebuild the (d2 bits << 32 | idx) keys from the points)
 //   k_shot_rank_wg  workgroup per keypoint: exact rank inside each bucket, span by span in LDS ->
 //                   FLANN's sorted order (k_shot_rank: the wave-per-64-rank-chunk variant)
 #include <hip/hip_runtime.h>
@@ -18,9 +19,14 @@
 namespace bsk {
 
 #define SG_BUCKETS 1024
-#ifndef SG_NT_STORE
-#define SG_NT_STORE 0  // 1: the gather's scattered key stores non-temporal (A/B of their write traffic)
-#endif
+
+// the gather's key of neighbour idx of the keypoint (kx, ky, kz): d2 by for_candidates' expression
+// and operands (pts4 holds the grid's coordinates), so the bits equal the ones the gather bucketed
+__device__ __forceinline__ unsigned long long sg_key(const float4* __restrict__ pts4, float kx, float ky, float kz,
+                                                     unsigned int idx) {
+    const float4 p = pts4[idx];
+    return ((unsigned long long)__float_as_uint(d2_flann(kx, ky, kz, p.x, p.y, p.z)) << 32) | idx;
+}
 
 // d2 bucket of the bucketed gather (k_shot_count/k_shot_gather_b/k_shot_rank): monotone in d2
 __device__ __forceinline__ int sg_bucket(float d2, float sc) {
@@ -155,13 +161,15 @@ __global__ void __launch_bounds__(1024) k_excl_scan(const int* __restrict__ coun
 // Bucketed gather: the keys land grouped by d2 bucket (buckets ascending, any order inside a
 // bucket): the workgroup scans its keypoint's bucket histogram (bh, from k_shot_count) into LDS
 // cursors, writes the bucket starts (bstart, relative to the segment) for k_shot_rank, and its 4
-// waves scatter every in-radius key of their share of the candidate groups to its bucket's next
-// slot (a workgroup per keypoint, as k_shot_count).
+// waves scatter the index of every in-radius neighbour of their share of the candidate groups to its
+// bucket's next slot (a workgroup per keypoint, as k_shot_count). 4-byte entries: the scatter's
+// partial-line writes cost 2.1 x the 8-byte keys' bytes (profiles/r05n_gather_pmc.txt), and the
+// rank kernels recompute d2 from the L2-resident points instead.
 __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, const float* __restrict__ kps, int k, float R,
                                                                 const long long* __restrict__ offs,
                                                                 const unsigned int* __restrict__ bh,
                                                                 unsigned int* __restrict__ bstart,
-                                                                unsigned long long* __restrict__ seg,
+                                                                unsigned int* __restrict__ seg,
                                                                 const int* __restrict__ err) {
     __shared__ CandLds lds[SG_WAVES];
     __shared__ unsigned int cu[SG_BUCKETS];
@@ -196,30 +204,28 @@ __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, con
             ur += hv[j];
         }
         __syncthreads();
-        unsigned long long* out = seg + offs[q];
+        unsigned int* out = seg + offs[q];
         for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
-            if (v) {
-                const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | idx;
-#if SG_NT_STORE
-                __builtin_nontemporal_store(key, &out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)]);
-#else
-                out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = key;
-#endif
-            }
+            if (v) out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = idx;
         }, 0, wave, SG_WAVES);
         __syncthreads();  // cu and wsum are rewritten for the next keypoint
     }
 }
 
 // wave per 64-rank chunk of a bucket-grouped segment: every key's exact (d2, idx) rank inside its
-// bucket -> the sorted segment, stored as the neighbour indices alone (keys are unique, buckets hold a few keys each). The buckets the
-// chunk's keys belong to span [lo, hi) of the segment (the chunk plus the parts of its two end
-// buckets outside it); when that fits SR_STAGE keys it is staged in LDS and ranked from there.
+// bucket -> the sorted segment, stored as the neighbour indices alone (keys are unique, buckets hold a
+// few keys each; sg_key rebuilds them from the gathered indices). The buckets the chunk's keys belong
+// to span [lo, hi) of the segment (the chunk plus the parts of its two end buckets outside it). The
+// wave first stages the keys of a window of SR_WPRE ranks either side of the chunk (its indices and
+// their points in flight together, before the bucket starts are known): a span inside it is ranked
+// from there; a larger one is restaged (<= SR_STAGE keys) or ranked from HBM.
 #define SR_STAGE 256
-__global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long long* __restrict__ offs,
+#define SR_WPRE 32
+__global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const float4* __restrict__ pts4,
+                                                   const float* __restrict__ kps, const long long* __restrict__ offs,
                                                    const int* __restrict__ cb, const int* __restrict__ owner,
                                                    const unsigned int* __restrict__ bstart,
-                                                   const unsigned long long* __restrict__ seg,
+                                                   const unsigned int* __restrict__ seg,
                                                    unsigned int* __restrict__ out, const int4* __restrict__ cinfo) {
     __shared__ unsigned long long stage[4][SR_STAGE];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -245,8 +251,18 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
         const float R2 = (float)((double)R * (double)R);
         const float sc = (float)SG_BUCKETS / R2;
         const unsigned int* bs = bstart + (size_t)q * SG_BUCKETS;
-        const unsigned long long* sg = seg + o;
-        const unsigned long long key = i < n ? sg[i] : ~0ull;
+        const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+        const unsigned int* sg = seg + o;
+        unsigned long long* st = stage[wave];
+        // the window [w0, w0 + 128): both loads of every lane issued before their points
+        const int w0 = c0 - SR_WPRE;
+        const int pa = w0 + lane, pb = w0 + 64 + lane;
+        const unsigned int ia = sg[pa < 0 ? 0 : (pa < n ? pa : n - 1)], ib = sg[pb < n ? pb : n - 1];
+        const unsigned long long ka = sg_key(pts4, kx, ky, kz, ia), kb = sg_key(pts4, kx, ky, kz, ib);
+        st[lane] = pa >= 0 && pa < n ? ka : ~0ull;
+        st[64 + lane] = pb < n ? kb : ~0ull;
+        __builtin_amdgcn_wave_barrier();
+        const unsigned long long key = st[SR_WPRE + lane];  // rank i = c0 + lane (~0 past n)
         const int b = sg_bucket(__uint_as_float((unsigned int)(key >> 32)), sc);
         const int b_lo = readlane_i(b, 0), b_hi = readlane_i(b, last - c0);
         const unsigned int lo = bs[b_lo], hi = b_hi + 1 < SG_BUCKETS ? bs[b_hi + 1] : (unsigned int)n;
@@ -256,14 +272,17 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
             e0 = b + 1 < SG_BUCKETS ? bs[b + 1] : (unsigned int)n;
         }
         unsigned int rank = 0;
-        if (hi - lo <= SR_STAGE) {
-            unsigned long long* st = stage[wave];
-            for (unsigned int j = lane; j < hi - lo; j += 64) st[j] = sg[lo + j];
+        if ((int)lo >= w0 && (int)hi <= w0 + 128) {
+            if (i < n)
+                for (unsigned int j = s0; j < e0; ++j) rank += st[j - w0] < key ? 1u : 0u;
+        } else if (hi - lo <= SR_STAGE) {
+            __builtin_amdgcn_wave_barrier();  // every lane holds its key: restage the span
+            for (unsigned int j = lane; j < hi - lo; j += 64) st[j] = sg_key(pts4, kx, ky, kz, sg[lo + j]);
             __builtin_amdgcn_wave_barrier();
             if (i < n)
                 for (unsigned int j = s0; j < e0; ++j) rank += st[j - lo] < key ? 1u : 0u;
         } else if (i < n) {
-            for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
+            for (unsigned int j = s0; j < e0; ++j) rank += sg_key(pts4, kx, ky, kz, sg[j]) < key ? 1u : 0u;
         }
         if (i < n) out[o + s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
         __builtin_amdgcn_wave_barrier();  // the next chunk restages
@@ -282,10 +301,11 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const long lo
 #ifndef RK_RANKMAX
 #define RK_RANKMAX 64  // spans whose buckets all hold <= this many keys rank in place; larger ones sort
 #endif
-__global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int* __restrict__ perm,
+__global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const float4* __restrict__ pts4,
+                                                      const float* __restrict__ kps, const int* __restrict__ perm,
                                                       const long long* __restrict__ offs,
                                                       const unsigned int* __restrict__ bstart,
-                                                      const unsigned long long* __restrict__ seg,
+                                                      const unsigned int* __restrict__ seg,
                                                       unsigned int* __restrict__ out, unsigned int rank_max) {
     __shared__ unsigned long long st[RK_SPAN];
     __shared__ unsigned int sbs[SG_BUCKETS + 1];
@@ -298,7 +318,8 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
     if (n <= 0) return;
     const float R2 = (float)((double)R * (double)R);
     const float sc = (float)SG_BUCKETS / R2;
-    const unsigned long long* sg = seg + o;
+    const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
+    const unsigned int* sg = seg + o;
     unsigned int* op = out + o;
     // the bucket starts, and end(1024) = n
     for (int b = t; b < SG_BUCKETS; b += RK_T) sbs[b] = bstart[(size_t)q * SG_BUCKETS + b];
@@ -330,16 +351,16 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
             // bucket b0 alone exceeds the span: rank it from HBM
             const unsigned int s0 = lo, e0 = sbs[b0 + 1];
             for (unsigned int i = s0 + t; i < e0; i += RK_T) {
-                const unsigned long long key = sg[i];
+                const unsigned long long key = sg_key(pts4, kx, ky, kz, sg[i]);
                 unsigned int rank = 0;
-                for (unsigned int j = s0; j < e0; ++j) rank += sg[j] < key ? 1u : 0u;
+                for (unsigned int j = s0; j < e0; ++j) rank += sg_key(pts4, kx, ky, kz, sg[j]) < key ? 1u : 0u;
                 op[s0 + rank] = (unsigned int)(key & 0xFFFFFFFFu);
             }
             e = b0 + 1;
         } else if (rank_path) {
             // small buckets: every key ranked against its bucket in LDS
             const unsigned int hi = sbs[e], m = hi - lo;
-            for (unsigned int i = t; i < m; i += RK_T) st[i] = sg[lo + i];
+            for (unsigned int i = t; i < m; i += RK_T) st[i] = sg_key(pts4, kx, ky, kz, sg[lo + i]);
             __syncthreads();
             for (unsigned int i = t; i < m; i += RK_T) {
                 const unsigned long long key = st[i];
@@ -357,7 +378,7 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const int
             const unsigned int hi = sbs[e], m = hi - lo;
             int P = 64;
             while (P < (int)m) P <<= 1;
-            for (int i = t; i < P; i += RK_T) st[i] = i < (int)m ? sg[lo + i] : ~0ull;
+            for (int i = t; i < P; i += RK_T) st[i] = i < (int)m ? sg_key(pts4, kx, ky, kz, sg[lo + i]) : ~0ull;
             __syncthreads();
             for (int size = 2; size <= P; size <<= 1) {
                 for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -408,28 +429,29 @@ hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, flo
 }
 
 hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
-                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s,
+                                const unsigned int* bh, unsigned int* bstart, unsigned int* seg, hipStream_t s,
                                 const int* err) {
     if (k <= 0) return hipSuccess;
     bsk::k_shot_gather_b<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, offs, bh, bstart, seg, err);
     return hipGetLastError();
 }
 
-hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long* offs, const unsigned int* bstart,
-                               const unsigned long long* seg, unsigned int* out, hipStream_t s, int rank_max) {
+hipError_t launch_shot_rank_wg(int k, float R, const float4* pts4, const float* kps, const int* perm,
+                               const long long* offs, const unsigned int* bstart, const unsigned int* seg,
+                               unsigned int* out, hipStream_t s, int rank_max) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_rank_wg<<<k, RK_T, 0, s>>>(k, R, perm, offs, bstart, seg, out,
+    bsk::k_shot_rank_wg<<<k, RK_T, 0, s>>>(k, R, pts4, kps, perm, offs, bstart, seg, out,
                                              rank_max < 0 ? (unsigned int)RK_RANKMAX : (unsigned int)rank_max);
     return hipGetLastError();
 }
 
-hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
-                            const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
-                            hipStream_t s, const int4* cinfo, int max_blocks) {
+hipError_t launch_shot_rank(int k, int n_chunks, float R, const float4* pts4, const float* kps, const long long* offs,
+                            const int* cb, const int* owner, const unsigned int* bstart, const unsigned int* seg,
+                            unsigned int* out, hipStream_t s, const int4* cinfo, int max_blocks) {
     if (k <= 0 || n_chunks <= 0) return hipSuccess;
     int blocks = (n_chunks + 3) / 4;
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    bsk::k_shot_rank<<<blocks, 256, 0, s>>>(k, R, offs, cb, owner, bstart, seg, out, cinfo);
+    bsk::k_shot_rank<<<blocks, 256, 0, s>>>(k, R, pts4, kps, offs, cb, owner, bstart, seg, out, cinfo);
     return hipGetLastError();
 }
 

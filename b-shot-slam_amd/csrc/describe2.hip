@@ -851,10 +851,10 @@ hipError_t launch_describe2(const Describe2Args& A, int part, hipStream_t s) {
                 // the main stream's small grids find CUs between them; results do not depend on it
                 const int step = (A.k + A.slices - 1) / (A.slices > 0 ? A.slices : 1);
                 for (int s0 = 0; s0 < A.k; s0 += step)
-                    if ((e = launch_shot_rank_wg(std::min(step, A.k - s0), A.R, A.perm + s0, A.offs, A.bstart, A.seg, A.sorted, s,
+                    if ((e = launch_shot_rank_wg(std::min(step, A.k - s0), A.R, A.pts4, A.kps, A.perm + s0, A.offs, A.bstart, A.seg, A.sorted, s,
                                                  A.rank_max)))
                         return e;
-            } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s, A.cinfo,
+            } else if ((e = launch_shot_rank(A.k, A.n_chunks, A.R, A.pts4, A.kps, A.offs, A.cb, A.owner, A.bstart, A.seg, A.sorted, s, A.cinfo,
                                              A.max_blocks))) {
                 return e;
             }

@@ -33,21 +33,24 @@ hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R,
                              hipStream_t s, unsigned int* bh = nullptr);
 // bucket-grouped gather (bstart: per-keypoint bucket starts) and the in-bucket rank that sorts it
 hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float R, const long long* offs,
-                                const unsigned int* bh, unsigned int* bstart, unsigned long long* seg, hipStream_t s,
+                                const unsigned int* bh, unsigned int* bstart, unsigned int* seg, hipStream_t s,
                                 const int* err = nullptr);
 // count + device-side plan (offs, chunk bases cb, LPT perm) against preallocated capacities;
 // err |= 16 (and empty ranges) when they do not suffice. k <= 8192.
 hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, float R, int* counts, unsigned int* bh,
                                   long long seg_cap, int chunk_cap, long long* offs, int* cb, int* perm, int* err,
                                   hipStream_t s);
-// out: the neighbour indices of every segment in (d2, idx) order (4 B each; the consumers recompute
-// d2 from the points with the gather's expression, bit-identical)
-// the same, a workgroup per keypoint in perm's order (spans of whole buckets staged in LDS)
-hipError_t launch_shot_rank_wg(int k, float R, const int* perm, const long long* offs, const unsigned int* bstart,
-                               const unsigned long long* seg, unsigned int* out, hipStream_t s, int rank_max = -1);
-hipError_t launch_shot_rank(int k, int n_chunks, float R, const long long* offs, const int* cb, const int* owner,
-                            const unsigned int* bstart, const unsigned long long* seg, unsigned int* out,
-                            hipStream_t s, const int4* cinfo = nullptr, int max_blocks = 0);
+// seg: the gather's bucket-grouped neighbour indices; out: every segment in (d2, idx) order (4 B
+// each; the rank kernels and the consumers recompute d2 from the points with the gather's
+// expression, bit-identical)
+// a workgroup per keypoint in perm's order (spans of whole buckets staged in LDS)
+hipError_t launch_shot_rank_wg(int k, float R, const float4* pts4, const float* kps, const int* perm,
+                               const long long* offs, const unsigned int* bstart, const unsigned int* seg,
+                               unsigned int* out, hipStream_t s, int rank_max = -1);
+// a wave per 64-rank chunk
+hipError_t launch_shot_rank(int k, int n_chunks, float R, const float4* pts4, const float* kps, const long long* offs,
+                            const int* cb, const int* owner, const unsigned int* bstart, const unsigned int* seg,
+                            unsigned int* out, hipStream_t s, const int4* cinfo = nullptr, int max_blocks = 0);
 hipError_t launch_match(const unsigned int* a, int na, const unsigned int* b, int nb, unsigned long long* best,
                         int* out, hipStream_t s);
 hipError_t launch_pack_points(const float* xyz, int n, float4* out, hipStream_t s);
@@ -123,7 +126,7 @@ struct Describe2Args {
     const float4* pts4 = nullptr;
     const float4* normals = nullptr;
     const float* kps = nullptr;
-    const unsigned long long* seg = nullptr;  // unsorted keys (gather)
+    const unsigned int* seg = nullptr;        // bucket-grouped neighbour indices (gather)
     unsigned int* sorted = nullptr;           // neighbour indices in (d2, idx) order (output of k_shot_rank)
     double* csum = nullptr;                   // 8 per chunk
     double* eig = nullptr;                    // 8 per keypoint
