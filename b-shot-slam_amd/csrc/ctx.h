@@ -89,6 +89,7 @@ struct CloudState {
     bool prefetched = false;  // loaded (and SR/ISS launched) ahead of use on the side stream
     int sr_state = 0;         // 0 not launched, 1 launched (results land in h_ratio at ev_sr)
     int iss_state = 0;        // 0 not launched, 1 launched (results land in h_flag at ev_iss)
+    int zeroed = 0;           // bit 0: errw[0] zeroed by the grid build, bit 1: errw[1] and issovf[0]
     DBuf<float> ratio;
     DBuf<double> third;
     DBuf<unsigned char> issflag;
@@ -162,6 +163,7 @@ struct bshot_ctx {
     DBuf<float4> normals_snap;
     int normals_snap_size = -1;  // -1: no snapshot held
     int normals_snap_n = 0;
+    int normals_snap_defer = 0;  // snapshot slots the next describe copies (ctx_normals_snapshot defer)
 
     // describe
     DBuf<float> kps;
@@ -312,7 +314,9 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k);
 // writes slots [0, k) and zero-fills past the logical size, so slots [0, min(k, size)) and the size
 // are all it can change. snapshot: queued on st before the describe; restore: after the describe
 // finished (the worker synchronised st), when its result is dropped; discard: when it is adopted.
-int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k);
+// defer: the copy is left to the next ctx_describe_on on st (its count kernel carries it, or it
+// queues the copy first), which must follow before anything else touches the normals.
+int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k, bool defer = false);
 int ctx_normals_restore(bshot_ctx* c);
 void ctx_normals_discard(bshot_ctx* c);
 // frame-sharded mode: slots [0, m) of the persistent normals array to the host (m <= its logical

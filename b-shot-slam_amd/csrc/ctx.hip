@@ -168,9 +168,11 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
     s.prefetched = false;
     s.sr_state = 0;
     s.iss_state = 0;
+    s.zeroed = 0;
     HIPCHK(ensure_events(s), "events");
     HIPCHK(s.pts4.ensure(n > 0 ? n : 1), "alloc pts4");
     HIPCHK(s.errw.ensure(2), "alloc err");
+    HIPCHK(s.issovf.ensure((size_t)n + 1), "alloc iss overflow");
     if (n > 0) {
         const int sg1 = c->stage_begin(BSHOT_STAGE_GRID, st);
         if (c->opt_ladder4) {
@@ -182,8 +184,11 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
 #define ISS_LEVEL5 1  // 0: ISS on the SR ladder's level 0 (cells r/16) as in round 4 (A/B)
 #endif
             s.iss_lvl = ISS_LEVEL5 && c->opt_iss_grid && 0.5f * c0 >= 0.5f * c->prm.iss_salient;  // cells r/32 >= salient / 2
-            HIPCHK(grid_build_ladder(lad, d_xyz, n, c0, s.pts4.p, st, 0xFu, 0, s.iss_lvl ? &s.grid_iss : nullptr),
+            // its first kernel also zeroes the SR / ISS error words and the ISS overflow count
+            HIPCHK(grid_build_ladder(lad, d_xyz, n, c0, s.pts4.p, st, 0xFu, 0, s.iss_lvl ? &s.grid_iss : nullptr,
+                                     s.errw.p, s.issovf.p),
                    "grid build (ladder)");
+            s.zeroed = 3;
         } else {
             HIPCHK(grid_build(s.grid_fine, d_xyz, n, c->prm.seg_radius * 0.125f, s.pts4.p, st), "grid build (r/8)");
             HIPCHK(grid_build(s.grid_coarse, d_xyz, n, c->prm.seg_radius * 0.5f, s.pts4.p, st), "grid build (r/2)");
@@ -204,7 +209,8 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.ratio.ensure(n > 0 ? n : 1), "alloc ratio");
     HIPCHK(s.h_ratio.ensure(n > 0 ? n : 1), "alloc pinned ratio");
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
-    HIPCHK(kfill(s.errw.p, 0, sizeof(int), st), "memset err");
+    if (!(s.zeroed & 1)) HIPCHK(kfill(s.errw.p, 0, sizeof(int), st), "memset err");
+    s.zeroed &= ~1;
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
@@ -229,7 +235,9 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     HIPCHK(s.issnmc.ensure(n > 0 ? n : 1), "alloc iss nms counts");
     HIPCHK(s.h_flag.ensure(n > 0 ? n : 1), "alloc pinned flags");
     HIPCHK(s.h_err.ensure(2), "alloc pinned err");
-    HIPCHK(kfill(s.errw.p + 1, 0, sizeof(int), st), "memset err");
+    const bool zeroed = (s.zeroed & 2) != 0;  // errw[1] and the overflow count, by the grid build
+    s.zeroed &= ~2;
+    if (!zeroed) HIPCHK(kfill(s.errw.p + 1, 0, sizeof(int), st), "memset err");
     if (n > 0) {
         const int sg3 = c->stage_begin(BSHOT_STAGE_ISS, st);
         // ISS on the SR ladder's points, no sort of its own: the ladder's fifth level (cells r/32 =
@@ -244,7 +252,7 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
         c->hmark("Q_iss_grid");
         HIPCHK(launch_iss(reuse && !lvl5 ? s.grid_l16 : s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
-                          s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks),
+                          s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks, zeroed),
                "iss launch");
         c->stage_end(sg3, st);
         c->hmark("Q_iss_k");
@@ -384,14 +392,17 @@ int ctx_iss_launch(bshot_ctx* c) {
     return cloud_iss(c, c->cs, c->iss);
 }
 
-int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k) {
+int ctx_normals_snapshot(bshot_ctx* c, hipStream_t st, int k, bool defer) {
     const int m = std::min(std::max(k, 0), c->normals_size);
     c->normals_snap_size = c->normals_size;
     c->normals_snap_n = m;
+    c->normals_snap_defer = 0;
     if (m > 0) {
         HIPCHK(c->normals_snap.ensure(m), "alloc normals snapshot");
-        HIPCHK(kcopy(c->normals_snap.p, c->normals.p, sizeof(float4) * m, st),
-               "snapshot normals");
+        if (defer)
+            c->normals_snap_defer = m;
+        else
+            HIPCHK(kcopy(c->normals_snap.p, c->normals.p, sizeof(float4) * m, st), "snapshot normals");
     }
     return BSHOT_OK;
 }
@@ -450,24 +461,41 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     const int n = S.n;
     // persistent normals array: resize(n) keeps [0, min) and value-initialises new slots
     HIPCHK(c->normals.ensure(std::max(n, std::max(k, 1))), "alloc normals");
-    if (n > c->normals_size)
-        HIPCHK(kfill(c->normals.p + c->normals_size, 0, sizeof(float4) * (n - c->normals_size), st),
-               "zero normals");
+    // A4: with normal_radius == shot_radius the normals' neighbours are the head of each keypoint's
+    // sorted SHOT segment (k_normals_seg after the rank below); otherwise a search of their own
+    const bool nseg = c->opt_normals_seg && c->prm.normal_radius == c->prm.shot_radius;
+    // the device-planned describe with the normals from the segments: its count kernel is the first
+    // to touch the error word and the normals, so it carries their fills
+    const bool dev_plan = !c->plan_on_host && k > 0 && k <= 8192 && c->seg_hint > 0;
+    const bool fold = nseg && dev_plan;
+    // a deferred normals snapshot (ctx_normals_snapshot): slots [0, snap) before this describe
+    const int snap = c->normals_snap_defer;
+    c->normals_snap_defer = 0;
+    if (snap > 0 && !fold)
+        HIPCHK(kcopy(c->normals_snap.p, c->normals.p, sizeof(float4) * snap, st), "snapshot normals");
+    float4* z4 = nullptr;
+    int nz = 0;
+    if (n > c->normals_size) {
+        if (fold) {
+            z4 = c->normals.p + c->normals_size;
+            nz = n - c->normals_size;
+        } else {
+            HIPCHK(kfill(c->normals.p + c->normals_size, 0, sizeof(float4) * (n - c->normals_size), st),
+                   "zero normals");
+        }
+    }
     c->normals_size = n;
     if (k <= 0) return BSHOT_OK;
     // errw: [0] error bits (2 normals overflow, 8 sort piece overflow, 16 device plan over
     // capacity), [2..3] the neighbourhood total as planned on the device
     HIPCHK(c->errw.ensure(4), "alloc err");
-    HIPCHK(kfill(c->errw.p, 0, 4 * sizeof(int), st), "memset err");
+    if (!fold) HIPCHK(kfill(c->errw.p, 0, 4 * sizeof(int), st), "memset err");
     HIPCHK(c->counts.ensure(k), "alloc counts");
     HIPCHK(c->offs.ensure(k + 1), "alloc offs");
     HIPCHK(c->rf.ensure(9 * (size_t)k), "alloc rf");
     HIPCHK(c->ok.ensure(k), "alloc ok");
     HIPCHK(c->bits.ensure(11 * (size_t)k), "alloc bits");
     HIPCHK(c->shot.ensure(352 * (size_t)k), "alloc shot");
-    // A4: with normal_radius == shot_radius the normals' neighbours are the head of each keypoint's
-    // sorted SHOT segment (k_normals_seg after the rank below); otherwise a search of their own
-    const bool nseg = c->opt_normals_seg && c->prm.normal_radius == c->prm.shot_radius;
     if (!nseg) {
         const int sg4 = c->stage_begin(BSHOT_STAGE_NORMALS, st);
         HIPCHK(launch_normals(S.ladder, c->ladder_mode(S), S.pts4.p, c->kps.p, k, c->prm.normal_radius,
@@ -479,7 +507,7 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     const int sg5 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);
     HIPCHK(c->sbh.ensure(1024 * (size_t)k), "alloc bucket hist");
     HIPCHK(c->sbst.ensure(1024 * (size_t)k), "alloc bucket starts");
-    if (!c->plan_on_host && k <= 8192 && c->seg_hint > 0) {
+    if (dev_plan) {
         // the whole describe queued without a host round trip: the plan (segment offsets, chunk
         // bases, LPT order) is computed on the device against capacities sized from the largest
         // neighbourhood total seen so far (+25%); an overflow (errw bit 16) makes the caller
@@ -498,7 +526,8 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
         HIPCHK(c->eig.ensure(8 * (size_t)k), "alloc eig");
         HIPCHK(c->okf.ensure(k), "alloc okf");
         HIPCHK(launch_shot_count_plan(S.grid_coarse, c->kps.p, k, R, c->counts.p, c->sbh.p, seg_cap, chunk_cap,
-                                      c->offs.p, c->cb.p, c->perm.p, c->errw.p, st),
+                                      c->offs.p, c->cb.p, c->perm.p, c->errw.p, st, fold, z4, nz,
+                                      snap > 0 ? c->normals_snap.p : nullptr, c->normals.p, snap),
                "shot count + plan");
         c->stage_end(sg5, st);
         const int sg6 = c->stage_begin(BSHOT_STAGE_SHOT_GATHER, st);

@@ -39,9 +39,19 @@ __device__ __forceinline__ int sg_bucket(float d2, float sc) {
 // (for_candidates' part / nparts), so a large neighbourhood takes a quarter of the dependent
 // round trips (the wave-per-keypoint kernel's tail was its largest keypoint: 0.33 ms under load).
 #define SG_WAVES 4
+// zw (nullable): the describe's 4-int error word, zeroed here; z4 / nz: float4s zeroed across the
+// grid (the new slots of the persistent normals array); cs4 -> cd4, cm float4s (the normals
+// snapshot, disjoint from z4) -- the fills and the copy this launch carries
 __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_count(GridView g, const float* __restrict__ kps, int k, float R,
-                                                             int* __restrict__ counts, unsigned int* __restrict__ bh) {
+                                                             int* __restrict__ counts, unsigned int* __restrict__ bh,
+                                                             int* __restrict__ zw, float4* __restrict__ z4, int nz,
+                                                             float4* __restrict__ cd4, const float4* __restrict__ cs4,
+                                                             int cm) {
     __shared__ CandLds lds[SG_WAVES];
+    if (zw && blockIdx.x == 0 && threadIdx.x < 4) zw[threadIdx.x] = 0;
+    for (int i = blockIdx.x * 64 * SG_WAVES + threadIdx.x; i < nz; i += gridDim.x * 64 * SG_WAVES)
+        z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = blockIdx.x * 64 * SG_WAVES + threadIdx.x; i < cm; i += gridDim.x * 64 * SG_WAVES) cd4[i] = cs4[i];
     __shared__ unsigned int hist[SG_BUCKETS];
     __shared__ int tot;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -409,21 +419,25 @@ namespace bsh {
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s, unsigned int* bh) {
     if (k <= 0) return hipSuccess;
-    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
+    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh, nullptr, nullptr, 0, nullptr,
+                                                  nullptr, 0);
     bsk::k_excl_scan<<<1, 1024, 0, s>>>(counts, k, offs);
     return hipGetLastError();
 }
 
 hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, float R, int* counts, unsigned int* bh,
                                   long long seg_cap, int chunk_cap, long long* offs, int* cb, int* perm, int* err,
-                                  hipStream_t s) {
+                                  hipStream_t s, bool zero_err, float4* z4, int nz, float4* cd4, const float4* cs4,
+                                  int cm) {
     if (k <= 0) return hipSuccess;
     if (k > DP_MAXK) return hipErrorInvalidValue;
 #ifdef DIAG_COUNT_TWICE
     // diagnostic builds only: the count kernel twice (it overwrites its outputs) -- its marginal cost
-    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
+    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh, nullptr, nullptr, 0, nullptr,
+                                                  nullptr, 0);
 #endif
-    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh);
+    bsk::k_shot_count<<<k, 64 * SG_WAVES, 0, s>>>(g.view(), kps, k, R, counts, bh, zero_err ? err : nullptr, z4, nz,
+                                                  cd4, cs4, cm);
     bsk::k_desc_plan<<<1, 1024, 0, s>>>(counts, k, seg_cap, chunk_cap, offs, cb, perm, err);
     return hipGetLastError();
 }

@@ -82,7 +82,7 @@ int gmap_insert(bshot_ctx* c, const float* kps_host, const float* ratio_host, co
 // order, each block in libstdc++ order, or insertion order when canonical), then the ref keypoints
 // transformed by ref_pose -> c->gtgt (float3) and c->ma rows [na, na + nb)
 int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_kps, const unsigned int* ref_bits,
-               int kref, const float ref_pose[16], int na, int canonical, int* nb_out);
+               int kref, const float ref_pose[16], int na, int canonical, int* nb_out, bool ref_uploaded = false);
 // featureMatching on the device targets: source words a (host) -> c->ma rows [0, na), gmap_query,
 // the Hamming match (ctx_match_dev) and one sync; targets' positions -> tgt (host, nb x 3)
 int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], float range, const float* ref_kps,

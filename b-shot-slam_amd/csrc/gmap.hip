@@ -552,6 +552,7 @@ __global__ void k_gmap_qcount(GMapDev m, int x0, int y0, int z0, int ny, int nz,
 #ifndef GM_SCAN_T
 #define GM_SCAN_T 256
 #endif
+// tot: the total, written straight to the pinned host counters (no copy launch)
 __global__ void __launch_bounds__(GM_SCAN_T) k_gmap_scan(const int* __restrict__ cnt, int npos, int* __restrict__ off,
                                                          int* __restrict__ tot) {
     __shared__ int part[GM_SCAN_T];
@@ -952,9 +953,8 @@ static int query_count(bshot_ctx* c, GMap& g, const QueryBox& q) {
     int* cnt = g.qcnt.p;
     bsk::k_gmap_qcount<<<(q.npos + 255) / 256, 256, 0, c->stream>>>(dev_view(g), q.x0, q.y0, q.z0, q.ny, q.nz, q.npos, cnt,
                                                                     cnt + q.npos);
-    bsk::k_gmap_scan<<<1, GM_SCAN_T, 0, c->stream>>>(cnt, q.npos, cnt + 2 * q.npos, cnt + 3 * q.npos);
-    HIPCHK(kcopy(g.p_ctr.p + GM_QTOT, cnt + 3 * q.npos, sizeof(int), c->stream),
-           "D2H map total");
+    bsk::k_gmap_scan<<<1, GM_SCAN_T, 0, c->stream>>>(cnt, q.npos, cnt + 2 * q.npos, g.p_ctr.p + GM_QTOT);
+    HIPCHK(hipGetLastError(), "gmap query scan");
     g.q_active = true;
     return BSHOT_OK;
 }
@@ -980,8 +980,19 @@ static QueryBox query_box(const float pos[3], float range) {
     return q;
 }
 
+// stage the reference keypoints (positions + descriptors) in g.p_refin; the caller uploads them to
+// g.refin (gmap_match: in one launch with its descriptors)
+static int stage_ref(GMap& g, const float* ref_kps, const unsigned int* ref_bits, int kref) {
+    if (kref <= 0) return BSHOT_OK;
+    if (g.refin.ensure(14 * (size_t)kref) != hipSuccess || g.p_refin.ensure(14 * (size_t)kref) != hipSuccess)
+        return BSHOT_EHIP;
+    std::memcpy(g.p_refin.p, ref_kps, sizeof(float) * 3 * kref);
+    std::memcpy(g.p_refin.p + 3 * (size_t)kref, ref_bits, sizeof(unsigned int) * 11 * kref);
+    return BSHOT_OK;
+}
+
 int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_kps, const unsigned int* ref_bits,
-               int kref, const float ref_pose[16], int na, int canonical, int* nb_out) {
+               int kref, const float ref_pose[16], int na, int canonical, int* nb_out, bool ref_uploaded) {
     GMap& g = own_map(c);
     int rc = gmap_init(c, g);
     if (rc) return rc;
@@ -1028,12 +1039,10 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
         base += mm;
     }
     if (kref > 0) {
-        HIPCHK(g.refin.ensure(14 * (size_t)kref), "gmap ref");
-        HIPCHK(g.p_refin.ensure(14 * (size_t)kref), "gmap pinned ref");
-        std::memcpy(g.p_refin.p, ref_kps, sizeof(float) * 3 * kref);
-        std::memcpy(g.p_refin.p + 3 * (size_t)kref, ref_bits, sizeof(unsigned int) * 11 * kref);
-        HIPCHK(kcopy(g.refin.p, g.p_refin.p, sizeof(float) * 14 * kref, c->stream),
-               "H2D ref");
+        if (!ref_uploaded) {
+            if ((rc = stage_ref(g, ref_kps, ref_bits, kref))) return c->fail("gmap ref alloc", rc);
+            HIPCHK(kcopy(g.refin.p, g.p_refin.p, sizeof(float) * 14 * kref, c->stream), "H2D ref");
+        }
         bsk::k_gmap_ref<<<(kref + 255) / 256, 256, 0, c->stream>>>(
             g.refin.p, reinterpret_cast<const unsigned int*>(g.refin.p + 3 * (size_t)kref), kref, xf(ref_pose),
             c->gtgt.p + 3 * (size_t)mtot, c->ma.p + 11 * ((size_t)na + mtot));
@@ -1080,14 +1089,20 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
                int32_t* corr_m, int* n_corr) {
     *n_corr = 0;
     HIPCHK(grow_keep(c->ma, 0, 11 * (size_t)(na > 0 ? na : 1), c->stream), "alloc descriptors");
+    GMap& g0 = own_map(c);
+    int rc = gmap_init(c, g0);
+    if (rc) return rc;
+    if ((rc = stage_ref(g0, ref_kps, ref_bits, kref))) return c->fail("gmap ref alloc", rc);
     if (na > 0) {
         HIPCHK(c->p_a.ensure(11 * (size_t)na), "alloc pinned descriptors");
         std::memcpy(c->p_a.p, a, sizeof(uint32_t) * 11 * na);
-        HIPCHK(kcopy(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * na, c->stream),
-               "H2D descriptors");
     }
+    // the descriptors and the reference keypoints in one launch
+    HIPCHK(kcopy2(c->ma.p, c->p_a.p, sizeof(uint32_t) * 11 * (size_t)(na > 0 ? na : 0), g0.refin.p, g0.p_refin.p,
+                  sizeof(float) * 14 * (size_t)(kref > 0 ? kref : 0), c->stream),
+           "H2D descriptors + ref");
     int nb = 0;
-    int rc = gmap_query(c, pos, range, ref_kps, ref_bits, kref, ref_pose, na, canonical, &nb);
+    rc = gmap_query(c, pos, range, ref_kps, ref_bits, kref, ref_pose, na, canonical, &nb, true);
     if (rc) return rc;
     *nb_out = nb;
     tgt.resize(3 * (size_t)nb);

@@ -41,9 +41,11 @@ hipError_t grid_build(DevGrid& g, const float* d_xyz, int n, float cell, float4*
 void grid_free(DevGrid& g, bool defer = false);
 // four nested grids (cells c0, 2c0, 4c0, 8c0) from one sort; g[1..3].spts alias g[0].spts.
 // level_mask: the levels whose hash tables are built (the sorted points are always written);
-// min_cap as grid_build's; finer (nullable): a fifth grid of cells c0 / 2 on the same points (ISS's)
+// min_cap as grid_build's; finer (nullable): a fifth grid of cells c0 / 2 on the same points (ISS's);
+// zero0 / zero1 (nullable, n >= 1): two ints each that the build's first kernel zeroes
 hipError_t grid_build_ladder(DevGrid* const* g, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s,
-                             unsigned level_mask = 0xFu, int min_cap = 0, DevGrid* finer = nullptr);
+                             unsigned level_mask = 0xFu, int min_cap = 0, DevGrid* finer = nullptr,
+                             int* zero0 = nullptr, int* zero1 = nullptr);
 
 
 }  // namespace bsh

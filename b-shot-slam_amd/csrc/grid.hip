@@ -87,9 +87,15 @@ __device__ __forceinline__ bool ladder_cells(float x, float y, float z, float c0
     return ix > -lim && ix < lim && iy > -lim && iy < lim && iz > -lim && iz < lim;
 }
 
+// zero (nullable): two int pairs the cloud's next kernels expect zeroed (SR / ISS error words, ISS
+// overflow count), so the build carries those fills
+struct ZeroWords {
+    int* p[2];
+};
 __global__ void k_ladder_keys(const float* __restrict__ xyz, int n, float c0, unsigned long long* __restrict__ keys,
-                              unsigned int* __restrict__ vals, float4* __restrict__ pts4) {
+                              unsigned int* __restrict__ vals, float4* __restrict__ pts4, ZeroWords zero) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 4 && zero.p[threadIdx.x >> 1]) zero.p[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     if (i >= n) return;
     const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
     pts4[i] = make_float4(x, y, z, __uint_as_float((unsigned)i));
@@ -183,7 +189,7 @@ static unsigned int pow2_at_least(unsigned int x) {
 // g[0..3]: grids of cell c0, 2 c0, 4 c0, 8 c0 built from one 63-bit radix sort; g[0] owns the
 // sort buffers and the cell-sorted points, g[1..3] own only their hash tables and alias g[0].spts
 hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, float c0, float4* d_pts4, hipStream_t s,
-                             unsigned level_mask, int min_cap, DevGrid* finer) {
+                             unsigned level_mask, int min_cap, DevGrid* finer, int* zero0, int* zero1) {
     hipError_t e;
     DevGrid& g0 = *gp[0];
     bool fresh = n > g0.cap || !g0.keys || g0.alias;
@@ -232,7 +238,7 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
         }
     }
     const int B = 256;
-    bsk::k_ladder_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, c0, g0.keys, g0.vals, d_pts4);
+    bsk::k_ladder_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, c0, g0.keys, g0.vals, d_pts4, bsk::ZeroWords{{zero0, zero1}});
     size_t tb = g0.tmp_bytes;
     if ((e = rocprim::radix_sort_pairs(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 63, s)))
         return e;

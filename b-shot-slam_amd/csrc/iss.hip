@@ -468,7 +468,7 @@ namespace bsh {
 
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc, int* err,
-                      hipStream_t s, int ovf_blocks, int nms_blocks) {
+                      hipStream_t s, int ovf_blocks, int nms_blocks, bool ovf_zeroed) {
     if (n <= 0) return hipSuccess;
 #ifdef DIAG_ISS_TWICE
     // diagnostic builds only: the lane kernel an extra time (its outputs are rewritten below)
@@ -479,7 +479,7 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
                                                                                  g21, g32, third, ovf, nml, nmc);
     }
 #endif
-    hipError_t e = kfill(ovf, 0, sizeof(int), s);
+    hipError_t e = ovf_zeroed ? hipSuccess : kfill(ovf, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn,
                                                                              g21, g32, third, ovf, nml, nmc);

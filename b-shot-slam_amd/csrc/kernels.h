@@ -27,7 +27,7 @@ hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc,
-                      int* err, hipStream_t s, int ovf_blocks = 0, int nms_blocks = 0);
+                      int* err, hipStream_t s, int ovf_blocks = 0, int nms_blocks = 0, bool ovf_zeroed = false);
 // bh (nullable, [k][1024] u32): per-keypoint d2-bucket histogram for the bucketed gather
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s, unsigned int* bh = nullptr);
@@ -36,10 +36,13 @@ hipError_t launch_shot_gather_b(const DevGrid& g, const float* kps, int k, float
                                 const unsigned int* bh, unsigned int* bstart, unsigned int* seg, hipStream_t s,
                                 const int* err = nullptr);
 // count + device-side plan (offs, chunk bases cb, LPT perm) against preallocated capacities;
-// err |= 16 (and empty ranges) when they do not suffice. k <= 8192.
+// err |= 16 (and empty ranges) when they do not suffice. k <= 8192. The count kernel also zeroes
+// err[0..3] (zero_err) and z4[0, nz), and copies cs4[0, cm) to cd4 (the fills and the normals
+// snapshot the caller would otherwise launch)
 hipError_t launch_shot_count_plan(const DevGrid& g, const float* kps, int k, float R, int* counts, unsigned int* bh,
                                   long long seg_cap, int chunk_cap, long long* offs, int* cb, int* perm, int* err,
-                                  hipStream_t s);
+                                  hipStream_t s, bool zero_err = false, float4* z4 = nullptr, int nz = 0,
+                                  float4* cd4 = nullptr, const float4* cs4 = nullptr, int cm = 0);
 // seg: the gather's bucket-grouped neighbour indices; out: every segment in (d2, idx) order (4 B
 // each; the rank kernels and the consumers recompute d2 from the points with the gather's
 // expression, bit-identical)

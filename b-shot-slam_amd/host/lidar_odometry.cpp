@@ -309,7 +309,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
     TicToc t_d;
     // describe is queued on the side stream; while it runs, ISS (own stream) is collected
     c->hmark("W_topk_done");
-    if (bsh::ctx_normals_snapshot(c, c->side, k) != BSHOT_OK) fail("lookahead normals snapshot");
+    if (bsh::ctx_normals_snapshot(c, c->side, k, true) != BSHOT_OK) fail("lookahead normals snapshot");
     if (bsh::ctx_describe_on(c, S, c->side, k) != BSHOT_OK) fail("lookahead describe");
     c->hmark("W_describe_queued");
     TicToc t_iss;
