@@ -356,6 +356,10 @@ def main():
                 odo.replica_insert(r, rec)
         return st
 
+    wc_sweeps = [] if os.environ.get("BENCH_INTERVALS") else None
+    if wc_sweeps is not None:
+        import ctypes
+
     def timed(stepf):
         # barrier + device sync on both sides of exactly K sweeps; the lookahead started by the last
         # timed sweep finishes inside the region (drain)
@@ -367,6 +371,10 @@ def main():
         for i in range(a.warmup, nwork):
             st_.append(stepf(i))
             mk_.append(time.perf_counter())
+            if wc_sweeps is not None:  # diagnostics (BENCH_INTERVALS): the work counters after every sweep
+                wc_ = (ctypes.c_int64 * 12)()
+                bshot_py.lib().bshot_work_counters(ctypes.c_void_p(odo.context()), wc_, 12)
+                wc_sweeps.append(list(wc_))
         return t_0, st_, mk_
 
     for i in range(a.warmup):
@@ -580,7 +588,11 @@ def main():
     if rank == 0:
         if os.environ.get("BENCH_INTERVALS"):
             iv = np.diff([t0] + marks) * 1e3
-            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": wc_main,
+            # per sweep (timed order): ICP iterations, targets, mutual matches, inliers, host phase ms
+            per = [[s.icp_iters, s.n_target, s.n_mutual, s.n_inliers, s.n_keypoints] + [round(x, 3) for x in s.host_ms]
+                   for s in stats]
+            print(json.dumps({"sweep_intervals_ms": np.round(iv, 3).tolist(), "work": wc_main, "per_sweep": per,
+                              "work_per_sweep": wc_sweeps,
                               # CLOCK_MONOTONIC ms, the clock of BSHOT_GROW_TRACE's lines
                               "t0_ms": round(t0 * 1e3, 3), "marks_ms": np.round(np.array(marks) * 1e3, 3).tolist()}),
                   file=sys.stderr)
