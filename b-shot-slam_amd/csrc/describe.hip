@@ -308,6 +308,30 @@ __global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const float4*
 // keypoint) instead of waiting on it. A bucket alone larger than RK_SPAN is ranked from HBM.
 #define RK_T 256
 #define RK_SPAN 2048
+#define RK_PER (RK_SPAN / RK_T)
+// the keys of span positions [0, n) (n <= P <= RK_SPAN) into st[0, P), ~0 past n: each thread's
+// index loads, then its point loads, all in flight before the first key is formed
+__device__ __forceinline__ void rk_stage(unsigned long long* st, const unsigned int* __restrict__ sg, unsigned int n,
+                                         int P, const float4* __restrict__ pts4, float kx, float ky, float kz) {
+    const int t = threadIdx.x;
+    unsigned int id[RK_PER];
+#pragma unroll
+    for (int j = 0; j < RK_PER; ++j) {
+        const unsigned int i = t + j * RK_T;
+        id[j] = sg[i < n ? i : (n ? n - 1 : 0)];  // (a span of empty buckets: n = 0, lo < the segment's end)
+    }
+    float4 p[RK_PER];
+#pragma unroll
+    for (int j = 0; j < RK_PER; ++j) p[j] = pts4[id[j]];
+#pragma unroll
+    for (int j = 0; j < RK_PER; ++j) {
+        const int i = t + j * RK_T;
+        if (i < P)
+            st[i] = i < (int)n ? ((unsigned long long)__float_as_uint(d2_flann(kx, ky, kz, p[j].x, p[j].y, p[j].z)) << 32) |
+                                     id[j]
+                               : ~0ull;
+    }
+}
 #ifndef RK_RANKMAX
 #define RK_RANKMAX 64  // spans whose buckets all hold <= this many keys rank in place; larger ones sort
 #endif
@@ -370,7 +394,7 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const flo
         } else if (rank_path) {
             // small buckets: every key ranked against its bucket in LDS
             const unsigned int hi = sbs[e], m = hi - lo;
-            for (unsigned int i = t; i < m; i += RK_T) st[i] = sg_key(pts4, kx, ky, kz, sg[lo + i]);
+            rk_stage(st, sg + lo, m, (int)m, pts4, kx, ky, kz);
             __syncthreads();
             for (unsigned int i = t; i < m; i += RK_T) {
                 const unsigned long long key = st[i];
@@ -388,7 +412,7 @@ __global__ void __launch_bounds__(RK_T) k_shot_rank_wg(int k, float R, const flo
             const unsigned int hi = sbs[e], m = hi - lo;
             int P = 64;
             while (P < (int)m) P <<= 1;
-            for (int i = t; i < P; i += RK_T) st[i] = i < (int)m ? sg_key(pts4, kx, ky, kz, sg[lo + i]) : ~0ull;
+            rk_stage(st, sg + lo, m, P, pts4, kx, ky, kz);
             __syncthreads();
             for (int size = 2; size <= P; size <<= 1) {
                 for (int stride = size >> 1; stride > 0; stride >>= 1) {

@@ -67,8 +67,10 @@ hipError_t launch_gather_io(const float4* pts4, const int* h_idx, int k, float* 
 // distances from the list's centre, in ascending order; entry e of source i at [e * ns + i]), its
 // count (-1: none) and radius. Iteration >= 1: the sources moved by T16 (src_in -> src_out) and
 // their exact 1-NN keys; keys (d2 bits << 32 | index) land in best_out (pinned host memory).
+// 256: fewer sources leave their lists for the LDS grid search, which runs slowly beside the
+// SHOT histogram's LDS atomics (128 -> 256: +4.4 % sweeps/s, 512: +3.2 %; profiles/r05w_*)
 #ifndef ICP_LIST_CAP
-#define ICP_LIST_CAP 128
+#define ICP_LIST_CAP 256
 #endif
 // the result of one ICP call (coherent pinned host memory): the composed transform, the iteration
 // count, then seq (written last, after the others have reached host memory)
