@@ -87,6 +87,7 @@ struct CloudState {
     const bsh::DevGrid* ladder[4] = {nullptr, nullptr, nullptr, nullptr};
     bool grids_ok = false;
     bool prefetched = false;  // loaded (and SR/ISS launched) ahead of use on the side stream
+    bool iss_pending = false; // queued with option iss_defer: its ISS launches at ctx_queue_iss
     int sr_state = 0;         // 0 not launched, 1 launched (results land in h_ratio at ev_sr)
     int iss_state = 0;        // 0 not launched, 1 launched (results land in h_flag at ev_iss)
     int zeroed = 0;           // bit 0: errw[0] zeroed by the grid build, bit 1: errw[1] and issovf[0]
@@ -149,6 +150,7 @@ struct bshot_ctx {
     int opt_rank_max = -1;      // k_shot_rank_wg's in-place threshold (-1: RK_RANKMAX; 0: every span sorted)
     int opt_rank_wg = 2;        // SHOT rank kernel: 0 wave per 64-rank chunk, 1 workgroup per keypoint, 2 by neighbourhood size
     int opt_desc_slices = 1;    // the histogram / rank_wg kernels in this many launches (LPT slices)
+    int opt_iss_defer = 0;      // 1: the queued sweep's ISS launches after the current sweep's ICP
     int opt_sr_start = 80;      // SR ladder start predicted from own-cell densities (percent scale; 0: step 0)
     int opt_iss_grid = 1;       // ISS on the SR ladder's points: its fifth level, cells r/32 (0: own grid)
     int opt_iss_cell = 2;       // ISS grid cell = opt_iss_cell x salient radius (2: <= 8 cells per query)
@@ -309,6 +311,8 @@ int ctx_sync_main(bshot_ctx* c);
 int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n);
 int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n);
+// the queued sweep's ISS when option iss_defer held it back (main thread, after ICP); no-op otherwise
+int ctx_queue_iss(bshot_ctx* c);
 int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k);
 // persistent-normals state around a lookahead describe of k keypoints on stream st: a describe
 // writes slots [0, k) and zero-fills past the logical size, so slots [0, min(k, size)) and the size

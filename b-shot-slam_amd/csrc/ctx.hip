@@ -168,6 +168,7 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
     s.prefetched = false;
     s.sr_state = 0;
     s.iss_state = 0;
+    s.iss_pending = false;
     s.zeroed = 0;
     HIPCHK(ensure_events(s), "events");
     HIPCHK(s.pts4.ensure(n > 0 ? n : 1), "alloc pts4");
@@ -298,6 +299,7 @@ int ctx_prefetch_dev(bshot_ctx* c, const float* d_xyz, int n) {
     if (holds(c->pf2, d_xyz, n)) {
         // queued earlier (grids, SR and ISS on the pre/iss streams): promote; the lookahead
         // describe on the side stream starts after its grids
+        if (int rc = ctx_queue_iss(c)) return rc;
         swap_slots(c, c->pf, c->pf2);
         c->pf2.prefetched = false;
         HIPCHK(hipStreamWaitEvent(c->side, c->pf.ev_loaded, 0), "wait queued cloud");
@@ -338,6 +340,13 @@ int ctx_queue_dev(bshot_ctx* c, const float* d_xyz, int n) {
     return ctx_queue_rest(c, d_xyz, n);
 }
 
+int ctx_queue_iss(bshot_ctx* c) {
+    if (!c->pf2.iss_pending) return BSHOT_OK;
+    c->pf2.iss_pending = false;
+    HIPCHK(hipStreamWaitEvent(c->iss, c->pf2.ev_loaded, 0), "wait cloud");
+    return cloud_iss(c, c->pf2, c->iss);
+}
+
 // main-thread half of ctx_queue_dev: 1 when the cloud must be queued (the pre stream then waits
 // for the work already on the main stream), 0 when it is already held, < 0 on error
 int ctx_queue_begin(bshot_ctx* c, const float* d_xyz, int n) {
@@ -369,7 +378,9 @@ int ctx_queue_rest(bshot_ctx* c, const float* d_xyz, int n) {
     rc = cloud_sr(c, c->pf2, c->pre);
     if (rc) return rc;
     c->hmark("Q_iss");
-    if (c->prm.run_iss) {
+    if (c->prm.run_iss && c->opt_iss_defer) {
+        c->pf2.iss_pending = true;
+    } else if (c->prm.run_iss) {
         HIPCHK(hipStreamWaitEvent(c->iss, c->pf2.ev_loaded, 0), "wait cloud");
         rc = cloud_iss(c, c->pf2, c->iss);
         if (rc) return rc;
@@ -1317,6 +1328,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "hist_pack") c->opt_hist_pack = value ? 1 : 0;
     else if (k == "rank_wg") c->opt_rank_wg = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "desc_slices") c->opt_desc_slices = value < 1 ? 1 : (value > 64 ? 64 : value);
+    else if (k == "iss_defer") c->opt_iss_defer = value ? 1 : 0;
     else if (k == "gpu_map") c->opt_gpu_map = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "xseq_targets") c->opt_xseq_targets = value ? 1 : 0;
     else if (k == "xchg_index") c->opt_xchg_index = value ? 1 : 0;

@@ -646,6 +646,7 @@ void LidarOdometry::evaluateEstimation() {
     }
     stats_.icp_iters = iters;
     ctx_->hmark("M_icp");
+    check(bsh::ctx_queue_iss(ctx_), "queued iss");  // option iss_defer: the queued sweep's ISS starts now
     stats_.host_ms[5] = (float)t_icp.toc();
     Matrix4f F;
     std::memcpy(F.m, Ticp, sizeof(Ticp));

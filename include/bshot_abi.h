@@ -305,7 +305,9 @@ int bshot_map_set_query_mode(bshot_map* m, int mode);
  *      "pre_fast" 1 (default): the preprocessor's one-sort path when it applies; "side_prio";
  *      "timing_mask" stage-event mask; "rank_wg" 2 (default: by neighbourhood size) / 1 / 0: SHOT
  *      neighbour ranking with a workgroup per keypoint or a wave per 64-rank chunk; "desc_slices" 1
- *      (default): the per-keypoint histogram / rank kernels in that many launches over the LPT order; "hist_pack" 1
+ *      (default): the per-keypoint histogram / rank kernels in that many launches over the LPT order;
+ *      "iss_defer" 0 (default) / 1: the queued sweep's ISS launches with its grids, or after the
+ *      current sweep's ICP; "hist_pack" 1
  *      (default): the SHOT apply packs 12 ranks per LDS float atomic when the device passed the
  *      lane-order check (bshot_debug_lds_lane_order); "icp_device" 0 (default) / 1: ICP iterations
  *      handed to the host's Umeyama, or the whole loop on the device. Behaviour: "gpu_map" 1 (default, libstdc++ order) / 2

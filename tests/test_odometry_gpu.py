@@ -71,13 +71,13 @@ def test_odometry_no_icp_no_iss():
 
 
 @pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"topk_thread": 0}), (2, {"ransac_dev": 0}),
-                                        (2, {"map_sync": 0})])
+                                        (2, {"map_sync": 0}), (2, {"iss_defer": 1})])
 def test_odometry_lookahead_device_frames(depth, opts):
     """Throughput mode: HBM-resident sweeps, the next sweep's grids/SR/ISS prefetched on the side
     stream during the current one (bshot_odom_set_next_device; depth 2 also queues the sweep after
     next, bshot_odom_set_next2_device) -- results must not change, whichever host threading
-    (top-K thread), RANSAC scorer (GPU or host) and map-insert wait (map_sync 0: stream-ordered,
-    the size not read back) the knobs select."""
+    (top-K thread), RANSAC scorer (GPU or host), map-insert wait (map_sync 0: stream-ordered,
+    the size not read back) and queued-ISS launch point (iss_defer 1: after ICP) the knobs select."""
     import torch
 
     frames = [bshot_py.synth_sweep(f)[0] for f in range(20, 25)]
