@@ -260,6 +260,9 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
 // list entries a lane loads per round trip of its scan (the wave waits for its longest scan; beside
 // the SHOT histogram the lists' lines come from the MALL, not the L2): 4 -> 16 cut the iterations'
 // wait 0.23 -> 0.19 ms per sweep (134 VGPRs; profiles/r05z_*)
+// the lists' LDS sorts are bitonic over ICP_LIST_CAP slots: a power of two (a 384-entry build hung
+// its GPU test, session r05zb)
+static_assert((ICP_LIST_CAP & (ICP_LIST_CAP - 1)) == 0, "ICP_LIST_CAP must be a power of two");
 #ifndef ICPH_BATCH
 #define ICPH_BATCH 16
 #endif
