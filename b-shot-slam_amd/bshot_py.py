@@ -40,6 +40,8 @@ class FrameStats(ctypes.Structure):
         ("h_diff", ctypes.c_float), ("t_diff", ctypes.c_float), ("T_ransac", ctypes.c_float * 16),
         ("pose", ctypes.c_float * 16), ("map_size", ctypes.c_int), ("repeat_sr", ctypes.c_float),
         ("repeat_iss", ctypes.c_float), ("host_ms", ctypes.c_float * 8),
+        ("corr_n", ctypes.c_int), ("corr_avg", ctypes.c_float), ("corr_sd", ctypes.c_float),
+        ("corr_med", ctypes.c_float),
     ]
     HOST_PHASES = ["extract", "iss", "describe", "match", "ransac", "icp", "map", "kp_eval"]
 

@@ -442,6 +442,9 @@ int ctx_normals_read(bshot_ctx* c, int m, float* out) {
 
 int ctx_normals_write(bshot_ctx* c, int size, int m, const float* slots) {
     if (size < 0 || m < 0 || m > size) return c->fail("normals state: bad sizes", BSHOT_EINVAL);
+    // a lookahead describe on the side stream reads and writes the array: it must have finished
+    // before the array is replaced (the caller drops its result, LidarOdometry::resetNormalsState)
+    HIPCHK(hipStreamSynchronize(c->side), "sync side stream");
     HIPCHK(c->normals.ensure(std::max(size, 1)), "alloc normals");
     if (m > 0) {
         HIPCHK(c->p_nrm.ensure(4 * (size_t)m), "alloc pinned normals");

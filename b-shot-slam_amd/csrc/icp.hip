@@ -85,11 +85,21 @@ __device__ __forceinline__ void icp_stream_level(const IcpGrids& G, int L, CandL
     else for_candidates(G.g[3], cs, qx, qy, qz, rs, rs2, f);
 }
 
+// The list's LDS sort row. The bitonic sort pads a list of n <= cap keys to the next power of two
+// P >= n (>= 64). Round 5's 384-entry experiment sized the row to cap (384) while P reached 512: the
+// pad's ~0 keys landed in the next wave's row, whose list then held key ~0 and loaded
+// tgt4[0xFFFFFFFF] (a GPU memory fault, session r05zb). The row is now the padded length itself,
+// ICP_LIST_ROW = the power of two >= max(cap, 64), and icp_build_list clamps P to the row it is
+// given, so no capacity can index past its own row.
+__host__ __device__ constexpr int icp_pow2_at_least(int x) { return x <= 64 ? 64 : 2 * icp_pow2_at_least((x + 1) / 2); }
+#define ICP_LIST_ROW (icp_pow2_at_least(ICP_LIST_CAP))
+static_assert(ICP_LIST_ROW >= ICP_LIST_CAP && (ICP_LIST_ROW & (ICP_LIST_ROW - 1)) == 0, "sort row");
+
 // Candidate list of source q (the whole wave) around its exact NN key m: every target within R of
 // q, R = d0 + {3000, 1500, 750, 350} mm (the largest whose count fits cap; d0 = the NN distance),
-// entries in ascending distance from q (sk: cap keys of LDS scratch for the sort): entry e at
-// dst[e * stride] (xyz, index bits) and its distance from q at dsd[e * stride]; *count = -1 (no
-// list) when even the smallest overflows or q is not finite. cap: a power of two.
+// entries in ascending distance from q (sk: ICP_LIST_ROW keys of LDS scratch for the sort, cap <=
+// ICP_LIST_ROW): entry e at dst[e * stride] (xyz, index bits) and its distance from q at
+// dsd[e * stride]; *count = -1 (no list) when even the smallest overflows or q is not finite.
 __device__ __forceinline__ void icp_build_list(const IcpGrids& G, CandLds* cs, float qx, float qy, float qz,
                                                unsigned long long m, const float4* __restrict__ tgt4, float4* dst,
                                                float* dsd, int stride, int cap, unsigned long long* sk, int* count_out,
@@ -131,10 +141,11 @@ __device__ __forceinline__ void icp_build_list(const IcpGrids& G, CandLds* cs, f
                 }
                 n += __popcll(bm);
             });
-            if (n <= cap) {
-                // ascending distance from q: a later scan stops at the first entry too far to matter
+            if (n <= cap && n <= ICP_LIST_ROW) {
+                // ascending distance from q: a later scan stops at the first entry too far to matter;
+                // the pad stays inside this wave's row (P <= ICP_LIST_ROW, a power of two >= n)
                 int P = 64;
-                while (P < n) P <<= 1;
+                while (P < n && P < ICP_LIST_ROW) P <<= 1;
                 for (int e = n + lane_id(); e < P; e += 64) sk[e] = ~0ull;
                 __builtin_amdgcn_wave_barrier();
                 wave_bitonic(sk, P);
@@ -208,7 +219,7 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
                                                               unsigned long long* __restrict__ best, int* done) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     __shared__ CandLds cl[ICP_WAVES];
-    __shared__ unsigned long long skl[ICP_WAVES][ICP_LIST_CAP];
+    __shared__ unsigned long long skl[ICP_WAVES][ICP_LIST_ROW];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     CandLds* cs = &cl[wave];
     cand_init(cs);
@@ -260,9 +271,6 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
 // list entries a lane loads per round trip of its scan (the wave waits for its longest scan; beside
 // the SHOT histogram the lists' lines come from the MALL, not the L2): 4 -> 16 cut the iterations'
 // wait 0.23 -> 0.19 ms per sweep (134 VGPRs; profiles/r05z_*)
-// the lists' LDS sorts are bitonic over ICP_LIST_CAP slots: a power of two (a 384-entry build hung
-// its GPU test, session r05zb)
-static_assert((ICP_LIST_CAP & (ICP_LIST_CAP - 1)) == 0, "ICP_LIST_CAP must be a power of two");
 #ifndef ICPH_BATCH
 #define ICPH_BATCH 16
 #endif
@@ -284,7 +292,7 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
     __shared__ float4 q_new[ICPH_THREADS];  // rebuilt lists: new centre (xyz) and radius (w)
     __shared__ int n_new[ICPH_THREADS];     // their counts; -2 = unchanged
     __shared__ int nq;
-    __shared__ unsigned long long skl[ICP_LIST_CAP];
+    __shared__ unsigned long long skl[ICP_LIST_ROW];
     const int lane = lane_id();
     cand_init(&cl);
     n_new[lane] = -2;
@@ -666,7 +674,7 @@ __global__ void __launch_bounds__(ICPR_THREADS) ICPR_ATTR k_icp_run(int ns, floa
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     extern __shared__ __attribute__((aligned(16))) float srec[];  // the stepping workgroup's records
     __shared__ CandLds cl[ICPR_WAVES];
-    __shared__ unsigned long long skl[ICPR_WAVES][ICP_LIST_CAP];
+    __shared__ unsigned long long skl[ICPR_WAVES][ICP_LIST_ROW];
     __shared__ float4 qq[ICPR_THREADS];
     __shared__ int nq, s_last, s_stop;
     __shared__ float sT[12];

@@ -4,6 +4,7 @@
 // proportional to N or K x neighbourhood runs in the gfx950 kernels through the context.
 #include "../../include/bshot/lidar_odometry.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -17,7 +18,10 @@
 
 namespace myslam {
 
-static void zero_stats(bshot_frame_stats& s) { std::memset(&s, 0, sizeof(s)); }
+static void zero_stats(bshot_frame_stats& s) {
+    std::memset(&s, 0, sizeof(s));
+    s.corr_n = -1;
+}
 
 // features of one sweep computed ahead of time on a worker thread (prefetchFrameDevice)
 // A2 top-K of a queued sweep (two ahead), computed on its own host thread as soon as the sweep's
@@ -114,6 +118,14 @@ void LidarOdometry::dropReady() {
     const bool external = ready_->external;  // another context's record: nothing to restore here
     ready_.reset();
     if (!external) check(bsh::ctx_normals_restore(ctx_), "restore normals");
+}
+
+void LidarOdometry::resetNormalsState(int size, int m, const float* slots) {
+    // the lookahead's describe (worker thread + side stream) ran over the array being replaced: join
+    // it and drop its result (its grids and SR stay valid, they do not read the normals), then write
+    joinAhead();
+    dropReady();
+    check(bsh::ctx_normals_write(ctx_, size, m, slots), "normals state");
 }
 
 void LidarOdometry::check(int rc, const char* where) {
@@ -651,12 +663,36 @@ void LidarOdometry::evaluateEstimation() {
     Matrix4f F;
     std::memcpy(F.m, Ticp, sizeof(Ticp));
     T_best_ = run_icp_ ? F * T_est : T_j;
-    if (evaluate_corr_ && !corr_.empty()) {
-        // correspondence distance statistics (:303-330): computed for the logs, not returned
+    stats_.corr_n = -1;
+    if (evaluate_corr_) {
+        // correspondence distance statistics (:303-330) over corr = the RANSAC inliers (:260):
+        // corr_cloud = cloud1 keypoints under T_best_ (evaluate_icp_) or T_j, as transformPointCloud
+        // does; pcl::geometry::distance = Eigen norm of the difference; float sums in corr order,
+        // divided by (float)size; median = sorted[size / 2]. The reference prints them (cout); here
+        // they go to bshot_frame_stats and the metrics JSON lines. With no inliers the reference
+        // divides 0 / 0 and reads an empty vector: NaN here.
         const Matrix4f& Tc = evaluate_icp_ ? T_best_ : T_j;
-        double acc = 0;
-        for (auto& c : corr_) acc += (Tc.transformPoint(cloud1_kps_[c.first]) - cloud2_kps_[c.second]).norm();
-        (void)acc;
+        const size_t n = corr_.size();
+        stats_.corr_n = (int)n;
+        if (n == 0) {
+            stats_.corr_avg = stats_.corr_sd = stats_.corr_med = NAN;
+        } else {
+            std::vector<float> dv;
+            dv.reserve(n);
+            float avg = 0;
+            for (auto& c : corr_) {
+                dv.push_back((Tc.transformPoint(cloud1_kps_[c.first]) - cloud2_kps_[c.second]).norm());
+                avg += dv.back();
+            }
+            avg = avg / (float)n;
+            float sd = 0;
+            for (float d : dv) sd += (d - avg) * (d - avg);
+            sd = std::sqrt(sd / (float)n);
+            std::sort(dv.begin(), dv.end());
+            stats_.corr_avg = avg;
+            stats_.corr_sd = sd;
+            stats_.corr_med = dv[n / 2];
+        }
     }
 }
 

@@ -75,7 +75,14 @@ void write_metrics(bshot_odom* o, const bshot_frame_stats& s, double wall_ms) {
                  std::isfinite(s.t_diff) ? (double)s.t_diff : -1.0, s.map_size, wall_ms, s.host_ms[0], s.host_ms[1],
                  s.host_ms[2], s.host_ms[3], s.host_ms[4], s.host_ms[5], s.host_ms[6], s.host_ms[7]);
     for (int i = 0; i < 12; ++i) std::fprintf(o->metrics, i ? ", %.9g" : "%.9g", (double)s.pose[i]);
-    std::fprintf(o->metrics, "]}\n");
+    std::fprintf(o->metrics, "]");
+    if (s.corr_n >= 0) {
+        // evaluate_corr_ (src/lidar_odometry.cpp:303-330): "Corr num", "Corr avg dist", "Corr SD dist", "Corr med"
+        auto num = [](float v) { return std::isfinite(v) ? (double)v : -1.0; };
+        std::fprintf(o->metrics, ", \"corr\": {\"n\": %d, \"avg_mm\": %.9g, \"sd_mm\": %.9g, \"med_mm\": %.9g}", s.corr_n,
+                     num(s.corr_avg), num(s.corr_sd), num(s.corr_med));
+    }
+    std::fprintf(o->metrics, "}\n");
     std::fflush(o->metrics);
 }
 
@@ -100,9 +107,10 @@ int run_frame(bshot_odom* o, const float* xyz, const float* d_xyz, int n, bshot_
     const int K = lo.params().num_keypoints;
     if (o->shard_owner && !ex) {
         // a sweep the chain owner extracts itself (a record was refused): its describe must start from
-        // the sequence's normals state, not from whatever this context last described
-        if (bsh::ctx_normals_write(lo.context(), o->seq_size, (int)(o->seq_nrm.size() / 4), o->seq_nrm.data()) < 0)
-            throw std::runtime_error(std::string("normals state: ") + bshot_last_error(lo.context()));
+        // the sequence's normals state, not from whatever this context last described -- including a
+        // lookahead describe the caller's set_next_device started on this context over its own array
+        // (joined and dropped first, so it is neither adopted nor still writing the array)
+        lo.resetNormalsState(o->seq_size, (int)(o->seq_nrm.size() / 4), o->seq_nrm.data());
     }
     myslam::Frame::Ptr f = myslam::Frame::createFrame();
     if (xyz) {
@@ -236,6 +244,16 @@ const char* bshot_odom_last_error(const bshot_odom* o) { return o ? o->err.c_str
 
 int bshot_odom_set_option(bshot_odom* o, const char* name, int value) {
     if (!o || !name) return BSHOT_EINVAL;
+    // the two evaluation switches of the reference's class (include/lidar_odometry.h:48-49,
+    // test/odometry_test.cpp:107-108); everything else is a context knob
+    if (!std::strcmp(name, "eval_corr")) {
+        o->lo->setEvaluateCorr(value != 0);
+        return BSHOT_OK;
+    }
+    if (!std::strcmp(name, "eval_icp")) {
+        o->lo->setEvaluateICP(value != 0);
+        return BSHOT_OK;
+    }
     return bshot_set_option(o->lo->context(), name, value);
 }
 

@@ -90,8 +90,11 @@ struct bshot_xchg {
     hipEvent_t ev_inserted = nullptr;  // the replica inserts reading the log (or recv) are done (their stream)
     bool inserts_queued = false;
     bshot_ctx* jc = nullptr;  // the context whose replicas the log feeds
-    // the exchange call and a replica reader (quiesce, from another thread of the caller's) both index
-    // the log: mu guards the log and the insert queueing
+    // Threading: a context is driven by one host thread at a time (bshot_abi.h), and so are the
+    // exchange feeding its replicas and the replica readers (bshot_odom_gpu_replica_*, which index the
+    // log through quiesce): a reader on another thread while an exchange runs is not supported -- the
+    // next exchange's inserts may grow (reallocate) a replica's pools under the reader's query kernel
+    // (ADVICE r05). mu only orders the log against bshot_xchg_destroy and the context's detach.
     std::mutex mu;
 };
 

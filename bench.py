@@ -42,9 +42,10 @@ def pmc_kernel(stage, path=None):
     separate passes) and, where collected, the SQ / TCC / TCP derived metrics."""
     import glob
     import re
-    # the default configuration's sets only (rNN<letter>_pmc.json; config sets carry a suffix: r04c_c5)
+    # the default configuration's sets only (rNN<letters>_pmc.json, e.g. r05x, r05za; config sets carry
+    # a suffix: r04c_c5), newest last
     files = [path] if path else sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
-                                       if re.fullmatch(r"r\d\d[a-z]?_pmc\.json", os.path.basename(f)))
+                                       if re.fullmatch(r"r\d\d[a-z]*_pmc\.json", os.path.basename(f)))
     if not files:
         return None, None
     try:

@@ -44,6 +44,10 @@ class LidarOdometry {
     // wait until the lookahead work in flight (worker, queue and top-K threads) has been issued and
     // finished on the host; the prefetched results stay ready for adoption
     void drainLookahead();
+    // replace the persistent normals array (include/bshot_bits.h:58-87) by a sequence's state
+    // (logical size, slots [0, m)); a pending lookahead describe is joined and dropped first.
+    // Extension: the frame-sharded chain owner's own extraction (bshot_odom_process_record)
+    void resetNormalsState(int size, int m, const float* slots);
     void extractKeypoints();
     void computeDescriptors();
     void featureMatching();

@@ -190,6 +190,13 @@ typedef struct {
     /* host wall ms per phase (TicToc, include/tic_toc.h): extract(SR+topK), iss, describe,
        match (map query + Hamming), ransac, icp, map update, kp_eval */
     float host_ms[8];
+    /* setEvaluateCorr(true) (bshot_odom option "eval_corr" 1): the reference's correspondence
+       statistics (src/lidar_odometry.cpp:303-330) over the RANSAC inliers, each cloud1 keypoint
+       under T_best (setEvaluateICP, option "eval_icp" 1, the default) or the RANSAC transform:
+       count, float mean, SD and the sorted median at size/2 of pcl::geometry::distance; NaN with no
+       inliers. corr_n = -1 (and the rest 0) when not evaluated. */
+    int corr_n;
+    float corr_avg, corr_sd, corr_med;
 } bshot_frame_stats;
 
 int bshot_odom_create(bshot_odom** out, int device, const bshot_params* p);
@@ -234,7 +241,9 @@ int bshot_odom_exchange(bshot_odom* o, bshot_xchg* x, int include_self);
  * nranks + peers - 1), the per-sweep insert work of a job with nranks + peers ranks */
 int bshot_odom_exchange_sim(bshot_odom* o, bshot_xchg* x, int peers);
 /* GPU replica of rank r's map: entry count (syncs), and its entries around pos within range (the
- * reference's block loop; libstdc++ order) -> xyz (n x 3), bits (n x 11); count or -needed */
+ * reference's block loop; libstdc++ order) -> xyz (n x 3), bits (n x 11); count or -needed.
+ * Call them from the thread that drives the odometry and its exchange (between two sweeps), never
+ * concurrently with bshot_odom_exchange: an exchange may grow a replica while it is read. */
 int bshot_odom_gpu_replica_size(bshot_odom* o, int replica);
 /* host records (bshot_odom_map_delta's layout) into GPU replica r, for transports other than RCCL */
 int bshot_odom_gpu_replica_insert(bshot_odom* o, int replica, const float* rec, int n);

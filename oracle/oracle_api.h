@@ -29,6 +29,8 @@ typedef struct {
     int run_iss;            /* 1 (ISS runs every frame, :164-170) */
     int map_canonical;      /* 0: map blocks in libstdc++ unordered_map order (the reference); 1: in
                                first-insert order (the GPU map's canonical mode, not the reference's) */
+    int eval_icp;           /* 1     setEvaluateICP (test/odometry_test.cpp:108): the corr statistics use
+                               T_best_ (1) or the RANSAC transform (0), src/lidar_odometry.cpp:306-309 */
 } oracle_params;
 
 typedef struct {
@@ -38,6 +40,11 @@ typedef struct {
     float pose[16];
     int map_size;
     float repeat_sr, repeat_iss; /* kpEvaluation rates (src/lidar_odometry.cpp:392-445) */
+    /* evaluate_corr_ statistics (src/lidar_odometry.cpp:303-330), always computed here: count of
+       RANSAC inliers, float mean, SD and sorted median (at size/2) of their distances after the
+       transform; NaN when there are none */
+    int corr_n;
+    float corr_avg, corr_sd, corr_med;
 } oracle_frame_stats;
 
 int oracle_seg_ratio(const float* xyz, int n, float radius, int max_nn, int sr_type, int32_t* idx_out,

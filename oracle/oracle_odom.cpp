@@ -2,6 +2,7 @@
 // CPU restatement of the per-frame odometry loop: LidarOdometry (src/lidar_odometry.cpp:29-445),
 // Keypoint (src/keypoint.cpp:23-32), Map (include/mymap.h:9-51, src/mymap.cpp:4-105) and the
 // headless frame loop of test/odometry_test.cpp:159-180 / test/kp_test.cpp:159-181.
+#include <algorithm>
 #include <bitset>
 #include <cmath>
 #include <cstring>
@@ -204,6 +205,33 @@ class OOdom {
 
     void pass_src2ref() { ref = src; iss_ref = iss_src; }
 
+    void corr_stats(const float T[16], oracle_frame_stats* st) const {
+        const size_t n = inl_q.size();
+        st->corr_n = (int)n;
+        if (n == 0) {
+            st->corr_avg = st->corr_sd = st->corr_med = NAN;
+            return;
+        }
+        std::vector<float> dv;
+        dv.reserve(n);
+        float avg = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const P3 a = xf(T, src->kps[inl_q[i]]);
+            const P3& b = c2kps[inl_m[i]];
+            const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+            dv.push_back(std::sqrt(dx * dx + (dy * dy + dz * dz)));
+            avg += dv.back();
+        }
+        avg = avg / (float)n;
+        float sd = 0;
+        for (size_t i = 0; i < n; ++i) sd += (dv[i] - avg) * (dv[i] - avg);
+        sd = std::sqrt(sd / (float)n);
+        std::sort(dv.begin(), dv.end());
+        st->corr_avg = avg;
+        st->corr_sd = sd;
+        st->corr_med = dv[n / 2];
+    }
+
     int process(const float* xyz, int n, oracle_frame_stats* st) {
         std::memset(st, 0, sizeof(*st));
         auto f = std::make_shared<OFrame>();
@@ -303,6 +331,10 @@ class OOdom {
         st->icp_iters = iters;
         if (p.run_icp) mul44(Ticp, T_est, T_best);
         else std::memcpy(T_best, ransac_T, sizeof(T_best));
+        // ---- evaluate_corr_ (:303-330): corr = the RANSAC inliers (:260), corr_cloud = cloud1
+        // keypoints under T_best_ (evaluate_icp_) or T_j; pcl::geometry::distance = Eigen norm of the
+        // difference (a0 + (a1 + a2), then sqrt); float sums in corr order, divided by (float)size
+        corr_stats(p.eval_icp ? T_best : ransac_T, st);
         // ---- kpEvaluation (kp_test only; cheap) (:392-445)
         st->repeat_sr = repeat_rate(src->kps, ref->kps);
         st->repeat_iss = repeat_rate(iss_src, iss_ref);
@@ -344,7 +376,7 @@ void oracle_default_params(oracle_params* p) {
     p->iss_salient = 60.f; p->iss_nonmax = 40.f; p->iss_gamma21 = 0.975; p->iss_gamma32 = 0.975; p->iss_min_nn = 5;
     p->normal_radius = 3000.f; p->normal_max_nn = 300; p->shot_radius = 3000.f; p->map_range = 100000.f;
     p->ransac_max_iter = 2000; p->ransac_thresh = 1500.0; p->icp_max_iter = 10; p->run_icp = 1; p->run_iss = 1;
-    p->map_canonical = 0;
+    p->map_canonical = 0; p->eval_icp = 1;
 }
 void* oracle_odom_create(const oracle_params* p) { return new OOdom(*p); }
 void oracle_odom_destroy(void* h) { delete static_cast<OOdom*>(h); }

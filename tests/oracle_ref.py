@@ -22,7 +22,7 @@ class OParams(ctypes.Structure):
         ("normal_radius", ctypes.c_float), ("normal_max_nn", ctypes.c_int), ("shot_radius", ctypes.c_float),
         ("map_range", ctypes.c_float), ("ransac_max_iter", ctypes.c_int), ("ransac_thresh", ctypes.c_double),
         ("icp_max_iter", ctypes.c_int), ("run_icp", ctypes.c_int), ("run_iss", ctypes.c_int),
-        ("map_canonical", ctypes.c_int),
+        ("map_canonical", ctypes.c_int), ("eval_icp", ctypes.c_int),
     ]
 
 
@@ -34,6 +34,8 @@ class OStats(ctypes.Structure):
         ("h_diff", ctypes.c_float), ("t_diff", ctypes.c_float), ("T_ransac", ctypes.c_float * 16),
         ("pose", ctypes.c_float * 16), ("map_size", ctypes.c_int), ("repeat_sr", ctypes.c_float),
         ("repeat_iss", ctypes.c_float),
+        ("corr_n", ctypes.c_int), ("corr_avg", ctypes.c_float), ("corr_sd", ctypes.c_float),
+        ("corr_med", ctypes.c_float),
     ]
 
 

@@ -65,6 +65,49 @@ def test_oracle_reproduces_sequence_fixture(seq):
         assert np.array_equal(q, seq[f"inl_q_{f}"]) and np.array_equal(m, seq[f"inl_m_{f}"])
 
 
+def corr_stats_restated(kps, tgt, q, m, T):
+    """evaluate_corr_ (src/lidar_odometry.cpp:303-330) restated in numpy float32, independently of the
+    oracle: pcl::transformPointCloud's ((m00 x + m01 y) + m02 z) + m03 per row, Eigen's
+    squaredNorm order a0 + (a1 + a2), float sums in corr order divided by (float)size, median at
+    size / 2 of the sorted distances."""
+    f32 = np.float32
+    T = np.asarray(T, np.float32).reshape(4, 4)
+    dv = []
+    avg = f32(0)
+    for i, j in zip(q, m):
+        p = kps[i]
+        a = [((T[r, 0] * p[0] + T[r, 1] * p[1]) + T[r, 2] * p[2]) + T[r, 3] for r in range(3)]
+        d = [f32(a[r] - tgt[j][r]) for r in range(3)]
+        dist = f32(np.sqrt(d[0] * d[0] + (d[1] * d[1] + d[2] * d[2])))
+        dv.append(dist)
+        avg = f32(avg + dist)
+    n = len(dv)
+    if n == 0:
+        return 0, np.nan, np.nan, np.nan
+    avg = f32(avg / f32(n))
+    sd = f32(0)
+    for dist in dv:
+        sd = f32(sd + (dist - avg) * (dist - avg))
+    sd = f32(np.sqrt(f32(sd / f32(n))))
+    return n, avg, sd, sorted(dv)[n // 2]
+
+
+@pytest.mark.parametrize("eval_icp", [1, 0])
+def test_oracle_corr_stats_match_restatement(seq, eval_icp):
+    """The oracle's evaluate_corr_ statistics against the numpy restatement above, on the 3-frame
+    sequence fixture (T_best_ with eval_icp, the RANSAC transform without)."""
+    od = orc.Odometry(orc.params(num_keypoints=int(seq["k"]), eval_icp=eval_icp))
+    for f in range(3):
+        st = od.process(seq[f"xyz_{f}"])
+        q, m = od.inliers()
+        tgt, _ = od.target()
+        T = np.array(st.pose if eval_icp else st.T_ransac, np.float32)
+        n, avg, sd, med = corr_stats_restated(od.keypoints(), tgt, q, m, T)
+        assert st.corr_n == n == len(q), f
+        got = np.array([st.corr_avg, st.corr_sd, st.corr_med], np.float32)
+        assert np.array_equal(_u(got), _u(np.array([avg, sd, med], np.float32))), (f, got, avg, sd, med)
+
+
 # ----------------------------------------------------------------------------- product (GPU)
 @pytest.mark.gpu
 def test_gpu_reproduces_stage_fixture(stages):

@@ -70,6 +70,44 @@ def test_odometry_no_icp_no_iss():
     _run_pair(range(3), run_icp=0, run_iss=0)
 
 
+@pytest.mark.parametrize("eval_icp", [1, 0])
+def test_evaluate_corr_stats_match_oracle(eval_icp):
+    """setEvaluateCorr(true) (src/lidar_odometry.cpp:303-330): the count, mean, SD and median of the
+    RANSAC inliers' distances under T_best_ (setEvaluateICP true) or the RANSAC transform, bit for
+    bit against the oracle, also in the metrics JSON lines; off (the default) they are not evaluated."""
+    import json
+    import os
+    import tempfile
+
+    kw = dict(num_keypoints=1024)
+    od = bshot_py.Odometry(0, bshot_py.default_params(**kw))
+    oo = orc.Odometry(orc.params(eval_icp=eval_icp, **kw))
+    path = os.path.join(tempfile.mkdtemp(), "m.jsonl")
+    try:
+        od.set_metrics_file(path)
+        for f in range(4):
+            xyz, _ = bshot_py.synth_sweep(30 + f)
+            if f == 1:
+                od.set_option("eval_corr", 1)
+                od.set_option("eval_icp", eval_icp)
+            st = od.process(xyz)
+            so = oo.process(xyz)
+            if f == 0:
+                assert st.corr_n == -1
+                continue
+            assert st.n_inliers == so.n_inliers and st.corr_n == so.corr_n == so.n_inliers, f
+            a = np.array([st.corr_avg, st.corr_sd, st.corr_med], np.float32)
+            b = np.array([so.corr_avg, so.corr_sd, so.corr_med], np.float32)
+            assert np.array_equal(_u(a), _u(b)), (f, a, b)
+        od.set_metrics_file(None)
+        lines = [json.loads(x) for x in open(path)]
+        assert len(lines) == 4 and "corr" not in lines[0]
+        assert lines[-1]["corr"]["n"] == st.corr_n
+        assert np.float32(lines[-1]["corr"]["med_mm"]) == np.float32(st.corr_med)
+    finally:
+        od.close()
+
+
 @pytest.mark.parametrize("depth,opts", [(1, {}), (2, {}), (2, {"topk_thread": 0}), (2, {"ransac_dev": 0}),
                                         (2, {"map_sync": 0}), (2, {"iss_defer": 1})])
 def test_odometry_lookahead_device_frames(depth, opts):

@@ -80,12 +80,15 @@ def _check(f, st, so, owner, oo):
     assert np.array_equal(_u(np.array(st.pose)), _u(np.array(so.pose))), f
 
 
-@pytest.mark.parametrize("W", [1, 2, 3])
-def test_frame_sharded_short_sweeps_match_oracle(W):
+@pytest.mark.parametrize("W,owner_next", [(1, 0), (2, 0), (3, 0), (2, 1)])
+def test_frame_sharded_short_sweeps_match_oracle(W, owner_next):
     """Sweeps with fewer than K keypoints in the middle of the sequence: with one
     extracting context every record is accepted (its stale slots are the sequence's); with W > 1
     the owner refuses the short sweeps' records and extracts them itself, and the whole chain still
-    equals the oracle's sequential run bit for bit."""
+    equals the oracle's sequential run bit for bit. owner_next: the caller also gives the owner the
+    next sweep (set_next_device), so the owner's context describes a lookahead over its own normals
+    array; a refused sweep's own extraction must join and drop it before restoring the sequence's
+    state, not adopt it."""
     import torch
     from test_edge_gpu import small_frame
 
@@ -111,6 +114,8 @@ def test_frame_sharded_short_sweeps_match_oracle(W):
                 recs[f] = ex[r].extract_device(dev[f].data_ptr(), len(xyzs[f]))
             ex[r].drain()
         for f in range(F):
+            if owner_next and f + 1 < F:
+                owner.set_next_device(dev[f + 1].data_ptr(), len(xyzs[f + 1]))
             try:
                 st = owner.process_record(recs[f])
             except bshot_py.BshotError as e:
