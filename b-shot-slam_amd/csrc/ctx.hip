@@ -215,7 +215,8 @@ static int cloud_sr(bshot_ctx* c, CloudState& s, hipStream_t st) {
     if (n > 0) {
         const int sg2 = c->stage_begin(BSHOT_STAGE_SR, st);
         HIPCHK(launch_seg_ratio(s.ladder, c->ladder_mode(s), s.pts4.p, n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks, c->opt_sr_xcd_chunk),
+                                c->opt_sr_start, s.ratio.p, s.errw.p, st, nullptr, c->opt_sr_blocks, c->opt_sr_xcd_chunk,
+                                c->opt_sr_run, (float)c->opt_sr_bratio / 100.f),
                "seg_ratio launch");
         c->stage_end(sg2, st);
     }
@@ -1301,7 +1302,8 @@ int bshot_debug_knn_stats(bshot_ctx* c, int64_t* out, int n) {
     HIPCHK(c->cs.ratio.ensure(c->cs.n), "alloc ratio");
     HIPCHK(hipMemsetAsync(k.p, 0, 32 * sizeof(unsigned long long), c->stream), "memset");
     HIPCHK(launch_seg_ratio(c->cs.ladder, c->ladder_mode(c->cs), c->cs.pts4.p, c->cs.n, c->prm.seg_radius, c->prm.seg_max_nn, c->prm.sr_type,
-                            c->opt_sr_start, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p, c->opt_sr_blocks, c->opt_sr_xcd_chunk),
+                            c->opt_sr_start, c->cs.ratio.p, c->cs.errw.p, c->stream, k.p, c->opt_sr_blocks, c->opt_sr_xcd_chunk,
+                                c->opt_sr_run, (float)c->opt_sr_bratio / 100.f),
            "seg_ratio (stats)");
     unsigned long long h[32];
     HIPCHK(hipMemcpyAsync(h, k.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
@@ -1324,6 +1326,8 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "ladder_front") c->opt_ladder_front = value ? 1 : 0;
     else if (k == "sr_blocks") c->opt_sr_blocks = value < 0 ? 0 : value;
     else if (k == "sr_xcd_chunk") c->opt_sr_xcd_chunk = value < 0 ? 0 : value;
+    else if (k == "sr_run") c->opt_sr_run = value < 1 ? 1 : value;
+    else if (k == "sr_bratio") c->opt_sr_bratio = value < 101 ? 101 : value;
     else if (k == "icp_device") c->opt_icp_device = value ? 1 : 0;
     else if (k == "icp_host_delay_ms") c->opt_icp_host_delay_ms = value < 0 ? 0 : value;
     else if (k == "diag_skip_icp") c->opt_diag_skip_icp = value ? 1 : 0;  // diagnostic: the period without ICP

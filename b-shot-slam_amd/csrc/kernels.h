@@ -22,7 +22,8 @@ hipError_t kfill(void* dst, unsigned char value, size_t bytes, hipStream_t s);
 int knn_max_nn();
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst = nullptr, int max_blocks = 8192, int xcd_chunk = 0);
+                            unsigned long long* kst = nullptr, int max_blocks = 8192, int xcd_chunk = 0, int run = 1,
+                            float bratio = 2.83f);
 hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float4* pts4, const float* kps, int k,
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,

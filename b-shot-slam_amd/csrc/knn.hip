@@ -191,9 +191,10 @@ __device__ __forceinline__ float bucket_radius(float rs, int b) {
 }
 
 template <bool DIAG>
-__device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
-                           int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
-                           unsigned long long ts1, const unsigned long long** sorted);
+__device__ __forceinline__ bool knn_finish(const GridView& g, KnnLds* L, float qx, float qy, float qz, float rs, float rs2,
+                                           int max_nn, int total, int* need_out, unsigned long long* kst,
+                                           unsigned long long chunks, unsigned long long ts1,
+                                           const unsigned long long** sorted);
 
 // Exact selection: leaves the `*need` nearest (d2, idx) sorted in (*sorted)[0, *need).
 // Returns false when > KNN_CAP keys tie at the boundary after 3 refinement levels (reported).
@@ -205,11 +206,16 @@ __device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, flo
 // in LDS (ballot compaction), so when they fit (<= KNN_CAP) the selection is a histogram of that
 // list plus a counting sort over LDS only -- no second pass over the candidates.
 // start_step: first ladder step tried (any step is exact; a later start only costs work);
-// *step_out: the step whose radius delivered the result; *total_out: in-radius count there.
+// rb > 0 (round 6): a radius known to hold >= max_nn points (an earlier query's
+// exact max_nn-th distance plus the distance between the two queries, k_seg_ratio's runs): one pass
+// at rb on the grid whose cell is >= rb / bratio replaces the ladder; if it holds fewer (float
+// slack, or a bound that does not hold), the ladder continues from the first step beyond rb. Exact
+// either way: the selection only needs a ball of radius <= r with >= max_nn points inside.
+// *kth_d2: d2 of the max_nn-th neighbour (the next query's bound), -1 when fewer than max_nn lie within r.
 template <bool DIAG>
 __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn,
-                           int start_step, int* need_out, int* step_out, int* total_out, unsigned long long* kst,
-                           const unsigned long long** sorted) {
+                           int start_step, float rb, float bratio, int* need_out, float* kth_d2,
+                           unsigned long long* kst, const unsigned long long** sorted) {
     unsigned long long chunks = 0, chunks_before = 0;
     const int lane = lane_id();
     unsigned long long ts0 = 0ull;
@@ -217,19 +223,33 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
     const float r2 = (float)((double)r * (double)r);
     float rs = r, rs2 = r2;
     int total = 0;
-    int step = start_step;
     const int last = lg.nsteps - 1;
+    int step = start_step;
     if (step > last) step = last;
+    int gl = lg.gi[step];
+    int blev = 3;  // the bounded pass's grid: the finest whose cell is >= rb / bratio
+    if (rb > 0.f && rb < r) {
+        step = -1;
+        for (int l = 2; l >= 0; --l)
+            if (rb <= bratio * lg.g[l].cell) blev = l;
+    }
     for (; step <= last; ++step) {
-        rs = step == last ? r : r * lg.frac[step];
-        rs2 = step == last ? r2 : (float)((double)rs * (double)rs);
+        if (step < 0) {
+            rs = rb;
+            rs2 = (float)((double)rb * (double)rb);
+            gl = blev;
+        } else {
+            rs = step == last ? r : r * lg.frac[step];
+            rs2 = step == last ? r2 : (float)((double)rs * (double)rs);
+            gl = lg.gi[step];
+        }
         const float sc = (float)KNN_NB / rs2;
         int cnt = 0;
         // keys past the LDS list are counted into the level-0 histogram as they stream (the list's
         // own keys join it afterwards, knn_finish): a step that overflows needs no extra pass for it
         hist_clear(L);
         // a step whose cube holds fewer than max_nn candidates cannot deliver: skipped unstreamed
-        const bool went = for_candidates(lg.g[lg.gi[step]], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
+        const bool went = for_candidates(lg.g[gl], &L->cand, qx, qy, qz, rs, rs2, [&](bool v, float d2, unsigned int idx) {
             if constexpr (DIAG) ++chunks;
             const unsigned long long m = __ballot(v);
             if (v) {
@@ -244,6 +264,7 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
         total = cnt;
         if constexpr (DIAG) {
             if (!went && lane == 0) atomicAdd(&kst[6], 1ull);
+            if (step < 0 && lane == 0) atomicAdd(&kst[total >= max_nn ? 27 : 28], 1ull);
         }
         if (total >= max_nn) break;
         if constexpr (DIAG) {
@@ -253,37 +274,39 @@ __device__ __forceinline__ bool knn_select(const LadderGrids& lg, KnnLds* L, flo
             }
             chunks_before = chunks;
         }
+        if (step < 0) {
+            // the bound did not deliver: the ladder from its first step beyond rb
+            int s0 = 0;
+            while (s0 < last && r * lg.frac[s0] <= rb) ++s0;
+            step = s0 - 1;
+        }
     }
-    if (step > last) step = last;
-    *step_out = step;
-    *total_out = total;
     unsigned long long ts1 = 0ull;
     if constexpr (DIAG) {
         ts1 = cycle_stamp();
         if (lane == 0) {
             atomicAdd(&kst[12], ts1 - ts0);
             atomicAdd(&kst[0], 1ull);
-            atomicAdd(&kst[16 + step], 1ull);
+            if (step >= 0) atomicAdd(&kst[16 + (step > last ? last : step)], 1ull);
             atomicAdd(&kst[9], (unsigned long long)(total < max_nn ? total : max_nn));
             atomicAdd(&kst[10], (unsigned long long)total);
         }
     }
-    return knn_finish<DIAG>(lg, L, qx, qy, qz, r, max_nn, step, total, need_out, kst, chunks, ts1, sorted);
+    const bool ok = knn_finish<DIAG>(lg.g[gl], L, qx, qy, qz, rs, rs2, max_nn, total, need_out, kst, chunks, ts1, sorted);
+    *kth_d2 = -1.f;
+    if (ok && total >= max_nn) *kth_d2 = __uint_as_float((unsigned)((*sorted)[max_nn - 1] >> 32));
+    return ok;
 }
 
-// The selection once a ladder step has delivered (>= max_nn keys in radius, or the last step):
-// L->list holds that step's first KNN_CAP in-radius keys, in any candidate order (the result does
-// not depend on it).
+// The selection once a ladder step (radius rs, rs2 = its square, streamed on grid g) has delivered
+// (>= max_nn keys in radius, or the last step): L->list holds that step's first KNN_CAP in-radius
+// keys, in any candidate order (the result does not depend on it).
 template <bool DIAG>
-__device__ __forceinline__ bool knn_finish(const LadderGrids& lg, KnnLds* L, float qx, float qy, float qz, float r, int max_nn, int step,
-                           int total, int* need_out, unsigned long long* kst, unsigned long long chunks,
-                           unsigned long long ts1, const unsigned long long** sorted) {
+__device__ __forceinline__ bool knn_finish(const GridView& g, KnnLds* L, float qx, float qy, float qz, float rs, float rs2,
+                                           int max_nn, int total, int* need_out, unsigned long long* kst,
+                                           unsigned long long chunks, unsigned long long ts1,
+                                           const unsigned long long** sorted) {
     const int lane = lane_id();
-    const int last = lg.nsteps - 1;
-    const float r2 = (float)((double)r * (double)r);
-    const float rs = step == last ? r : r * lg.frac[step];
-    const float rs2 = step == last ? r2 : (float)((double)rs * (double)rs);
-    const GridView& g = lg.g[lg.gi[step]];
     const int need = total < max_nn ? total : max_nn;
     *need_out = need;
     if (need == 0) return true;
@@ -609,16 +632,18 @@ template <bool DIAG>
 __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrids lg, const float4* __restrict__ pts4, int n,
                                                               float radius, int max_nn, int sr_type, int hint,
                                                               float* __restrict__ ratio, int* __restrict__ err,
-                                                              unsigned long long* __restrict__ kst, int zc) {
+                                                              unsigned long long* __restrict__ kst, int zc, int run,
+                                                              float bratio) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // the wave index in an SGPR: the wave's LDS base is then rematerialised, not held in a VGPR
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     KnnLds* L = reinterpret_cast<KnnLds*>(smem) + wave;
     cand_init(&L->cand);
     const int nw = gridDim.x * KNN_WAVES;
+    const int nu = (n + run - 1) / run;  // runs of `run` consecutive cell-order queries, one per wave pass
     const float4* __restrict__ order = lg.g[0].spts;
     float* fl = reinterpret_cast<float*>(L->list);
-    int j0 = blockIdx.x * KNN_WAVES + wave;
+    int u0 = blockIdx.x * KNN_WAVES + wave;
     if (zc > 0) {
         // XCD-local chunks of cell order: workgroups b, b + 8, ... share an XCD (the dispatcher deals
         // workgroups round-robin over the 8 XCDs), so the workgroups of label g = b % 8 take chunks
@@ -627,37 +652,57 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) SR_ATTR k_seg_ratio(LadderGrid
         // chunk's neighbourhood instead of all eight holding the same one
         const int g = blockIdx.x & 7, i = blockIdx.x >> 3;
         const int m = i / zc, o = i - m * zc;
-        j0 = ((m * 8 + g) * zc + o) * KNN_WAVES + wave;
+        u0 = ((m * 8 + g) * zc + o) * KNN_WAVES + wave;
     }
-    for (int j = j0; j < n; j += nw) {
-        const float4 sp = order[j];
-        const int q = (int)__float_as_uint(sp.w);
-        float out = __builtin_nanf("");
-        const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
-        const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
-        if (!origin && fin) {
-            int need = 0, used = 0, tot = 0;
-            const unsigned long long* sorted = nullptr;
-            const int start = hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
-            const bool ok = knn_select<DIAG>(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, &need, &used, &tot, kst, &sorted);
-            unsigned long long tm0 = 0ull;
-            if constexpr (DIAG) tm0 = cycle_stamp();
-            if (!ok) {
-                if (lane == 0) atomicOr(err, 1);
-            } else if (need > 0) {
+    for (int u = u0; u < nu; u += nw) {
+        // the run's queries chain their radii: the exact max_nn-th distance of the previous query
+        // (pr, at pp) bounds this one's by pr + |q - pp| (triangle inequality), so after the first
+        // query of a run each streams one ball barely larger than its own max_nn-NN ball instead of
+        // the sqrt(2) radius ladder (consecutive cell-order queries lie a few cm apart)
+        float pr = -1.f;
+        float4 pp = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int jend = (u + 1) * run < n ? (u + 1) * run : n;
+        for (int j = u * run; j < jend; ++j) {
+            const float4 sp = order[j];
+            const int q = (int)__float_as_uint(sp.w);
+            float out = __builtin_nanf("");
+            const bool origin = sp.x == 0.f && sp.y == 0.f && sp.z == 0.f;
+            const bool fin = __builtin_isfinite(sp.x) && __builtin_isfinite(sp.y) && __builtin_isfinite(sp.z);
+            if (!origin && fin) {
+                int need = 0;
+                float kd2 = -1.f;
+                const unsigned long long* sorted = nullptr;
+                float rb = 0.f;
+                if (pr >= 0.f) {
+                    // relative 1e-5 and 0.01 mm of slack over the float rounding of both distances;
+                    // exactness does not depend on it (a ball holding fewer than max_nn falls back)
+                    const double dx = (double)sp.x - pp.x, dy = (double)sp.y - pp.y, dz = (double)sp.z - pp.z;
+                    rb = (float)((sqrt((double)pr) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-5) + 0.01);
+                }
+                const int start = rb == 0.f && hint > 0 ? ladder_start(lg, sp.x, sp.y, sp.z, radius, max_nn, hint) : 0;
+                const bool ok = knn_select<DIAG>(lg, L, sp.x, sp.y, sp.z, radius, max_nn, start, rb, bratio, &need, &kd2,
+                                                 kst, &sorted);
+                pr = kd2;
+                pp = sp;
+                unsigned long long tm0 = 0ull;
+                if constexpr (DIAG) tm0 = cycle_stamp();
+                if (!ok) {
+                    if (lane == 0) atomicOr(err, 1);
+                } else if (need > 0) {
 #if SR_DIAG_NOFIN
-                out = (float)need;  // diagnostic builds only: the selection without the ratio
+                    out = (float)need;  // diagnostic builds only: the selection without the ratio
 #else
-                out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
+                    out = sr_of_neighbours(sorted, pts4, need, fl, sp, sr_type);
 #endif
+                }
+                if constexpr (DIAG) {
+                    const unsigned long long tm1 = cycle_stamp();
+                    if (lane == 0) atomicAdd(&kst[15], tm1 - tm0);
+                }
             }
-            if constexpr (DIAG) {
-                const unsigned long long tm1 = cycle_stamp();
-                if (lane == 0) atomicAdd(&kst[15], tm1 - tm0);
-            }
+            if (lane == 0) ratio[q] = out;
+            __builtin_amdgcn_wave_barrier();
         }
-        if (lane == 0) ratio[q] = out;
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -677,9 +722,10 @@ __global__ void __launch_bounds__(64 * KNN_WAVES) k_normals(LadderGrids lg, cons
         const float kx = kps[3 * q], ky = kps[3 * q + 1], kz = kps[3 * q + 2];
         float nx = qn, ny = qn, nz = qn, curv = qn;
         if (__builtin_isfinite(kx) && __builtin_isfinite(ky) && __builtin_isfinite(kz)) {
-            int need = 0, used = 0, tot = 0;
+            int need = 0;
+            float kd2;
             const unsigned long long* sorted = nullptr;
-            if (!knn_select<false>(lg, L, kx, ky, kz, radius, max_nn, 0, &need, &used, &tot, nullptr, &sorted)) {
+            if (!knn_select<false>(lg, L, kx, ky, kz, radius, max_nn, 0, 0.f, 0.f, &need, &kd2, nullptr, &sorted)) {
                 if (lane == 0) atomicOr(err, 2);
             } else if (need > 0) {
                 if (need >= 3) {
@@ -758,29 +804,31 @@ static LadderGrids ladder(const DevGrid* const* g4, int mode) {
 
 hipError_t launch_seg_ratio(const DevGrid* const* g4, int ladder_mode, const float4* pts4, int n, float radius,
                             int max_nn, int sr_type, int hint, float* ratio, int* err, hipStream_t s,
-                            unsigned long long* kst, int max_blocks, int xcd_chunk) {
+                            unsigned long long* kst, int max_blocks, int xcd_chunk, int run, float bratio) {
     const size_t lds = bsk::knn_lds_bytes();
-    int blocks = (n + KNN_WAVES - 1) / KNN_WAVES;
+    if (run < 1) run = 1;
+    const int nu = (n + run - 1) / run;  // wave passes: runs of `run` consecutive cell-order queries
+    int blocks = (nu + KNN_WAVES - 1) / KNN_WAVES;
     // fewer, longer-lived waves cost less dispatch; more, short-lived ones let high-priority
     // kernels of other streams in sooner
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
     int zc = 0;  // workgroups per XCD-local chunk (one query per wave only)
     if (xcd_chunk > 0 && (max_blocks <= 0 || blocks < max_blocks)) {
-        zc = (xcd_chunk + KNN_WAVES - 1) / KNN_WAVES;
+        zc = (xcd_chunk + KNN_WAVES * run - 1) / (KNN_WAVES * run);
         const int rounds = (blocks + 8 * zc - 1) / (8 * zc);
         blocks = rounds * 8 * zc;  // whole rounds of 8 chunks; the workgroups past n exit at once
     }
 #ifdef DIAG_SR_TWICE
     // diagnostic builds only: SR twice (idempotent) -- its marginal cost
     bsk::k_seg_ratio<false><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
-                                                                hint, ratio, err, nullptr, zc);
+                                                                hint, ratio, err, nullptr, zc, run, bratio);
 #endif
     if (kst)
         bsk::k_seg_ratio<true><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
-                                                                   hint, ratio, err, kst, zc);
+                                                                   hint, ratio, err, kst, zc, run, bratio);
     else
         bsk::k_seg_ratio<false><<<blocks, 64 * KNN_WAVES, lds, s>>>(ladder(g4, ladder_mode), pts4, n, radius, max_nn, sr_type,
-                                                                    hint, ratio, err, nullptr, zc);
+                                                                    hint, ratio, err, nullptr, zc, run, bratio);
     return hipGetLastError();
 }
 

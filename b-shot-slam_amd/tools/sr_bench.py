@@ -37,6 +37,8 @@ for arg in sys.argv[1:] or ["default"]:
                       "chunks_per_q": round(s[5] / q, 3), "failed_chunks_per_q": round(s[26] / q, 3),
                       "streaming_path_frac": round(s[11] / q, 4), "in_radius_per_q": round(s[10] / q, 1),
                       "refine_passes_per_q": round(s[7] / q, 4),
+                      # bounded passes (runs of cell-order queries): delivered / fell back to the ladder
+                      "bounded_frac": round(s[27] / q, 4), "bounded_fallback_frac": round(s[28] / q, 4),
                       # per-query wave-clock shares (DIAG launch): ladder + streaming, selection from
                       # the LDS list, selection on the streaming path, the ratio (centroid + signs)
                       "cycle_share": {k: round(s[i] / max(1, s[12] + s[13] + s[14] + s[15]), 3)

@@ -47,11 +47,15 @@ def test_seg_ratio_bit_exact(ctx, cloud, sr_ref, ladder):
 
 
 @pytest.mark.parametrize("opts", [{"sr_xcd_chunk": 0}, {"sr_xcd_chunk": 4096}, {"sr_start": 0}, {"sr_start": 300},
-                                  {"sr_blocks": 1024}])
+                                  {"sr_blocks": 1024}, {"sr_run": 1}, {"sr_run": 3}, {"sr_run": 64},
+                                  {"sr_run": 64, "sr_bratio": 101}, {"sr_bratio": 200}, {"sr_bratio": 1000},
+                                  {"sr_run": 16, "sr_blocks": 512, "sr_xcd_chunk": 0}])
 def test_seg_ratio_schedules_agree(ctx, cloud, sr_ref, opts):
-    """The SR launch's query schedule (XCD-local chunks or round-robin, a persistent grid), and the
-    ladder's start step only change the work done, never a ratio."""
-    defaults = {"sr_xcd_chunk": 1024, "sr_start": 80, "sr_blocks": 0}
+    """The SR launch's query schedule (XCD-local chunks or round-robin, a persistent grid), the
+    ladder's start step, and the runs of cell-order queries whose radii chain from their
+    predecessor's max_nn-th distance (sr_run, with the bounded pass's grid choice sr_bratio) only
+    change the work done, never a ratio."""
+    defaults = {"sr_xcd_chunk": 1024, "sr_start": 80, "sr_blocks": 0, "sr_run": 8, "sr_bratio": 283}
     try:
         for k, v in opts.items():
             ctx.set_option(k, v)
@@ -79,12 +83,13 @@ def _edge_cloud():
     return xyz[rng.permutation(len(xyz))]
 
 
-@pytest.mark.parametrize("sr_type", [0, 1, 2])
-def test_seg_ratio_edge_cases(sr_type):
+@pytest.mark.parametrize("sr_type,run", [(0, 8), (1, 8), (2, 8), (0, 1), (0, 256)])
+def test_seg_ratio_edge_cases(sr_type, run):
     xyz = _edge_cloud()
     ridx, rrat = orc.seg_ratio(xyz, sr_type=sr_type)
     c = bshot_py.Context(0, bshot_py.default_params(sr_type=sr_type))
     try:
+        c.set_option("sr_run", run)
         c.set_cloud(xyz)
         idx, rat = c.seg_ratio()
         np.testing.assert_array_equal(idx, ridx)
