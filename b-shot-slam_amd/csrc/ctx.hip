@@ -254,7 +254,8 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
         c->hmark("Q_iss_grid");
         HIPCHK(launch_iss(reuse && !lvl5 ? s.grid_l16 : s.grid_iss, s.pts4.p, n, c->prm.iss_salient, c->prm.iss_nonmax, c->prm.iss_min_nn,
                           c->prm.iss_gamma21, c->prm.iss_gamma32, s.third.p, s.issflag.p, s.issovf.p, s.issnml.p,
-                          s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks, zeroed),
+                          s.issnmc.p, s.errw.p + 1, st, c->opt_iss_ovf_blocks, c->opt_iss_nms_blocks, zeroed,
+                          c->opt_iss_xcd_chunk),
                "iss launch");
         c->stage_end(sg3, st);
         c->hmark("Q_iss_k");
@@ -1342,6 +1343,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "topk_thread") c->opt_topk_thread = value ? 1 : 0;
     else if (k == "iss_grid") c->opt_iss_grid = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
+    else if (k == "iss_xcd_chunk") c->opt_iss_xcd_chunk = value < 0 ? 0 : value;
     else if (k == "pre_fast") c->opt_pre_fast = value ? 1 : 0;
     else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;

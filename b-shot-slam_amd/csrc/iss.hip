@@ -38,6 +38,20 @@ __device__ __forceinline__ double iss_third(const double* sm, double g21, double
     return 0.0;
 }
 
+#ifndef ISS_CELL_ORDER
+#define ISS_CELL_ORDER 1
+#endif
+// A point's list position: its place in the grid's cell order (ISS_CELL_ORDER, spts .w = index) or
+// its index. The overflow list and the non-max lists nml[slot][position] are kept by position, so
+// the lane kernel's lanes (consecutive positions) write whole lines.
+__device__ __forceinline__ int iss_point_of(const GridView& g, int jp) {
+#if ISS_CELL_ORDER
+    return (int)__float_as_uint(g.spts[jp].w);
+#else
+    return jp;
+#endif
+}
+
 // wave/point fallback for the points whose neighbourhood overflowed the lane kernel's list:
 // ovf[0] = count, ovf[1..] = point indices
 // nml != null (nonmax <= salient): a point whose non-max neighbours (a prefix of its sorted list) number
@@ -65,7 +79,8 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
         npend = 0;
     };
     for (int oi = blockIdx.x * ISS_WAVES + wave; oi < n_ovf; oi += gridDim.x * ISS_WAVES) {
-        const int q = ovf[1 + oi];
+        const int jp = ovf[1 + oi];  // the point's list position (iss_point_of)
+        const int q = iss_point_of(g, jp);
         const float4 c = pts4[q];
         double out = 0.0;
         bool pend = false;
@@ -94,7 +109,7 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
                     for (int r = lane; r < cnt; r += 64)
                         cnm += __popcll(__ballot((unsigned int)(L->list[r] >> 32) < r2nm_bits));
                     if (cnm <= 32) {
-                        if (lane < cnm) nml[(size_t)lane * n + q] = (unsigned int)L->list[lane];
+                        if (lane < cnm) nml[(size_t)lane * n + jp] = (unsigned int)L->list[lane];
                         if (lane == 0) nmc[q] = cnm;
                     }
                 }
@@ -145,9 +160,6 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
 // as it holds more than ISS_LCAP neighbours and hands the point to the overflow list (wave kernel
 // above). The kept keys are then sorted by (d2, idx) in registers with a bitonic network sized to
 // the wave's longest list, and the double scatter matrix is summed in that rank order.
-#ifndef ISS_CELL_ORDER
-#define ISS_CELL_ORDER 1
-#endif
 #ifndef ISS_LCAP
 #define ISS_LCAP 32
 #endif
@@ -185,7 +197,7 @@ template <int N>
 __device__ __forceinline__ int iss_sum_sorted(const unsigned long long (*keys)[ISS_LBLOCK], int t, int cnt,
                                               const float4* __restrict__ pts4, double cx, double cy, double cz,
                                               double* sm, unsigned int r2nm_bits, unsigned int* __restrict__ nml,
-                                              int n, int q) {
+                                              int n, int jp) {
     unsigned long long k[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) k[i] = i < cnt ? keys[i][t] : ~0ull;
@@ -194,7 +206,7 @@ __device__ __forceinline__ int iss_sum_sorted(const unsigned long long (*keys)[I
 #pragma unroll
     for (int i = 0; i < N; ++i)
         if (i < cnt && (unsigned int)(k[i] >> 32) < r2nm_bits) {  // d2 >= 0: bit order = float order
-            nml[(size_t)i * n + q] = (unsigned int)k[i];
+            nml[(size_t)i * n + jp] = (unsigned int)k[i];
             cnm = i + 1;
         }
 #pragma unroll
@@ -221,7 +233,7 @@ __device__ __forceinline__ int iss_sum_sorted(const unsigned long long (*keys)[I
 __device__ __forceinline__ int iss_sum_merge32(unsigned long long (*keys)[ISS_LBLOCK], int t, int cnt,
                                                const float4* __restrict__ pts4, double cx, double cy, double cz,
                                                double* sm, unsigned int r2nm_bits, unsigned int* __restrict__ nml,
-                                               int n, int q) {
+                                               int n, int jp) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         unsigned long long k[16];
@@ -256,7 +268,7 @@ __device__ __forceinline__ int iss_sum_merge32(unsigned long long (*keys)[ISS_LB
             pp[u] = pts4[i < cnt ? (unsigned)(kk[u] & 0xFFFFFFFFu) : 0u];  // unconditional: loads in flight together
             if (i < cnt) {
                 if ((unsigned int)(kk[u] >> 32) < r2nm_bits) {  // d2 >= 0: bit order = float order
-                    nml[(size_t)i * n + q] = (unsigned int)kk[u];
+                    nml[(size_t)i * n + jp] = (unsigned int)kk[u];
                     cnm = i + 1;
                 }
             }
@@ -275,22 +287,32 @@ __device__ __forceinline__ int iss_sum_merge32(unsigned long long (*keys)[ISS_LB
 __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float4* __restrict__ pts4, int n,
                                                         float salient, float nonmax, int min_nn, double g21,
                                                         double g32, double* __restrict__ third, int* __restrict__ ovf,
-                                                        unsigned int* __restrict__ nml, int* __restrict__ nmc) {
+                                                        unsigned int* __restrict__ nml, int* __restrict__ nmc, int zc) {
     static_assert(ISS_LCAP == 16 || ISS_LCAP == 32, "the sort networks cover 8, 16 and 32 keys");
     __shared__ unsigned long long keys[ISS_LCAP][ISS_LBLOCK];  // [slot][thread]: conflict-free columns
     const int t = threadIdx.x;
+    int blk = blockIdx.x;
+    if (zc > 0) {
+        // XCD-local chunks (as k_seg_ratio): the workgroups of label g = b % 8 (one XCD) take chunks
+        // g, g + 8, ... of zc workgroups each, so each XCD's L2 holds its own stretch of cell order:
+        // its points, their cells' hash-table lines and the neighbours they read
+        const int gx = blockIdx.x & 7, i = blockIdx.x >> 3;
+        const int m = i / zc, o = i - m * zc;
+        blk = (m * 8 + gx) * zc + o;
+    }
 #if ISS_CELL_ORDER
     // points in the grid's cell order (spts .w = index): a wave's lanes scan the same or adjacent
     // cells, so their loops and loads stay together
-    const int j = blockIdx.x * ISS_LBLOCK + t;
+    const int j = blk * ISS_LBLOCK + t;
     const bool live = j < n;
     const float4 sp = live ? g.spts[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     const int q = live ? (int)__float_as_uint(sp.w) : n;
     const float4 c = sp;
 #else
-    const int q = blockIdx.x * ISS_LBLOCK + t;
+    const int q = blk * ISS_LBLOCK + t;
     const bool live = q < n;
     const float4 c = live ? pts4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int j = q;
 #endif
     const bool fin = live && __builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z);
     int cnt = 0;
@@ -361,7 +383,7 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
         }
     }
     const bool over = cnt > ISS_LCAP;
-    if (over) ovf[1 + atomicAdd(&ovf[0], 1)] = q;  // third[q] written by the overflow pass
+    if (over) ovf[1 + atomicAdd(&ovf[0], 1)] = j;  // third[q] written by the overflow pass
     const bool work = fin && !over && cnt >= min_nn;
     double out = 0.0;
     // wave-uniform network size: the longest kept list of the wave
@@ -372,13 +394,13 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
         const double cx = c.x, cy = c.y, cz = c.z;
         const unsigned int r2nm = __float_as_uint((float)((double)nonmax * (double)nonmax));
         int cnm;
-        if (wmax <= 8) cnm = iss_sum_sorted<8>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
-        else if (wmax <= 16) cnm = iss_sum_sorted<16>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+        if (wmax <= 8) cnm = iss_sum_sorted<8>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, j);
+        else if (wmax <= 16) cnm = iss_sum_sorted<16>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, j);
 #if ISS_LCAP > 16
 #if ISS_MERGE32
-        else cnm = iss_sum_merge32(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+        else cnm = iss_sum_merge32(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, j);
 #else
-        else cnm = iss_sum_sorted<32>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, q);
+        else cnm = iss_sum_sorted<32>(keys, t, cnt, pts4, cx, cy, cz, sm, r2nm, nml, n, j);
 #endif
 #endif
         out = iss_third(sm, g21, g32);
@@ -391,11 +413,12 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
 // non-maximum suppression from the lane kernel's lists (nonmax <= salient): flag[i] = the point has
 // at least min_nn neighbours inside the non-max radius and none with a strictly larger third
 // eigenvalue. Overflow points (nmc = -1) are left to k_iss_nms_ovf.
-__global__ void __launch_bounds__(256) k_iss_nms_list(int n, int min_nn, const double* __restrict__ third,
+__global__ void __launch_bounds__(256) k_iss_nms_list(GridView g, int n, int min_nn, const double* __restrict__ third,
                                                       const unsigned int* __restrict__ nml,
                                                       const int* __restrict__ nmc, unsigned char* __restrict__ flag) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const int jp = blockIdx.x * blockDim.x + threadIdx.x;  // list position
+    if (jp >= n) return;
+    const int i = iss_point_of(g, jp);
     const double ti = third[i];
     if (!(ti > 0.0)) {
         flag[i] = 0;
@@ -407,7 +430,7 @@ __global__ void __launch_bounds__(256) k_iss_nms_list(int n, int min_nn, const d
     for (int s0 = 0; s0 < m; s0 += 8) {
         unsigned int j[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) j[u] = s0 + u < m ? nml[(size_t)(s0 + u) * n + i] : (unsigned int)i;
+        for (int u = 0; u < 8; ++u) j[u] = s0 + u < m ? nml[(size_t)(s0 + u) * n + jp] : (unsigned int)i;
         double tj[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) tj[u] = third[j[u]];
@@ -428,7 +451,7 @@ __global__ void __launch_bounds__(256) k_iss_nms_wave(GridView g, const float4* 
     const int cnt_pts = all ? n : ovf[0];
     const float r2 = (float)((double)nonmax * (double)nonmax);
     for (int oi = wv; oi < cnt_pts; oi += nw) {
-        const int q = all ? oi : ovf[1 + oi];
+        const int q = all ? oi : iss_point_of(g, ovf[1 + oi]);
         if (!all && nmc[q] >= 0) continue;  // decided from its list (k_iss_nms_list)
         const double tq = third[q];
         const float4 c = pts4[q];
@@ -468,7 +491,7 @@ namespace bsh {
 
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc, int* err,
-                      hipStream_t s, int ovf_blocks, int nms_blocks, bool ovf_zeroed) {
+                      hipStream_t s, int ovf_blocks, int nms_blocks, bool ovf_zeroed, int xcd_chunk) {
     if (n <= 0) return hipSuccess;
 #ifdef DIAG_ISS_TWICE
     // diagnostic builds only: the lane kernel an extra time (its outputs are rewritten below)
@@ -476,13 +499,19 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
         hipError_t e0 = kfill(ovf, 0, sizeof(int), s);
         if (e0 != hipSuccess) return e0;
         bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn,
-                                                                                 g21, g32, third, ovf, nml, nmc);
+                                                                                 g21, g32, third, ovf, nml, nmc, 0);
     }
 #endif
     hipError_t e = ovf_zeroed ? hipSuccess : kfill(ovf, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    bsk::k_iss_lane<<<(n + ISS_LBLOCK - 1) / ISS_LBLOCK, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn,
-                                                                             g21, g32, third, ovf, nml, nmc);
+    int lblocks = (n + ISS_LBLOCK - 1) / ISS_LBLOCK, zc = 0;
+    if (xcd_chunk > 0) {
+        // whole rounds of 8 XCD-local chunks; the workgroups past n exit at once
+        zc = (xcd_chunk + ISS_LBLOCK - 1) / ISS_LBLOCK;
+        lblocks = (lblocks + 8 * zc - 1) / (8 * zc) * (8 * zc);
+    }
+    bsk::k_iss_lane<<<lblocks, ISS_LBLOCK, 0, s>>>(g.view(), pts4, n, salient, nonmax, min_nn, g21, g32, third, ovf, nml,
+                                                   nmc, zc);
     const size_t lds = sizeof(bsk::IssLds) * ISS_WAVES;
     // the overflow count is device-side: a fixed grid strides over it, idle waves exit at once
 #ifndef ISS_OVF_NML
@@ -496,7 +525,7 @@ hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient
         g.view(), pts4, ovf, salient, min_nn, g21, g32, third, err, r2nm_bits, lists ? nml : nullptr, nmc, n);
     if (nonmax <= salient) {
         // the non-max neighbours are a prefix of the lane kernel's sorted salient neighbours
-        bsk::k_iss_nms_list<<<(n + 255) / 256, 256, 0, s>>>(n, min_nn, third, nml, nmc, flag);
+        bsk::k_iss_nms_list<<<(n + 255) / 256, 256, 0, s>>>(g.view(), n, min_nn, third, nml, nmc, flag);
         bsk::k_iss_nms_wave<<<nms_blocks > 0 ? nms_blocks : 1024, 256, 0, s>>>(g.view(), pts4, n, ovf, 0, nonmax, min_nn,
                                                                                third, flag, nmc);
     } else {

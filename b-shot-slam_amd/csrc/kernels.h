@@ -28,7 +28,8 @@ hipError_t launch_normals(const DevGrid* const* g4, int ladder_mode, const float
                           float radius, int max_nn, float4* normals, int* err, hipStream_t s);
 hipError_t launch_iss(const DevGrid& g, const float4* pts4, int n, float salient, float nonmax, int min_nn, double g21,
                       double g32, double* third, unsigned char* flag, int* ovf, unsigned int* nml, int* nmc,
-                      int* err, hipStream_t s, int ovf_blocks = 0, int nms_blocks = 0, bool ovf_zeroed = false);
+                      int* err, hipStream_t s, int ovf_blocks = 0, int nms_blocks = 0, bool ovf_zeroed = false,
+                      int xcd_chunk = 0);
 // bh (nullable, [k][1024] u32): per-keypoint d2-bucket histogram for the bucketed gather
 hipError_t launch_shot_count(const DevGrid& g, const float* kps, int k, float R, int* counts, long long* offs,
                              hipStream_t s, unsigned int* bh = nullptr);

@@ -1,6 +1,6 @@
-"""Diagnostic: standalone ISS stage time (grid + lane kernel + overflow kernel + NMS, stage events, 10
-launches) on one synthetic HDL-64 sweep, for the library BSHOT_LIB selects (A/B of builds).
-usage: python iss_bench.py [option sets "name=value,..."]; every set's ISS indices must equal the first's."""
+"""Diagnostic: standalone ISS stage time (stage events, 10 sweeps) on one synthetic HDL-64 sweep per
+option set ("name=value,name=value"; none: the defaults); the ISS keypoints of every set must be
+identical to the first's."""
 import json
 import os
 import sys
@@ -18,9 +18,9 @@ for arg in sys.argv[1:] or ["default"]:
     for kk, vv in opts.items():
         c.set_option(kk, vv)
     c.set_cloud(pc)
-    out = c.iss()
-    same = ref is None or np.array_equal(out, ref)
-    ref = out.copy() if ref is None else ref
+    cur = c.iss()
+    same = ref is None or np.array_equal(cur, ref)
+    ref = cur if ref is None else ref
     c.set_timing(True)
     c.stage_reset()
     for _ in range(10):
@@ -29,5 +29,6 @@ for arg in sys.argv[1:] or ["default"]:
     st = c.stage_times()
     c.set_timing(False)
     print(json.dumps({"lib": os.environ.get("BSHOT_LIB", "tree"), "options": arg, "identical": bool(same),
-                      "n_iss": int(len(out)), **{k: round(v[0] / 10, 4) for k, v in st.items() if v[1]}}))
+                      "iss_ms": round(st["iss"][0] / 10, 4), "grid_ms": round(st["grid"][0] / 10, 4),
+                      "n_iss": int(len(cur))}))
 c.close()

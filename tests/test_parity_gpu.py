@@ -106,15 +106,18 @@ def test_topk_keypoints_exact(sr_ref):
         np.testing.assert_array_equal(a[0], b[0])
 
 
-@pytest.mark.parametrize("iss_grid", [1, 0])
-def test_iss_exact(ctx, cloud, iss_grid):
-    """ISS on the SR ladder's finest grid (default) and on a grid of its own."""
+@pytest.mark.parametrize("iss_grid,xcd", [(1, 1024), (0, 1024), (1, 0), (1, 64)])
+def test_iss_exact(ctx, cloud, iss_grid, xcd):
+    """ISS on the SR ladder's finest grid (default) and on a grid of its own; the lane kernel's
+    points in XCD-local chunks of cell order (1024 default, 64) or in plain block order (0)."""
     ctx.set_option("iss_grid", iss_grid)
+    ctx.set_option("iss_xcd_chunk", xcd)
     try:
         ctx.set_cloud(cloud)
         got = ctx.iss()
     finally:
         ctx.set_option("iss_grid", 1)
+        ctx.set_option("iss_xcd_chunk", 1024)
     ref, _ = orc.iss(cloud)
     np.testing.assert_array_equal(got, ref)
 
