@@ -141,8 +141,8 @@ struct bshot_ctx {
     int opt_sr_xcd_chunk = 1024;  // SR queries per XCD-local chunk of cell order (0: round-robin queries)
     int opt_sr_blocks = 0;      // SR grid cap (0: one run of queries per wave -- short waves let the main stream in)
     int opt_iss_xcd_chunk = 1024;  // ISS lane kernel: points per XCD-local chunk of cell order (0: blocks in order)
-    int opt_sr_run = 8;         // SR cell-order queries per wave pass, each after the first bounded by its predecessor
-    int opt_sr_bratio = 283;    // SR bounded pass: grid cell >= radius * 100 / this (percent)
+    int opt_sr_run = 4;         // SR cell-order queries per wave pass, each after the first bounded by its predecessor
+    int opt_sr_bratio = 200;    // SR bounded pass: grid cell >= radius * 100 / this (percent)
     int opt_side_prio = 0;      // describe (side) stream priority: 0 low (as SR/ISS ahead), 1 middle, 2 the main stream's
     int opt_map_sync = 1;       // GPU map insert: wait for it and report the map size per sweep (0: stream-ordered, size -1)
     int opt_host_map_log = 1;   // LidarOdometry keeps the GPU map's insert log for the host Map view (bshot_odom: 0)

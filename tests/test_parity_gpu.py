@@ -48,14 +48,14 @@ def test_seg_ratio_bit_exact(ctx, cloud, sr_ref, ladder):
 
 @pytest.mark.parametrize("opts", [{"sr_xcd_chunk": 0}, {"sr_xcd_chunk": 4096}, {"sr_start": 0}, {"sr_start": 300},
                                   {"sr_blocks": 1024}, {"sr_run": 1}, {"sr_run": 3}, {"sr_run": 64},
-                                  {"sr_run": 64, "sr_bratio": 101}, {"sr_bratio": 200}, {"sr_bratio": 1000},
+                                  {"sr_run": 64, "sr_bratio": 101}, {"sr_bratio": 283}, {"sr_bratio": 1000},
                                   {"sr_run": 16, "sr_blocks": 512, "sr_xcd_chunk": 0}])
 def test_seg_ratio_schedules_agree(ctx, cloud, sr_ref, opts):
     """The SR launch's query schedule (XCD-local chunks or round-robin, a persistent grid), the
     ladder's start step, and the runs of cell-order queries whose radii chain from their
     predecessor's max_nn-th distance (sr_run, with the bounded pass's grid choice sr_bratio) only
     change the work done, never a ratio."""
-    defaults = {"sr_xcd_chunk": 1024, "sr_start": 80, "sr_blocks": 0, "sr_run": 8, "sr_bratio": 283}
+    defaults = {"sr_xcd_chunk": 1024, "sr_start": 80, "sr_blocks": 0, "sr_run": 4, "sr_bratio": 200}
     try:
         for k, v in opts.items():
             ctx.set_option(k, v)
