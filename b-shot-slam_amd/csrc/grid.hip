@@ -15,6 +15,19 @@
 #include "kernels.h"
 #include "regrow.h"
 
+// the ladder's 63-bit key sort: rocprim's default picks block sort + merge passes below 1M items
+// (~1 + 7 launches at 130k keys); GRID_SORT_ONESWEEP (diagnostic builds) forces its onesweep radix
+// passes instead
+#ifndef GRID_SORT_ONESWEEP
+#define GRID_SORT_ONESWEEP 0
+#endif
+#if GRID_SORT_ONESWEEP
+using LadderSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                    rocprim::default_config, 0>;
+#else
+using LadderSortConfig = rocprim::default_config;
+#endif
+
 namespace bsk {
 
 __global__ void k_grid_keys(const float* __restrict__ xyz, int n, float cell, unsigned long long* __restrict__ keys,
@@ -183,6 +196,10 @@ namespace bsh {
 static unsigned int pow2_at_least(unsigned int x) {
     unsigned int p = 1024;
     while (p < x) p <<= 1;
+#ifdef GRID_H_FIXED
+    // diagnostic builds only (table-size sensitivity; safe only for clouds with < 2^GRID_H_FIXED cells)
+    if (p > (1u << GRID_H_FIXED)) p = 1u << GRID_H_FIXED;
+#endif
     return p;
 }
 
@@ -214,7 +231,7 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
         if ((e = hipMalloc(&g0.vals2, sizeof(unsigned int) * g0.cap))) return e;
         if ((e = hipMalloc(&g0.spts, sizeof(float4) * g0.cap))) return e;
         size_t tb = 0;
-        if ((e = rocprim::radix_sort_pairs(nullptr, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)g0.cap, 0, 63,
+        if ((e = rocprim::radix_sort_pairs<LadderSortConfig>(nullptr, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)g0.cap, 0, 63,
                                            s)))
             return e;
         g0.tmp_bytes = tb;
@@ -240,7 +257,7 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
     const int B = 256;
     bsk::k_ladder_keys<<<(n + B - 1) / B, B, 0, s>>>(d_xyz, n, c0, g0.keys, g0.vals, d_pts4, bsk::ZeroWords{{zero0, zero1}});
     size_t tb = g0.tmp_bytes;
-    if ((e = rocprim::radix_sort_pairs(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 63, s)))
+    if ((e = rocprim::radix_sort_pairs<LadderSortConfig>(g0.tmp, tb, g0.keys, g0.keys2, g0.vals, g0.vals2, (unsigned)n, 0, 63, s)))
         return e;
     // the levels' tables: one clear and one fill launch for all of them (the sorted points are
     // always scattered: the other levels alias them)

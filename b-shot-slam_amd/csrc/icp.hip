@@ -264,6 +264,15 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
 // after max_iter - 1 iterations, or when a wait exceeds ICP_WAIT_TICKS; the host then restarts the
 // iterations from the current positions (ctx_icp).
 #define ICPH_THREADS 64
+// sources per workgroup (lanes [ICPH_SRC, 64) idle in the scan): a source that leaves its list takes a
+// wave-wide grid search and list rebuild, queued on its own wave, and on the sweeps where ICP moves
+// far (a gated frame starts from the previous pose) hundreds leave (profiles/r06e_icp_tail.txt: the
+// 18 sweeps with >= 60 searches wait 0.89 ms for iterations 1.. against 0.07 ms, corr 0.93); fewer
+// sources per wave spread those searches over more waves
+#ifndef ICPH_SRC
+#define ICPH_SRC 64
+#endif
+static_assert(ICPH_SRC >= 1 && ICPH_SRC <= ICPH_THREADS, "sources per iteration workgroup");
 #define ICP_WAIT_TICKS 100000000ll  // 1 s at the 100 MHz wall clock: a launch that cannot finish exits
 #ifndef ICPH_WPE
 #define ICPH_WPE 0
@@ -296,8 +305,8 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
     const int lane = lane_id();
     cand_init(&cl);
     n_new[lane] = -2;
-    const int i = blockIdx.x * ICPH_THREADS + lane;
-    const bool have = i < ns;
+    const int i = blockIdx.x * ICPH_SRC + lane;
+    const bool have = lane < ICPH_SRC && i < ns;
     float qx = 0.f, qy = 0.f, qz = 0.f, x0 = 0.f, y0 = 0.f, z0 = 0.f, R = 0.f;
     int n = -1;
     if (have) {
@@ -390,7 +399,7 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
             int cnt2;
             float R2;
             icp_build_list(G, &cl, q.x, q.y, q.z, m, tgt4, lst_w + qi, lsd_w + qi, ns, cap, skl, &cnt2, &R2);
-            if (lane == 0) { q_new[qi - (int)blockIdx.x * ICPH_THREADS] = make_float4(q.x, q.y, q.z, R2); n_new[qi - (int)blockIdx.x * ICPH_THREADS] = cnt2; }
+            if (lane == 0) { q_new[qi - (int)blockIdx.x * ICPH_SRC] = make_float4(q.x, q.y, q.z, R2); n_new[qi - (int)blockIdx.x * ICPH_SRC] = cnt2; }
         }
         // the rebuilt lists (stored by this wave) are read by their owner lanes from the next iteration on
         __builtin_amdgcn_s_waitcnt(0);
@@ -862,7 +871,7 @@ hipError_t launch_icp(const float* src0, int ns, float4* lst, float* lsd, int* l
 }
 
 int icp_lists_blocks(int ns) { return (ns + ICP_WAVES - 1) / ICP_WAVES; }
-int icp_iter_blocks(int ns) { return (ns + ICPH_THREADS - 1) / ICPH_THREADS; }
+int icp_iter_blocks(int ns) { return (ns + ICPH_SRC - 1) / ICPH_SRC; }
 
 hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
                                  float4* lst, float* lsd, int* lcnt, float4* lcen, unsigned long long* best_out,
