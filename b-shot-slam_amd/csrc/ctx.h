@@ -114,6 +114,13 @@ struct CloudState {
     void release();
 };
 
+// the SR error word of a cloud (CloudState::errw[0]): 1 = a kNN list overflow (k_seg_ratio), 8 = a
+// finite point beyond the ladder key range (k_ladder_cells4)
+inline const char* sr_error_message(int bits) {
+    if (bits & 8) return "seg_ratio: a point lies beyond the grid's coordinate range (|x|, |y|, |z| >= 2^20 finest cells of seg_radius / 32)";
+    return "seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)";
+}
+
 namespace bsh {
 struct GMap;       // csrc/gmap.hip
 struct PreState;   // csrc/preprocess.hip

@@ -1141,7 +1141,7 @@ int bshot_seg_ratio(bshot_ctx* c, int32_t* idx, float* ratio, int* n_out) {
     CloudState& s = c->cs;
     HIPCHK(hipEventSynchronize(s.ev_sr), "sync ratio");
     c->resolve_events();
-    if (s.h_err.p[0]) return c->fail("seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)", BSHOT_ECAP);
+    if (s.h_err.p[0]) return c->fail(sr_error_message(s.h_err.p[0]), BSHOT_ECAP);
     const int n = s.n;
     const float* h = s.h_ratio.p;
     int m = 0;

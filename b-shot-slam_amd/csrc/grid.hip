@@ -152,15 +152,23 @@ __global__ void k_grid_clear4(Tables4 T, unsigned level_mask) {
 }
 
 // the cells of every level in level_mask at once, and the points in key order
+// range_err (nullable): bit 8 set when a finite point lies beyond the key range (|cell| >= 2^20 at the
+// finest level: +-98 km per axis at c0 = 187.5 mm). Such a point is in no cell, so no search finds
+// it; the SR error word carries the bit and the sweep fails loudly instead of dropping the point
+// (ADVICE r05). Non-finite points have no cell by design (the reference's searches skip them too).
 __global__ void k_ladder_cells4(const unsigned long long* __restrict__ keys, const unsigned int* __restrict__ vals,
                                 const float4* __restrict__ pts4, int n, float c0, Tables4 T, unsigned level_mask,
-                                float4* __restrict__ spts) {
+                                float4* __restrict__ spts, int* __restrict__ range_err) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const float4 p = pts4[vals[j]];
     spts[j] = p;
     const unsigned long long k = keys[j];
-    if (k == BS_EMPTY_KEY) return;
+    if (k == BS_EMPTY_KEY) {
+        if (range_err && __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z))
+            atomicOr(range_err, 8);
+        return;
+    }
     const unsigned long long km1 = j > 0 ? keys[j - 1] : BS_EMPTY_KEY;
     int ix, iy, iz;
     ladder_cells(p.x, p.y, p.z, c0, ix, iy, iz);
@@ -281,7 +289,8 @@ hipError_t grid_build_ladder(DevGrid* const* gp, const float* d_xyz, int n, floa
         if ((level_mask >> L) & 1u) hmax = std::max(hmax, gl->H);
     }
     if (hmax) bsk::k_grid_clear4<<<(hmax + B - 1) / B, B, 0, s>>>(T, level_mask);
-    bsk::k_ladder_cells4<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, c0, T, level_mask, g0.spts);
+    bsk::k_ladder_cells4<<<(n + B - 1) / B, B, 0, s>>>(g0.keys2, g0.vals2, d_pts4, n, c0, T, level_mask, g0.spts,
+                                                        zero0);
     return hipGetLastError();
 }
 

@@ -275,7 +275,7 @@ void LidarOdometry::queueFrameDevice(const float* d_xyz, int n) {
             }
             c->hmark("T_sr_ready");
             if (h_err[0]) {
-                p->err = "seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)";
+                p->err = sr_error_message(h_err[0]);
                 return;
             }
             if (select_from_ratios(h_ratio, n, kwant, p->kidx, p->kr, &p->nv) < 0) p->err = "topk";
@@ -308,8 +308,7 @@ void LidarOdometry::runAhead(Lookahead& la) {
         la.kr = std::move(la.topk->kr);
         la.topk.reset();
     } else {
-        if (S.h_err.p[0])
-            throw std::runtime_error("seg_ratio: neighbourhood with too many exactly tied boundary keys (kNN list overflow)");
+        if (S.h_err.p[0]) throw std::runtime_error(sr_error_message(S.h_err.p[0]));
         if (select_from_ratios(S.h_ratio.p, S.n, prm_.num_keypoints, la.kidx, la.kr, &la.nv) < 0) fail("topk");
     }
     const int k = (int)la.kidx.size();

@@ -32,7 +32,7 @@ typedef struct bshot_ctx bshot_ctx;
 /* Defaults = the reference's hard-coded constants (cited per field). */
 typedef struct {
     float seg_radius;     /* 3000  src/lidar_odometry.cpp:68 (SR radius, mm) */
-    int seg_max_nn;       /* 300   src/lidar_odometry.cpp:70 */
+    int seg_max_nn;       /* 300   src/lidar_odometry.cpp:70 (at most 484: the kNN engine's LDS rows) */
     int sr_type;          /* 0 CV, 1 CVS, 2 CVSN: include/lidar_odometry.h:47 setSRType */
     int num_keypoints;    /* 600   src/lidar_odometry.cpp:138 (BASELINE config 2: 2048) */
     float iss_salient;    /* 60    src/lidar_odometry.cpp:452 */
@@ -41,7 +41,8 @@ typedef struct {
     double iss_gamma32;   /* 0.975 src/lidar_odometry.cpp:455 */
     int iss_min_nn;       /* 5     src/lidar_odometry.cpp:456 */
     float normal_radius;  /* 3000  src/lidar_odometry.cpp:174 */
-    int normal_max_nn;    /* 300   include/bshot_bits.h:66 */
+    int normal_max_nn;    /* 300   include/bshot_bits.h:66 (at most 512 when normal_radius == shot_radius,
+                             else 484) */
     float shot_radius;    /* 3000  src/lidar_odometry.cpp:175 */
     float map_range;      /* 100000 src/lidar_odometry.cpp:198 */
     int ransac_max_iter;  /* 2000  src/lidar_odometry.cpp:254 */
@@ -62,7 +63,10 @@ int bshot_sync(bshot_ctx* c);
 /* hipStream_t the context launches on (as void*), for callers that time or chain work. */
 void* bshot_stream(bshot_ctx* c);
 
-/* ---- A0: cloud (replaces LidarOdometry::setSrcFrame, src/lidar_odometry.cpp:29-41) ------- */
+/* ---- A0: cloud (replaces LidarOdometry::setSrcFrame, src/lidar_odometry.cpp:29-41). Points are
+ *      indexed on grids whose finest cell is seg_radius / 32: a finite point farther than 2^20 such
+ *      cells from the origin on any axis (+-98 km at the default 3000 mm) fails the sweep's SR with
+ *      BSHOT_ECAP instead of being dropped. ------------------------------------------------------ */
 int bshot_set_cloud(bshot_ctx* c, const float* xyz, int n);         /* host pointer (H2D copy) */
 int bshot_set_cloud_device(bshot_ctx* c, const float* d_xyz, int n); /* device-resident input */
 

@@ -98,6 +98,23 @@ def test_seg_ratio_edge_cases(sr_type, run):
         c.close()
 
 
+def test_seg_ratio_point_beyond_grid_range_fails_loudly():
+    """A finite point beyond the grids' coordinate range (2^20 finest cells, +-98 km at the default
+    radius) is in no cell: the sweep fails with BSHOT_ECAP rather than computing ratios without it."""
+    rng = np.random.default_rng(5)
+    xyz = rng.normal(0, 2000, (5000, 3)).astype(np.float32)
+    c = bshot_py.Context(0)
+    try:
+        c.set_cloud(xyz)
+        c.seg_ratio()  # in range: fine
+        xyz[17] = (2.0e8, 0.0, 0.0)
+        c.set_cloud(xyz)
+        with pytest.raises(bshot_py.BshotError, match="coordinate range"):
+            c.seg_ratio()
+    finally:
+        c.close()
+
+
 def test_topk_keypoints_exact(sr_ref):
     ridx, rrat = sr_ref
     for k in (600, 2048):
