@@ -215,7 +215,11 @@ __device__ __forceinline__ bool for_candidates(const GridView& g, CandLds* cs, f
 // bitonic sort of a[0, P) ascending, P power of two, one wave
 __device__ __forceinline__ void wave_bitonic(unsigned long long* a, int P) {
     const int lane = lane_id();
+    // kept rolled: where a caller bounds P (icp_build_list) the unrolled stages cost its kernel ~40
+    // VGPRs and a scratch spill
+#pragma unroll 1
     for (int k = 2; k <= P; k <<= 1) {
+#pragma unroll 1
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = lane; i < P; i += 64) {
                 const int p = i ^ j;

@@ -89,8 +89,8 @@ __device__ __forceinline__ void icp_stream_level(const IcpGrids& G, int L, CandL
 // P >= n (>= 64). Round 5's 384-entry experiment sized the row to cap (384) while P reached 512: the
 // pad's ~0 keys landed in the next wave's row, whose list then held key ~0 and loaded
 // tgt4[0xFFFFFFFF] (a GPU memory fault, session r05zb). The row is now the padded length itself,
-// ICP_LIST_ROW = the power of two >= max(cap, 64), and icp_build_list clamps P to the row it is
-// given, so no capacity can index past its own row.
+// ICP_LIST_ROW = the power of two >= max(cap, 64), so for any capacity the pad of a list that fits
+// (n <= cap) ends inside its own row; the launchers refuse any cap but ICP_LIST_CAP.
 __host__ __device__ constexpr int icp_pow2_at_least(int x) { return x <= 64 ? 64 : 2 * icp_pow2_at_least((x + 1) / 2); }
 #define ICP_LIST_ROW (icp_pow2_at_least(ICP_LIST_CAP))
 static_assert(ICP_LIST_ROW >= ICP_LIST_CAP && (ICP_LIST_ROW & (ICP_LIST_ROW - 1)) == 0, "sort row");
@@ -141,11 +141,14 @@ __device__ __forceinline__ void icp_build_list(const IcpGrids& G, CandLds* cs, f
                 }
                 n += __popcll(bm);
             });
-            if (n <= cap && n <= ICP_LIST_ROW) {
+            if (n <= cap) {
                 // ascending distance from q: a later scan stops at the first entry too far to matter;
-                // the pad stays inside this wave's row (P <= ICP_LIST_ROW, a power of two >= n)
+                // the pad stays inside this wave's row: P is the power of two >= n (>= 64), n <= cap, and
+                // the row holds ICP_LIST_ROW = the power of two >= max(cap, 64) keys, so P <= the row.
+                // (A compile-time clamp of P or n here let the compiler bound and unroll the pad and
+                // write loops: 66 -> 105 VGPRs and a scratch spill in k_icp_lists.)
                 int P = 64;
-                while (P < n && P < ICP_LIST_ROW) P <<= 1;
+                while (P < n) P <<= 1;
                 for (int e = n + lane_id(); e < P; e += 64) sk[e] = ~0ull;
                 __builtin_amdgcn_wave_barrier();
                 wave_bitonic(sk, P);
@@ -264,15 +267,18 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
 // after max_iter - 1 iterations, or when a wait exceeds ICP_WAIT_TICKS; the host then restarts the
 // iterations from the current positions (ctx_icp).
 #define ICPH_THREADS 64
-// sources per workgroup (lanes [ICPH_SRC, 64) idle in the scan): a source that leaves its list takes a
-// wave-wide grid search and list rebuild, queued on its own wave, and on the sweeps where ICP moves
-// far (a gated frame starts from the previous pose) hundreds leave (profiles/r06e_icp_tail.txt: the
-// 18 sweeps with >= 60 searches wait 0.89 ms for iterations 1.. against 0.07 ms, corr 0.93); fewer
-// sources per wave spread those searches over more waves
-#ifndef ICPH_SRC
-#define ICPH_SRC 64
+// helper waves per iteration workgroup: wave 0 owns the workgroup's 64 sources (lane per source) and
+// alone polls the host's release (system-scope loads); a source that leaves its list takes a
+// wave-wide grid search and list rebuild, and on the sweeps where ICP moves far (a gated frame
+// starts from the previous pose) hundreds leave -- the 18 sweeps of 199 with >= 60 such searches
+// waited 0.89 ms for iterations 1.. against 0.07 ms (corr 0.93, profiles/r06e_icp_tail.txt). The
+// workgroup's waves take the queued searches in turn, so a wave's queue is a quarter as long; the
+// helpers wait at the workgroup barrier (no polling, no issue slots). More polling waves instead
+// (fewer sources per wave) made every hand-over slower: 32 -> 128 / 256 polling waves took the
+// whole ICP phase 0.68 -> 2.2 / 3.0 ms (r06f).
+#ifndef ICPH_WAVES
+#define ICPH_WAVES 4
 #endif
-static_assert(ICPH_SRC >= 1 && ICPH_SRC <= ICPH_THREADS, "sources per iteration workgroup");
 #define ICP_WAIT_TICKS 100000000ll  // 1 s at the 100 MHz wall clock: a launch that cannot finish exits
 #ifndef ICPH_WPE
 #define ICPH_WPE 0
@@ -288,7 +294,7 @@ static_assert(ICPH_SRC >= 1 && ICPH_SRC <= ICPH_THREADS, "sources per iteration 
 #else
 #define ICPH_ATTR
 #endif
-__global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const float* __restrict__ src0, int ns, int j0,
+__global__ void __launch_bounds__(ICPH_THREADS * ICPH_WAVES) ICPH_ATTR k_icp_iterations(const float* __restrict__ src0, int ns, int j0,
                                                                  const float4* lst, const float* lsd,
                                                                  const int* __restrict__ lcnt,
                                                                  const float4* __restrict__ lcen, int cap, IcpGrids G,
@@ -296,17 +302,19 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
                                                                  const bsh::IcpSync* sy, int* done,
                                                                  unsigned long long* best, int* qstat) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
-    __shared__ CandLds cl;
+    __shared__ CandLds cl[ICPH_WAVES];
     __shared__ float4 q_queue[ICPH_THREADS];
     __shared__ float4 q_new[ICPH_THREADS];  // rebuilt lists: new centre (xyz) and radius (w)
     __shared__ int n_new[ICPH_THREADS];     // their counts; -2 = unchanged
     __shared__ int nq;
-    __shared__ unsigned long long skl[ICP_LIST_ROW];
-    const int lane = lane_id();
-    cand_init(&cl);
-    n_new[lane] = -2;
-    const int i = blockIdx.x * ICPH_SRC + lane;
-    const bool have = lane < ICPH_SRC && i < ns;
+    __shared__ int go_sh;                    // the release wave 0 saw (-1: stop)
+    __shared__ float T_sh[16];               // its step transform
+    __shared__ unsigned long long skl[ICPH_WAVES][ICP_LIST_ROW];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    cand_init(&cl[wave]);
+    if (wave == 0) n_new[lane] = -2;
+    const int i = blockIdx.x * ICPH_THREADS + lane;
+    const bool have = wave == 0 && i < ns;
     float qx = 0.f, qy = 0.f, qz = 0.f, x0 = 0.f, y0 = 0.f, z0 = 0.f, R = 0.f;
     int n = -1;
     if (have) {
@@ -320,25 +328,28 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
     const float4* L = lst + (have ? i : 0);  // entry e at L[e * ns]: the wave's lanes read one 1 KB row
     const float* Ld = lsd + (have ? i : 0);
     for (int j = j0; j < max_iter; ++j) {
-        int g = 0;
-        if (lane == 0) {
-            const long long t0 = wall_clock64();
-            while (true) {
-                g = __hip_atomic_load(&sy->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (g < 0 || g >= j) break;
-                if (wall_clock64() - t0 > ICP_WAIT_TICKS) { g = -1; break; }
-                __builtin_amdgcn_s_sleep(2);
+        if (wave == 0) {
+            int g = 0;
+            if (lane == 0) {
+                const long long t0 = wall_clock64();
+                while (true) {
+                    g = __hip_atomic_load(&sy->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (g < 0 || g >= j) break;
+                    if (wall_clock64() - t0 > ICP_WAIT_TICKS) { g = -1; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                go_sh = g;
+                nq = 0;
             }
+            g = __shfl(g, 0, 64);
+            if (g >= 0 && lane < 16) T_sh[lane] = __hip_atomic_load(&sy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        g = __shfl(g, 0, 64);
-        if (g < 0) break;
-        float Tl = lane < 16 ? __hip_atomic_load(&sy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0.f;
-        float T[12];
-#pragma unroll
-        for (int u = 0; u < 12; ++u) T[u] = __shfl(Tl, u, 64);
-        if (lane == 0) nq = 0;
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        if (go_sh < 0) break;  // every wave of the workgroup
         if (have) {
+            float T[12];
+#pragma unroll
+            for (int u = 0; u < 12; ++u) T[u] = T_sh[u];
             const float x = qx, y = qy, z = qz;
             qx = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
             qy = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
@@ -382,37 +393,37 @@ __global__ void __launch_bounds__(ICPH_THREADS) ICPH_ATTR k_icp_iterations(const
             if (ok) icp_put_key(&best[(size_t)(j & 1) * ns + i], m);
             else q_queue[atomicAdd(&nq, 1)] = make_float4(qx, qy, qz, __int_as_float(i));
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
         const int nqueued = nq;
-        if (qstat && lane == 0 && nqueued) {  // instrumentation (bshot_work_counters 9, 10): grid searches
+        if (qstat && threadIdx.x == 0 && nqueued) {  // instrumentation (bshot_work_counters 9, 10): grid searches
             atomicAdd(&qstat[0], nqueued);
             atomicMax(&qstat[1], nqueued);
         }
-        for (int t = 0; t < nqueued; ++t) {
+        for (int t = wave; t < nqueued; t += ICPH_WAVES) {
             // the exact grid search, then a new list around the current position (its owner lane
             // takes over the new centre, count and radius below), so a source that outgrew its list
             // pays the search once
             const float4 q = q_queue[t];
             const int qi = __float_as_int(q.w);
-            const unsigned long long m = icp_wave_nn(G, &cl, q.x, q.y, q.z, tgt4, nt);
+            const unsigned long long m = icp_wave_nn(G, &cl[wave], q.x, q.y, q.z, tgt4, nt);
             if (lane == 0) icp_put_key(&best[(size_t)(j & 1) * ns + qi], m);
             int cnt2;
             float R2;
-            icp_build_list(G, &cl, q.x, q.y, q.z, m, tgt4, lst_w + qi, lsd_w + qi, ns, cap, skl, &cnt2, &R2);
-            if (lane == 0) { q_new[qi - (int)blockIdx.x * ICPH_SRC] = make_float4(q.x, q.y, q.z, R2); n_new[qi - (int)blockIdx.x * ICPH_SRC] = cnt2; }
+            icp_build_list(G, &cl[wave], q.x, q.y, q.z, m, tgt4, lst_w + qi, lsd_w + qi, ns, cap, skl[wave], &cnt2, &R2);
+            if (lane == 0) { q_new[qi - (int)blockIdx.x * ICPH_THREADS] = make_float4(q.x, q.y, q.z, R2); n_new[qi - (int)blockIdx.x * ICPH_THREADS] = cnt2; }
         }
-        // the rebuilt lists (stored by this wave) are read by their owner lanes from the next iteration on
+        // every wave's key stores have completed before the flag (wave 0 sets it after the barrier);
+        // the rebuilt lists (same CU) are read by their owner lanes from the next iteration on
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
         if (have && n_new[lane] != -2) {
             const float4 c = q_new[lane];
             x0 = c.x; y0 = c.y; z0 = c.z; R = c.w;
             n = n_new[lane];
             n_new[lane] = -2;
         }
-        __builtin_amdgcn_wave_barrier();
-        icp_put_flag(&done[blockIdx.x], j);
+        if (wave == 0) icp_put_flag(&done[blockIdx.x], j);
     }
 }
 
@@ -871,7 +882,7 @@ hipError_t launch_icp(const float* src0, int ns, float4* lst, float* lsd, int* l
 }
 
 int icp_lists_blocks(int ns) { return (ns + ICP_WAVES - 1) / ICP_WAVES; }
-int icp_iter_blocks(int ns) { return (ns + ICPH_SRC - 1) / ICPH_SRC; }
+int icp_iter_blocks(int ns) { return (ns + ICPH_THREADS - 1) / ICPH_THREADS; }
 
 hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const* g4, const float4* tgt4, int nt, int cap,
                                  float4* lst, float* lsd, int* lcnt, float4* lcen, unsigned long long* best_out,
@@ -890,7 +901,7 @@ hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4
                                  int* qstat) {
     if (ns <= 0 || nt <= 0 || max_iter <= j0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
-    bsk::k_icp_iterations<<<icp_iter_blocks(ns), ICPH_THREADS, 0, s>>>(src0, ns, j0, lst, lsd, lcnt, lcen, cap, icp_views(g4),
+    bsk::k_icp_iterations<<<icp_iter_blocks(ns), ICPH_THREADS * ICPH_WAVES, 0, s>>>(src0, ns, j0, lst, lsd, lcnt, lcen, cap, icp_views(g4),
                                                                       tgt4, nt, max_iter, sy, done, best, qstat);
     return hipGetLastError();
 }
