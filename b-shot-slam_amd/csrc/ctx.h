@@ -245,6 +245,9 @@ struct bshot_ctx {
     int opt_icp_host_delay_ms = 0;  // tests: the host loop sleeps this long before releasing iteration 3
     PinBuf<bsh::IcpOut> p_iout;  // ICP result: composed transform, iteration count, seq (coherent)
     int icp_seq = 0;             // seq of the last ICP call
+    bsh::IcpDevSync* idsy = nullptr;  // ICP host loop: the release relayed in device memory (option icp_relay)
+    unsigned int icp_relay_seq = 0;  // per persistent-kernel launch (a stale word never matches)
+    int opt_icp_relay = 1;       // 1: workgroup 0 alone polls the host's release and relays it
     DBuf<float4> ipos, ilcen;    // ICP loop: current source positions, list centres (xyz) + radii (w)
     DBuf<float> irec;            // ICP loop: the iteration's Umeyama records (7 x ns floats)
     DBuf<bsh::IcpCtl> ictl;      // ICP loop state

@@ -861,8 +861,14 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                 HIPCHK(c->iqstat.ensure(2), "alloc icp stats");
                 HIPCHK(kfill(c->iqstat.p, 0, 2 * sizeof(int), c->stream), "zero icp stats");
             }
+            if (c->opt_icp_relay && !c->idsy) {
+                HIPCHK(hipMalloc(&c->idsy, sizeof(IcpDevSync)), "alloc icp relay");
+                HIPCHK(kfill(c->idsy, 0, sizeof(IcpDevSync), c->stream), "zero icp relay");
+            }
+            IcpDevSync* dsy = c->opt_icp_relay ? c->idsy : nullptr;
             HIPCHK(launch_icp_iterations(d_src0, ns, 1, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilcen.p, ICP_LIST_CAP, g4,
-                                         c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p, c->stream, c->iqstat.p),
+                                         c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p, c->stream, c->iqstat.p, dsy,
+                                         ++c->icp_relay_seq),
                    "icp iterations");
             c->stage_end(sg14);
             auto release = [&](int go) { __atomic_store_n(&sy->go, go, __ATOMIC_RELEASE); };
@@ -902,7 +908,7 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
                        "icp lists (restart)");
                 HIPCHK(launch_icp_iterations(c->p_src2.p, ns, j + 1, c->ilst.p, c->ilsd.p, c->ilcnt.p, c->ilcen.p,
                                              ICP_LIST_CAP, g4, c->itgt.p, nt, max_iter, sy, done1, c->p_ibest.p,
-                                             c->stream),
+                                             c->stream, nullptr, dsy, ++c->icp_relay_seq),
                        "icp iterations (restart)");
                 return BSHOT_OK;
             };
@@ -1069,6 +1075,8 @@ void bshot_destroy(bshot_ctx* c) {
     bsh::velo_free(c->velo);
     c->velo = nullptr;
     c->gout.release(); c->ilst.release(); c->ilsd.release(); c->ilcnt.release(); c->p_iout.release(); c->p_isync.release(); c->p_ibest.release(); c->p_idone.release(); c->p_src2.release(); c->ipos.release(); c->ilcen.release(); c->irec.release(); c->ictl.release(); c->isync.release(); c->itgt3.release(); c->itgt.release(); c->ibest.release(); c->iqstat.release();
+    if (c->idsy) (void)hipFree(c->idsy);
+    c->idsy = nullptr;
     if (trace) std::fprintf(stderr, "destroy step 5\n");
     (void)hipStreamDestroy(c->stream);
     if (trace) std::fprintf(stderr, "destroy step 6\n");
@@ -1344,6 +1352,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "iss_grid") c->opt_iss_grid = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
     else if (k == "iss_xcd_chunk") c->opt_iss_xcd_chunk = value < 0 ? 0 : value;
+    else if (k == "icp_relay") c->opt_icp_relay = value ? 1 : 0;
     else if (k == "pre_fast") c->opt_pre_fast = value ? 1 : 0;
     else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;
     else if (k == "ransac_dev") c->opt_ransac_dev = value ? 1 : 0;

@@ -300,7 +300,8 @@ __global__ void __launch_bounds__(ICPH_THREADS * ICPH_WAVES) ICPH_ATTR k_icp_ite
                                                                  const float4* __restrict__ lcen, int cap, IcpGrids G,
                                                                  const float4* __restrict__ tgt4, int nt, int max_iter,
                                                                  const bsh::IcpSync* sy, int* done,
-                                                                 unsigned long long* best, int* qstat) {
+                                                                 unsigned long long* best, int* qstat,
+                                                                 bsh::IcpDevSync* dsy, unsigned int seq) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical main-stream kernel: issue ahead of side-stream waves
     __shared__ CandLds cl[ICPH_WAVES];
     __shared__ float4 q_queue[ICPH_THREADS];
@@ -329,12 +330,27 @@ __global__ void __launch_bounds__(ICPH_THREADS * ICPH_WAVES) ICPH_ATTR k_icp_ite
     const float* Ld = lsd + (have ? i : 0);
     for (int j = j0; j < max_iter; ++j) {
         if (wave == 0) {
+            // the host's release of iteration j: read from pinned host memory by workgroup 0 (every
+            // workgroup without the relay), which republishes it in device memory for the others --
+            // 32 waves polling host memory made every hand-over slower (r06f: 64 pollers doubled the
+            // ICP phase). Relaxed device-scope stores and loads, ordered by waiting for the stores'
+            // completion before the word: no L2 write-back fence.
+            const bool host_poll = !dsy || blockIdx.x == 0;
             int g = 0;
             if (lane == 0) {
                 const long long t0 = wall_clock64();
                 while (true) {
-                    g = __hip_atomic_load(&sy->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (g < 0 || g >= j) break;
+                    if (host_poll) {
+                        g = __hip_atomic_load(&sy->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (g < 0 || g >= j) break;
+                    } else {
+                        const unsigned long long w = __hip_atomic_load(&dsy->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned int)(w >> 32) == seq) {
+                            const unsigned int lo = (unsigned int)w;
+                            if (lo == 0xFFFFFFFFu) { g = -1; break; }
+                            if ((int)lo - 1 >= j) { g = (int)lo - 1; break; }
+                        }
+                    }
                     if (wall_clock64() - t0 > ICP_WAIT_TICKS) { g = -1; break; }
                     __builtin_amdgcn_s_sleep(2);
                 }
@@ -342,7 +358,21 @@ __global__ void __launch_bounds__(ICPH_THREADS * ICPH_WAVES) ICPH_ATTR k_icp_ite
                 nq = 0;
             }
             g = __shfl(g, 0, 64);
-            if (g >= 0 && lane < 16) T_sh[lane] = __hip_atomic_load(&sy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            float t = 0.f;
+            if (g >= 0 && lane < 16) {
+                t = host_poll ? __hip_atomic_load(&sy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                              : __hip_atomic_load(&dsy->T[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                T_sh[lane] = t;
+            }
+            if (dsy && blockIdx.x == 0) {
+                // republish: the step first, then the word once the step's stores have completed
+                if (g >= 0 && lane < 16) __hip_atomic_store(&dsy->T[lane], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_waitcnt(0);
+                if (lane == 0)
+                    __hip_atomic_store(&dsy->word,
+                                       ((unsigned long long)seq << 32) | (g < 0 ? 0xFFFFFFFFull : (unsigned long long)(g + 1)),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();
         if (go_sh < 0) break;  // every wave of the workgroup
@@ -898,11 +928,11 @@ hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const
 hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4* lst, const float* lsd, const int* lcnt,
                                  const float4* lcen, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
                                  int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s,
-                                 int* qstat) {
+                                 int* qstat, IcpDevSync* dsy, unsigned int seq) {
     if (ns <= 0 || nt <= 0 || max_iter <= j0) return hipSuccess;
     if (cap != ICP_LIST_CAP) return hipErrorInvalidValue;
     bsk::k_icp_iterations<<<icp_iter_blocks(ns), ICPH_THREADS * ICPH_WAVES, 0, s>>>(src0, ns, j0, lst, lsd, lcnt, lcen, cap, icp_views(g4),
-                                                                      tgt4, nt, max_iter, sy, done, best, qstat);
+                                                                      tgt4, nt, max_iter, sy, done, best, qstat, dsy, seq);
     return hipGetLastError();
 }
 

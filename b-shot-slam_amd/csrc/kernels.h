@@ -90,6 +90,14 @@ struct IcpSync {
     int pad0[31];
     float T[16];
 };
+// the release relayed in device memory (option icp_relay): workgroup 0 polls IcpSync in pinned host
+// memory and republishes each release here; the other workgroups poll this word (device scope)
+// instead of host memory. word = call sequence << 32 | (go + 1), low half 0xFFFFFFFF = stop.
+struct IcpDevSync {
+    unsigned long long word;
+    int pad0[30];
+    float T[16];
+};
 int icp_lists_blocks(int ns);
 int icp_iter_blocks(int ns);
 // iteration 0 (a wave per source): keys of src0 into best_out (pinned), the candidate lists (lcen:
@@ -103,7 +111,7 @@ hipError_t launch_icp_lists_host(const float* src0, int ns, const DevGrid* const
 hipError_t launch_icp_iterations(const float* src0, int ns, int j0, const float4* lst, const float* lsd, const int* lcnt,
                                  const float4* lcen, int cap, const DevGrid* const* g4, const float4* tgt4, int nt,
                                  int max_iter, const IcpSync* sy, int* done, unsigned long long* best, hipStream_t s,
-                                 int* qstat = nullptr);
+                                 int* qstat = nullptr, IcpDevSync* dsy = nullptr, unsigned int seq = 0);
 // the loop state of one ICP call (device memory): the last step, the composed transform, PCL's
 // previous MSE, the iteration count and the stop flag every queued kernel checks first
 struct IcpCtl {

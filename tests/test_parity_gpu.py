@@ -236,10 +236,13 @@ def test_match_exact_random_and_ties(ctx):
         np.testing.assert_array_equal(g, r)
 
 
-@pytest.mark.parametrize("device_loop", [0, 1])
-def test_icp_exact(ctx, cloud, sr_ref, device_loop):
+@pytest.mark.parametrize("device_loop,relay", [(0, 1), (0, 0), (1, 1)])
+def test_icp_exact(ctx, cloud, sr_ref, device_loop, relay):
     """A11: ICP (iteration 0 builds candidate lists, later iterations search them) vs the oracle,
-    bit for bit: the host's float Umeyama loop (default) and the device loop (option icp_device)."""
+    bit for bit: the host's float Umeyama loop (default; its releases read by one workgroup and
+    relayed in device memory, or read from host memory by every workgroup: option icp_relay) and the
+    device loop (option icp_device)."""
+    ctx.set_option("icp_relay", relay)
     ridx, rrat = sr_ref
     kidx, _ = orc.select_topk(ridx, rrat, 600)
     tgt = cloud[kidx]
@@ -251,12 +254,14 @@ def test_icp_exact(ctx, cloud, sr_ref, device_loop):
         T, it = ctx.icp(src, tgt)
     finally:
         ctx.set_option("icp_device", 0)
+        ctx.set_option("icp_relay", 1)
     Tr, itr = orc.icp(src, tgt)
     assert it == itr
     np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
 
 
-def test_icp_host_stall_restarts(ctx, cloud, sr_ref):
+@pytest.mark.parametrize("relay", [1, 0])
+def test_icp_host_stall_restarts(ctx, cloud, sr_ref, relay):
     """a host stall longer than the persistent kernel's 1 s wait (the host sleeps 1.3 s
     before releasing iteration 3) makes the kernel exit; the host restarts the iterations from its
     current positions and the result is still the oracle's, bit for bit."""
@@ -268,10 +273,12 @@ def test_icp_host_stall_restarts(ctx, cloud, sr_ref):
     src = src.astype(np.float32)
     w0 = ctx.work()
     ctx.set_option("icp_host_delay_ms", 1300)
+    ctx.set_option("icp_relay", relay)
     try:
         T, it = ctx.icp(src, tgt)
     finally:
         ctx.set_option("icp_host_delay_ms", 0)
+        ctx.set_option("icp_relay", 1)
     w1 = ctx.work()
     Tr, itr = orc.icp(src, tgt)
     assert it == itr and it > 3
