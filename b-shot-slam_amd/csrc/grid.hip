@@ -21,9 +21,16 @@
 #ifndef GRID_SORT_ONESWEEP
 #define GRID_SORT_ONESWEEP 0
 #endif
+#ifndef GRID_SORT_BLOCK_ITEMS
+#define GRID_SORT_BLOCK_ITEMS 0  // 0: rocprim's default block sort (1024 keys); else 256 x this / 256 keys per block
+#endif
 #if GRID_SORT_ONESWEEP
 using LadderSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                     rocprim::default_config, 0>;
+#elif GRID_SORT_BLOCK_ITEMS > 0
+using LadderSortConfig = rocprim::radix_sort_config<rocprim::default_config,
+                                                    rocprim::merge_sort_config<256, 256, GRID_SORT_BLOCK_ITEMS / 256>,
+                                                    rocprim::default_config>;
 #else
 using LadderSortConfig = rocprim::default_config;
 #endif
