@@ -173,7 +173,7 @@ static int cloud_load(bshot_ctx* c, CloudState& s, const float* d_xyz, int n, hi
     HIPCHK(ensure_events(s), "events");
     HIPCHK(s.pts4.ensure(n > 0 ? n : 1), "alloc pts4");
     HIPCHK(s.errw.ensure(2), "alloc err");
-    HIPCHK(s.issovf.ensure((size_t)n + 1), "alloc iss overflow");
+    HIPCHK(s.issovf.ensure(2 * (size_t)n + 2), "alloc iss overflow");  // count + (point, position) pairs
     if (n > 0) {
         const int sg1 = c->stage_begin(BSHOT_STAGE_GRID, st);
         if (c->opt_ladder4) {
@@ -232,7 +232,7 @@ static int cloud_iss(bshot_ctx* c, CloudState& s, hipStream_t st) {
     const int n = s.n;
     HIPCHK(s.third.ensure(n > 0 ? n : 1), "alloc third");
     HIPCHK(s.issflag.ensure(n > 0 ? n : 1), "alloc issflag");
-    HIPCHK(s.issovf.ensure((size_t)n + 1), "alloc iss overflow");
+    HIPCHK(s.issovf.ensure(2 * (size_t)n + 2), "alloc iss overflow");  // count + (point, position) pairs
     HIPCHK(s.issnml.ensure((size_t)32 * (n > 0 ? n : 1)), "alloc iss nms lists");
     HIPCHK(s.issnmc.ensure(n > 0 ? n : 1), "alloc iss nms counts");
     HIPCHK(s.h_flag.ensure(n > 0 ? n : 1), "alloc pinned flags");

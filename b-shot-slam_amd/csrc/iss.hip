@@ -53,7 +53,7 @@ __device__ __forceinline__ int iss_point_of(const GridView& g, int jp) {
 }
 
 // wave/point fallback for the points whose neighbourhood overflowed the lane kernel's list:
-// ovf[0] = count, ovf[1..] = point indices
+// ovf[0] = count, then from ovf + 2 one (point index, list position) pair per overflow point
 // nml != null (nonmax <= salient): a point whose non-max neighbours (a prefix of its sorted list) number
 // at most 32 also gets its NMS list, as the lane kernel's points do (nmc >= 0: k_iss_nms_list
 // decides it; -1 leaves it to the wave NMS)
@@ -79,8 +79,8 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
         npend = 0;
     };
     for (int oi = blockIdx.x * ISS_WAVES + wave; oi < n_ovf; oi += gridDim.x * ISS_WAVES) {
-        const int jp = ovf[1 + oi];  // the point's list position (iss_point_of)
-        const int q = iss_point_of(g, jp);
+        const int2 e = reinterpret_cast<const int2*>(ovf + 2)[oi];  // the point and its list position
+        const int q = e.x, jp = e.y;
         const float4 c = pts4[q];
         double out = 0.0;
         bool pend = false;
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
                         cnm += __popcll(__ballot((unsigned int)(L->list[r] >> 32) < r2nm_bits));
                     if (cnm <= 32) {
                         if (lane < cnm) nml[(size_t)lane * n + jp] = (unsigned int)L->list[lane];
-                        if (lane == 0) nmc[q] = cnm;
+                        if (lane == 0) nmc[jp] = cnm;
                     }
                 }
                 // neighbour offsets in double (neigh - central), rank order
@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
         }
     }
     const bool over = cnt > ISS_LCAP;
-    if (over) ovf[1 + atomicAdd(&ovf[0], 1)] = j;  // third[q] written by the overflow pass
+    if (over) reinterpret_cast<int2*>(ovf + 2)[atomicAdd(&ovf[0], 1)] = make_int2(q, j);  // third[q]: the overflow pass
     const bool work = fin && !over && cnt >= min_nn;
     double out = 0.0;
     // wave-uniform network size: the longest kept list of the wave
@@ -404,9 +404,9 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
 #endif
 #endif
         out = iss_third(sm, g21, g32);
-        nmc[q] = cnm;
+        nmc[j] = cnm;
     }
-    if (live && over) nmc[q] = -1;
+    if (live && over) nmc[j] = -1;
     if (live && !over) third[q] = out;
 }
 
@@ -419,12 +419,12 @@ __global__ void __launch_bounds__(256) k_iss_nms_list(GridView g, int n, int min
     const int jp = blockIdx.x * blockDim.x + threadIdx.x;  // list position
     if (jp >= n) return;
     const int i = iss_point_of(g, jp);
+    const int m = nmc[jp];  // non-max lists and their counts are kept by list position
     const double ti = third[i];
     if (!(ti > 0.0)) {
         flag[i] = 0;
         return;
     }
-    const int m = nmc[i];
     if (m < 0) return;
     bool bigger = false;
     for (int s0 = 0; s0 < m; s0 += 8) {
@@ -451,8 +451,9 @@ __global__ void __launch_bounds__(256) k_iss_nms_wave(GridView g, const float4* 
     const int cnt_pts = all ? n : ovf[0];
     const float r2 = (float)((double)nonmax * (double)nonmax);
     for (int oi = wv; oi < cnt_pts; oi += nw) {
-        const int q = all ? oi : iss_point_of(g, ovf[1 + oi]);
-        if (!all && nmc[q] >= 0) continue;  // decided from its list (k_iss_nms_list)
+        const int2 e = all ? make_int2(oi, oi) : reinterpret_cast<const int2*>(ovf + 2)[oi];
+        const int q = e.x;
+        if (!all && nmc[e.y] >= 0) continue;  // decided from its list (k_iss_nms_list)
         const double tq = third[q];
         const float4 c = pts4[q];
         unsigned char f = 0;

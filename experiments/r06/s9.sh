@@ -8,6 +8,10 @@ T=${1:-r06i}
 L=b-shot-slam_amd/lib
 BSHOT_LIB=$R/$L/ab/libbshot_b4k.so timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "seg_ratio or iss or icp_exact" > $O/${T}_pytest_b4k.log 2>&1
 rc=$?; echo "b4k: $(tail -1 $O/${T}_pytest_b4k.log)"; [ $rc -eq 0 ] || exit $rc
+for V in amd ab/libbshot_hd1 ab/libbshot_hd2; do
+  F=$L/$V.so; [ "$V" = amd ] && F=$L/libbshot_amd.so
+  BSHOT_LIB=$R/$F timeout -k 10 120 python b-shot-slam_amd/tools/describe_bench.py 2>/dev/null | sed "s|^|$V |" || exit 1
+done | tee $O/${T}_describe_diag.txt
 rm -f $O/abm_*
 bash experiments/quick/ab_multi.sh 3 $L/libbshot_amd.so $L/ab/libbshot_b4k.so $L/ab/libbshot_b2k.so | tee $O/${T}_ab_sort.txt || exit 1
 cd /tmp && export TMPDIR=/tmp
