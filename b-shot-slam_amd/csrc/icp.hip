@@ -181,8 +181,12 @@ __device__ __forceinline__ void icp_put_flag(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// waves (sources) per k_icp_lists workgroup: 1. The lists kernel runs on the main stream beside the
+// lookahead's SR, which fills a CU's LDS to 5.8 KB of 160 (24 waves x 6.4 KB): a 4-wave workgroup
+// (10.3 KB) waited for SR workgroups to exit, a 1-wave one (2.6 KB) starts at once -- ICP's
+// iteration-0 wait 0.21 -> 0.06 ms per sweep, 683 / 666 -> 707 / 722 sweeps/s (r06l)
 #ifndef ICP_WAVES
-#define ICP_WAVES 4
+#define ICP_WAVES 1
 #endif
 // per-source Umeyama record of an iteration, SoA rows in rec (row stride icp_rs(ns): 16-B aligned
 // rows): source xyz (the source's current position), its NN target xyz, the NN's d2
@@ -267,17 +271,18 @@ __global__ void __launch_bounds__(64 * ICP_WAVES) k_icp_lists(const float* __res
 // after max_iter - 1 iterations, or when a wait exceeds ICP_WAIT_TICKS; the host then restarts the
 // iterations from the current positions (ctx_icp).
 #define ICPH_THREADS 64
-// helper waves per iteration workgroup: wave 0 owns the workgroup's 64 sources (lane per source) and
-// alone polls the host's release (system-scope loads); a source that leaves its list takes a
-// wave-wide grid search and list rebuild, and on the sweeps where ICP moves far (a gated frame
-// starts from the previous pose) hundreds leave -- the 18 sweeps of 199 with >= 60 such searches
-// waited 0.89 ms for iterations 1.. against 0.07 ms (corr 0.93, profiles/r06e_icp_tail.txt). The
-// workgroup's waves take the queued searches in turn, so a wave's queue is a quarter as long; the
-// helpers wait at the workgroup barrier (no polling, no issue slots). More polling waves instead
-// (fewer sources per wave) made every hand-over slower: 32 -> 128 / 256 polling waves took the
-// whole ICP phase 0.68 -> 2.2 / 3.0 ms (r06f).
+// waves per iteration workgroup: wave 0 owns the workgroup's 64 sources (lane per source) and alone
+// polls the host's release (system-scope loads); a source that leaves its list takes a wave-wide
+// grid search and list rebuild, and on the sweeps where ICP moves far (a gated frame starts from the
+// previous pose) hundreds leave -- the 18 sweeps of 199 with >= 60 such searches waited 0.89 ms for
+// iterations 1.. against 0.07 ms (corr 0.93, profiles/r06e_icp_tail.txt). The workgroup's waves take
+// the queued searches in turn; the helper waits at the workgroup barrier (no polling, no issue
+// slots). 2 waves (7.5 KB of LDS): ICP 0.35-0.36 ms per sweep, 736 / 739 sweeps/s; 1 wave (4.9 KB)
+// 0.36, 707 / 722; 4 waves (12.7 KB, more than SR leaves a CU) 0.49, 716 / 725 (r06l). More polling
+// waves instead (fewer sources per wave) made every hand-over slower: 32 -> 128 / 256 polling waves
+// took the whole ICP phase 0.68 -> 2.2 / 3.0 ms (r06f).
 #ifndef ICPH_WAVES
-#define ICPH_WAVES 4
+#define ICPH_WAVES 2
 #endif
 #define ICP_WAIT_TICKS 100000000ll  // 1 s at the 100 MHz wall clock: a launch that cannot finish exits
 #ifndef ICPH_WPE
