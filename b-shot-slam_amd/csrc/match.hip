@@ -80,7 +80,9 @@ __global__ void __launch_bounds__(HM_THREADS) k_ham_min(HamDir d0, HamDir d1) {
 #define HP_THREADS 256
 #define HP_ROWS 2                          // query rows per thread
 #define HP_TROWS (HP_THREADS * HP_ROWS)    // query rows per workgroup
-#define HP_TILE 128                        // reference rows per LDS tile
+#ifndef HP_TILE
+#define HP_TILE 128  // reference rows per LDS tile
+#endif
 #define HP_SHIFT 23
 
 // wave-wide min of a u32 (DPP: row shifts, then the row broadcasts; the result is in lane 63)
