@@ -512,17 +512,33 @@ __device__ __forceinline__ int ladder_start(const LadderGrids& lg, float qx, flo
     return lg.nsteps - 1;
 }
 
-// sequential float sum of a[0, n) in index order (8 loads in flight, dependent adds)
+// sequential float sum of a[0, n) in index order (a 16-B aligned LDS row). Software-pipelined over
+// two register groups: each group's 8 elements are loaded while the other group's 8 dependent adds
+// run, so the LDS latency hides behind the chain (the plain loop waited for its own loads every 8
+// elements: the ratio phase was a quarter of the kernel's wave time, profiles/r06c_sr_bench.txt). The
+// empty asm with a memory clobber keeps the compiler from sinking a prefetch back to its use.
 __device__ __forceinline__ float seq_sum(const float* a, int n) {
     float acc = 0.f;
-    int r = 0;
-    for (; r + 8 <= n; r += 8) {
-        const float a0 = a[r], a1 = a[r + 1], a2 = a[r + 2], a3 = a[r + 3];
-        const float a4 = a[r + 4], a5 = a[r + 5], a6 = a[r + 6], a7 = a[r + 7];
-        acc = acc + a0; acc = acc + a1; acc = acc + a2; acc = acc + a3;
-        acc = acc + a4; acc = acc + a5; acc = acc + a6; acc = acc + a7;
+    const int n8 = n & ~7;
+    const float4* a4 = reinterpret_cast<const float4*>(a);
+    if (n8 > 0) {
+        float4 a0 = a4[0], a1 = a4[1];
+        for (int r = 0; r < n8; r += 16) {
+            const int nb = (r + 8 < n8 ? r + 8 : r) >> 2;
+            const float4 b0 = a4[nb], b1 = a4[nb + 1];
+            asm volatile("" ::: "memory");
+            acc = acc + a0.x; acc = acc + a0.y; acc = acc + a0.z; acc = acc + a0.w;
+            acc = acc + a1.x; acc = acc + a1.y; acc = acc + a1.z; acc = acc + a1.w;
+            if (r + 8 >= n8) break;
+            const int na = (r + 16 < n8 ? r + 16 : r + 8) >> 2;
+            a0 = a4[na];
+            a1 = a4[na + 1];
+            asm volatile("" ::: "memory");
+            acc = acc + b0.x; acc = acc + b0.y; acc = acc + b0.z; acc = acc + b0.w;
+            acc = acc + b1.x; acc = acc + b1.y; acc = acc + b1.z; acc = acc + b1.w;
+        }
     }
-    for (; r < n; ++r) acc = acc + a[r];
+    for (int r = n8; r < n; ++r) acc = acc + a[r];
     return acc;
 }
 
