@@ -175,6 +175,16 @@ __global__ void __launch_bounds__(1024) k_excl_scan(const int* __restrict__ coun
 // bucket's next slot (a workgroup per keypoint, as k_shot_count). 4-byte entries: the scatter's
 // partial-line writes cost 2.1 x the 8-byte keys' bytes (profiles/r05n_gather_pmc.txt), and the
 // rank kernels recompute d2 from the L2-resident points instead.
+// SG_STAGE > 0 (diagnostic builds): a segment of at most SG_STAGE entries is scattered into LDS
+// and written out whole afterwards, coalesced; a larger one is scattered directly (the entries'
+// positions are the same either way). It cuts the partial-line writes VERDICT r05 #4 measured
+// (config 2: 185.6 -> 126.5 MB per launch at 8192 entries, 82.4 at 16384; config 5: 1380 -> 1233 /
+// 913) and the standalone gather 0.163 -> 0.137 ms, but the 33-65 KB of LDS every workgroup then
+// holds slowed config 5 by 3-4 % and left config 2 even in the pipeline (profiles/r06t_*), so the
+// product scatters directly.
+#ifndef SG_STAGE
+#define SG_STAGE 0
+#endif
 __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, const float* __restrict__ kps, int k, float R,
                                                                 const long long* __restrict__ offs,
                                                                 const unsigned int* __restrict__ bh,
@@ -184,6 +194,9 @@ __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, con
     __shared__ CandLds lds[SG_WAVES];
     __shared__ unsigned int cu[SG_BUCKETS];
     __shared__ int wsum[SG_WAVES];
+#if SG_STAGE > 0
+    __shared__ unsigned int stg[SG_STAGE];
+#endif
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     cand_init(&lds[wave]);
     const float R2 = (float)((double)R * (double)R);
@@ -214,11 +227,22 @@ __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, con
             ur += hv[j];
         }
         __syncthreads();
-        unsigned int* out = seg + offs[q];
-        for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
-            if (v) out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = idx;
-        }, 0, wave, SG_WAVES);
-        __syncthreads();  // cu and wsum are rewritten for the next keypoint
+        const long long o = offs[q];
+        unsigned int* out = seg + o;
+#if SG_STAGE > 0
+        const int n = (int)(offs[q + 1] - o);
+        if (n <= SG_STAGE) {
+            for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
+                if (v) stg[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = idx;
+            }, 0, wave, SG_WAVES);
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += 64 * SG_WAVES) out[i] = stg[i];
+        } else
+#endif
+            for_candidates(g, &lds[wave], kx, ky, kz, R, R2, [&](bool v, float d2, unsigned int idx) {
+                if (v) out[atomicAdd(&cu[sg_bucket(d2, sc)], 1u)] = idx;
+            }, 0, wave, SG_WAVES);
+        __syncthreads();  // cu, wsum and stg are rewritten for the next keypoint
     }
 }
 
