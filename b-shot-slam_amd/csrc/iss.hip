@@ -167,6 +167,9 @@ __global__ void __launch_bounds__(64 * ISS_WAVES) k_iss_scatter(GridView g, cons
 #ifndef ISS_SCAN
 #define ISS_SCAN 4  // points of a cell loaded at once by a lane (8: 108 VGPRs, the same sweeps/s, r05i)
 #endif
+#ifndef ISS_PRUNE
+#define ISS_PRUNE 1  // 0: every cell of the 3 x 3 x 3 cube probed and scanned (A/B)
+#endif
 #ifndef ISS_MERGE32
 #define ISS_MERGE32 1  // 0: the 32-key register network (A/B)
 #endif
@@ -359,6 +362,16 @@ __global__ void __launch_bounds__(ISS_LBLOCK) k_iss_lane(GridView g, const float
                 for (int u = 0; u < 8; ++u) {
                     const int v = b0 + u, iz = z0 + v % nz, r = v / nz, iy = y0 + r % ny, ix = x0 + r / ny;
                     ck[u] = v < ncell ? cell_key(ix, iy, iz) : BS_EMPTY_KEY;
+#if ISS_PRUNE
+                    // a cube cell whose box lies farther than lim from the point holds no in-ball
+                    // point (for_candidates' rule, cand_cell): neither probed nor scanned
+                    const float cl = g.cell, bx0 = (float)ix * cl, by0 = (float)iy * cl, bz0 = (float)iz * cl;
+                    float dx = 0.f, dy = 0.f, dz = 0.f;
+                    if (c.x < bx0) dx = bx0 - c.x; else if (c.x > bx0 + cl) dx = c.x - (bx0 + cl);
+                    if (c.y < by0) dy = by0 - c.y; else if (c.y > by0 + cl) dy = c.y - (by0 + cl);
+                    if (c.z < bz0) dz = bz0 - c.z; else if (c.z > bz0 + cl) dz = c.z - (bz0 + cl);
+                    if (!(dx * dx + dy * dy + dz * dz <= lim * lim)) ck[u] = BS_EMPTY_KEY;
+#endif
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
