@@ -261,6 +261,8 @@ struct bshot_ctx {
     int opt_iss_ovf_blocks = 512;  // grid of the ISS overflow kernel (grid-strides over the device-side count)
     int opt_iss_nms_blocks = 1024;  // grid of the ISS overflow non-max kernel (grid-strides likewise)
     bsh::DevGrid icp_lad[4];  // ICP target grids: nested cells 1000 .. 8000 mm, one sort per ICP call
+    DBuf<int> icp_err;     // the ICP target grids' error word (8: a finite target beyond the key range)
+    PinBuf<int> p_icp_err;  // its copy, read after the ICP call (coherent)
     DBuf<float> itgt3;
     const float* icp_prep_tgt = nullptr;  // device targets whose ICP grids ctx_icp_prepare has queued
     int icp_prep_nt = 0;

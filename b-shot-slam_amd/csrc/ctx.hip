@@ -727,9 +727,20 @@ int ctx_sync_main(bshot_ctx* c) {
 // the ICP targets' nested grids (cells 1000, 2000, 4000, 8000 mm, all hashed) from one
 // nested-key sort of d_tgt; float4 targets in index order -> itgt. A sort-free build by counting
 // (four launches instead of ~13) measured 2-4 % slower end to end (profiles/r05g_ab_*.txt)
+// A finite target beyond the grids' key range (|cell index| >= 2^20 at the 500 mm level: about
+// +-524 km) would be left out of every level; the build flags it in icp_err (value 8), copied to
+// pinned memory behind the build, and ctx_icp fails the call with BSHOT_ECAP instead of matching
+// against a partial target set (non-finite targets are left out, as PCL's kd-tree does).
 static hipError_t icp_grids(bshot_ctx* c, const float* d_tgt, int nt, int min_cap) {
     DevGrid* lad[4] = {&c->icp_lad[0], &c->icp_lad[1], &c->icp_lad[2], &c->icp_lad[3]};
-    return grid_build_ladder(lad, d_tgt, nt, 1000.f, c->itgt.p, c->stream, 0xFu, min_cap);
+    hipError_t e = c->icp_err.ensure(2);
+    if (e != hipSuccess) return e;
+    c->p_icp_err.coherent = true;
+    if ((e = c->p_icp_err.ensure(1)) != hipSuccess) return e;
+    if ((e = grid_build_ladder(lad, d_tgt, nt, 1000.f, c->itgt.p, c->stream, 0xFu, min_cap, nullptr, c->icp_err.p,
+                               nullptr)) != hipSuccess)
+        return e;
+    return kcopy(c->p_icp_err.p, c->icp_err.p, sizeof(int), c->stream);
 }
 
 // the ICP targets' grids queued ahead (right after the map query, while the host runs RANSAC): the
@@ -957,6 +968,10 @@ int ctx_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, in
             release(-1);  // the persistent kernel's waves exit
             HIPCHK(hipStreamSynchronize(c->stream), "sync icp");
         }
+        // the grids' range flag: its copy ran before the ICP kernels whose results were read above
+        if (__atomic_load_n(c->p_icp_err.p, __ATOMIC_ACQUIRE) & 8)
+            return c->fail("ICP target beyond the target grids' coordinate range (about +-524 km from the origin)",
+                           BSHOT_ECAP);
     }
     std::memcpy(T, fin.m, sizeof(float) * 16);
     *iters = it;

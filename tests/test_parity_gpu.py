@@ -347,6 +347,27 @@ def test_icp_grid_edge_cases(big):
         c.close()
 
 
+def test_icp_target_beyond_grid_range_fails_loudly():
+    """A11: a finite target beyond the target grids' key range (2^20 cells of 500 mm, about +-524 km)
+    is in no cell: the ICP call fails with BSHOT_ECAP instead of matching against the other targets;
+    the same context then runs an in-range call normally (the flag is per build)."""
+    rng = np.random.default_rng(12)
+    tgt = (rng.random((2000, 3)) * [40000, 40000, 4000] - [20000, 20000, 2000]).astype(np.float32)
+    src = (tgt[:500] + rng.normal(0, 200, (500, 3))).astype(np.float32)
+    far = tgt.copy()
+    far[33] = (6.0e8, 0.0, 0.0)
+    c = bshot_py.Context(0)
+    try:
+        with pytest.raises(bshot_py.BshotError, match="coordinate range"):
+            c.icp(src, far)
+        T, it = c.icp(src, tgt)
+        Tr, itr = orc.icp(src, tgt)
+        assert it == itr
+        np.testing.assert_array_equal(T.view(np.uint32), Tr.view(np.uint32))
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("seed,frac", [(1, 0.6), (2, 0.3), (3, 0.9), (4, 0.05), (6, 0.15)])
 def test_ransac_dev_matches_host(ctx, seed, frac):
     """A10 with the hypotheses scored on the GPU (bshot_ransac_dev) == host RANSAC == oracle, bit
