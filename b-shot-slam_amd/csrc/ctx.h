@@ -147,6 +147,7 @@ struct bshot_ctx {
     int opt_ladder_front = 1;   // two radius steps r/16, r/(8 sqrt 2) in front of the fine ladder
     int opt_sr_xcd_chunk = 1024;  // SR queries per XCD-local chunk of cell order (0: round-robin queries)
     int opt_sr_blocks = 0;      // SR grid cap (0: one run of queries per wave -- short waves let the main stream in)
+    int opt_gmap_slots0 = 1 << 20;  // GPU map: keypoint slots reserved up front (grown by doubling past them)
     int opt_iss_xcd_chunk = 1024;  // ISS lane kernel: points per XCD-local chunk of cell order (0: blocks in order)
     int opt_sr_run = 4;         // SR cell-order queries per wave pass, each after the first bounded by its predecessor
     int opt_sr_bratio = 200;    // SR bounded pass: grid cell >= radius * 100 / this (percent)

@@ -1367,6 +1367,7 @@ int bshot_set_option(bshot_ctx* c, const char* name, int value) {
     else if (k == "iss_grid") c->opt_iss_grid = value ? 1 : 0;
     else if (k == "iss_ovf_blocks") c->opt_iss_ovf_blocks = value < 0 ? 0 : value;
     else if (k == "iss_xcd_chunk") c->opt_iss_xcd_chunk = value < 0 ? 0 : value;
+    else if (k == "gmap_slots0") c->opt_gmap_slots0 = value < 2 ? 2 : value;
     else if (k == "icp_relay") c->opt_icp_relay = value ? 1 : 0;
     else if (k == "pre_fast") c->opt_pre_fast = value ? 1 : 0;
     else if (k == "iss_nms_blocks") c->opt_iss_nms_blocks = value < 0 ? 0 : value;

@@ -666,9 +666,20 @@ static hipError_t grow_keep(DBuf<T>& b, size_t used, size_t need, hipStream_t s)
     return hipSuccess;
 }
 
+// Up-front room for the map's keypoints (option gmap_slots0, default 2^20: 16 + 44 B each, 60 MB of
+// the GPU's 288 GB) and for the matcher's target descriptors: a grow_keep inside the sweep loop
+// costs a hipMalloc and a sync of the main stream, and a 20-sweep bench region held five of them as
+// the map doubled from 2 Ki slots (BSHOT_GROW_TRACE, profiles/r06ze_grow.txt). Past the reservation
+// the map still grows by doubling (test_gpu_map_modes_vs_oracle runs it from 64 slots).
+#ifndef GM_TARGETS0
+#define GM_TARGETS0 (1 << 18)
+#endif
 static int gmap_init(bshot_ctx* c, GMap& g, hipStream_t st = nullptr) {
     if (!st) st = c->stream;
     if (g.ready) return BSHOT_OK;
+    const size_t s0 = (size_t)c->opt_gmap_slots0;
+    HIPCHK(grow_keep(g.kpos, 0, s0, st), "gmap slots");
+    HIPCHK(grow_keep(g.kdesc, 0, 11 * s0, st), "gmap slots");
     g.tsize = 1u << 16;
     HIPCHK(g.tkey.ensure(g.tsize), "gmap table");
     HIPCHK(g.tval.ensure(g.tsize), "gmap table");
@@ -1022,9 +1033,11 @@ int gmap_query(bshot_ctx* c, const float pos[3], float range, const float* ref_k
     const int nb = mtot + kref;
     // targets: positions in c->gtgt (float3), descriptors in c->ma after the na source rows
     HIPCHK(c->gtgt.ensure(3 * (size_t)(nb > 0 ? nb : 1)), "alloc targets");
-    if (c->ma.cap < 11 * ((size_t)na + nb)) {
+    // at least GM_TARGETS0 rows from the first sweep on (the targets grow with the map)
+    const size_t ma_need = 11 * std::max((size_t)na + nb, (size_t)GM_TARGETS0);
+    if (c->ma.cap < ma_need) {
         // keep the source rows already staged at the front
-        HIPCHK(grow_keep(c->ma, 11 * (size_t)na, 11 * ((size_t)na + nb), c->stream), "alloc descriptors");
+        HIPCHK(grow_keep(c->ma, 11 * (size_t)na, ma_need, c->stream), "alloc descriptors");
     }
     int base = 0;
     for (GMap* m : maps) {
@@ -1088,7 +1101,8 @@ int gmap_match(bshot_ctx* c, const unsigned int* a, int na, const float pos[3], 
                std::vector<float>& tgt, int32_t* left_nn, std::vector<int32_t>& right_nn, int32_t* corr_q,
                int32_t* corr_m, int* n_corr) {
     *n_corr = 0;
-    HIPCHK(grow_keep(c->ma, 0, 11 * (size_t)(na > 0 ? na : 1), c->stream), "alloc descriptors");
+    HIPCHK(grow_keep(c->ma, 0, 11 * std::max((size_t)(na > 0 ? na : 1), (size_t)GM_TARGETS0), c->stream),
+           "alloc descriptors");
     GMap& g0 = own_map(c);
     int rc = gmap_init(c, g0);
     if (rc) return rc;

@@ -19,11 +19,15 @@ def _u(a):
     return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 0])
-def test_gpu_map_modes_vs_oracle(mode):
+@pytest.mark.parametrize("mode,slots0", [(1, None), (2, None), (0, None), (1, 64)])
+def test_gpu_map_modes_vs_oracle(mode, slots0):
+    """slots0: the map's up-front slot reservation (option gmap_slots0, default 2^20); 64 makes the
+    map grow by doubling, its contents kept, over the sequence's inserts."""
     frames = [bshot_py.synth_sweep(f)[0][::2].copy() for f in range(8)]
     od = bshot_py.Odometry(0, bshot_py.default_params(num_keypoints=800))
     od.set_option("gpu_map", mode)
+    if slots0 is not None:
+        od.set_option("gmap_slots0", slots0)
     oo = orc.Odometry(orc.params(num_keypoints=800, map_canonical=1 if mode == 2 else 0))
     try:
         for f, xyz in enumerate(frames):
