@@ -526,11 +526,12 @@ int ctx_describe_on(bshot_ctx* c, CloudState& S, hipStream_t st, int k) {
     if (dev_plan) {
         // the whole describe queued without a host round trip: the plan (segment offsets, chunk
         // bases, LPT order) is computed on the device against capacities sized from the largest
-        // neighbourhood total seen so far (+25%); an overflow (errw bit 16) makes the caller
+        // neighbourhood total seen so far (the margin below); an overflow (errw bit 16) makes the caller
         // re-run this describe with the host-side plan
-        // +50%: a sequence's neighbourhood totals drift by tens of percent, and an overflow costs a
-        // second describe (re-planned on the host)
-        const long long seg_cap = c->seg_hint + c->seg_hint / 2 + 262144;
+        // 2 x: a sequence's neighbourhood totals drift by tens of percent, and an overflow costs a
+        // second describe re-planned on the host (+50% still overflowed once in a 200-sweep bench
+        // region, profiles/r06zh_grow200.txt); 4-byte entries, so the margin is tens of MB of HBM
+        const long long seg_cap = 2 * c->seg_hint + 1048576;
         const int chunk_cap = (int)(seg_cap / 64) + k + 1;
         HIPCHK(c->seg.ensure((size_t)seg_cap), "alloc seg");
         HIPCHK(c->segtmp.ensure((size_t)seg_cap), "alloc segtmp");
