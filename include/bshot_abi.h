@@ -120,7 +120,10 @@ int bshot_ransac_scores(bshot_ctx* c, const float* cs, const float* ct, int nidx
                         double thresh, int32_t* cnt);
 
 /* ---- A11: point-to-point ICP (PCL IterativeClosestPoint defaults, src/lidar_odometry.cpp:291-297).
- *      src is already transformed by the initial guess; T_out = ICP final transformation. ---- */
+ *      src is already transformed by the initial guess; T_out = ICP final transformation.
+ *      A finite target beyond the target grids' key range (2^20 cells of 500 mm: about +-524 km from
+ *      the origin on any axis) fails the call with BSHOT_ECAP; non-finite targets are left out, as
+ *      PCL's kd-tree does. ---- */
 int bshot_icp(bshot_ctx* c, const float* src, int ns, const float* tgt, int nt, int max_iter, float* T_out,
               int* iters);
 
