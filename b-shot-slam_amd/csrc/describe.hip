@@ -255,16 +255,22 @@ __global__ void __launch_bounds__(64 * SG_WAVES) k_shot_gather_b(GridView g, con
 // from there; a larger one is restaged (<= SR_STAGE keys) or ranked from HBM.
 #define SR_STAGE 256
 #define SR_WPRE 32
-__global__ void __launch_bounds__(256) k_shot_rank(int k, float R, const float4* __restrict__ pts4,
+// SRK_WAVES waves per workgroup (4). 1-wave workgroups (2 KB of LDS, fitting beside SR's
+// workgroups as the ICP kernels' do) measured slower: their many small workgroups slowed the main
+// stream's matching 0.25 -> 0.31 ms per sweep (profiles/r06zl_ab*.txt)
+#ifndef SRK_WAVES
+#define SRK_WAVES 4
+#endif
+__global__ void __launch_bounds__(64 * SRK_WAVES) k_shot_rank(int k, float R, const float4* __restrict__ pts4,
                                                    const float* __restrict__ kps, const long long* __restrict__ offs,
                                                    const int* __restrict__ cb, const int* __restrict__ owner,
                                                    const unsigned int* __restrict__ bstart,
                                                    const unsigned int* __restrict__ seg,
                                                    unsigned int* __restrict__ out, const int4* __restrict__ cinfo) {
-    __shared__ unsigned long long stage[4][SR_STAGE];
+    __shared__ unsigned long long stage[SRK_WAVES][SR_STAGE];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     // grid-stride over chunks: a capped grid (Describe2Args::max_blocks) instead of a block per 4 chunks
-    for (int c = blockIdx.x * 4 + wave; c < cb[k]; c += gridDim.x * 4) [&]() {
+    for (int c = blockIdx.x * SRK_WAVES + wave; c < cb[k]; c += gridDim.x * SRK_WAVES) [&]() {
         int q, n, c0;
         long long o;
         if (cinfo) {
@@ -511,9 +517,11 @@ hipError_t launch_shot_rank(int k, int n_chunks, float R, const float4* pts4, co
                             const int* cb, const int* owner, const unsigned int* bstart, const unsigned int* seg,
                             unsigned int* out, hipStream_t s, const int4* cinfo, int max_blocks) {
     if (k <= 0 || n_chunks <= 0) return hipSuccess;
-    int blocks = (n_chunks + 3) / 4;
-    if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    bsk::k_shot_rank<<<blocks, 256, 0, s>>>(k, R, pts4, kps, offs, cb, owner, bstart, seg, out, cinfo);
+    int blocks = (n_chunks + SRK_WAVES - 1) / SRK_WAVES;
+    // max_blocks caps the grid in 4-wave units (the chunk kernels' convention): the same waves in flight
+    const int cap = max_blocks > 0 ? max_blocks * 4 / SRK_WAVES : 0;
+    if (cap > 0 && blocks > cap) blocks = cap;
+    bsk::k_shot_rank<<<blocks, 64 * SRK_WAVES, 0, s>>>(k, R, pts4, kps, offs, cb, owner, bstart, seg, out, cinfo);
     return hipGetLastError();
 }
 

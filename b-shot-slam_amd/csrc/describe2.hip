@@ -211,7 +211,9 @@ __device__ __forceinline__ int lrf_eig_of_sums(const double* tot, long long vali
 // 64 B together), lane 7 the valid counts (integers); lane 0 then runs the Jacobi solver.
 // nmax > 0: the same wave first writes the keypoint's normal from the head of its sorted segment
 // (segment_normal; normal_radius == shot_radius), which the histogram kernel reads.
-#define LE_WAVES 4
+#ifndef LE_WAVES
+#define LE_WAVES 4  // 2 x the keypoints per workgroup (even: the LRF sums; odd: the normal)
+#endif
 __global__ void __launch_bounds__(64 * LE_WAVES) k_lrf_eig(int k, const int* __restrict__ cb,
                                                            const double* __restrict__ csum, double* __restrict__ eig,
                                                            int* __restrict__ okf, const float4* __restrict__ pts4,
